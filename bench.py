@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""bench.py -- Mpixels/s encoded on MI355X (BASELINE.json metric).
+
+One step = the whole encode path (colour -> DCT -> quant -> zigzag ->
+histograms -> optimized Huffman tables -> bit pack -> JFIF with stuffing) over
+one batch of synthetic frames already resident in HBM.  Default workload is
+SURVEY §8(d) config 3: 256 frames of 3840x2160 per GPU (weak scaling: each
+rank encodes its own 256 frames; frames are independent, so there is no
+data-path collective -- DESIGN.md §Multi-GPU).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Rank 0 prints one JSON line (metric, value, roofline, cpu_baseline, ...).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(REPO, "jpeg-encoder-decoder_amd"), os.path.join(REPO, "tests"),
+          os.path.join(REPO, "oracle")):
+    sys.path.insert(0, p)
+
+import mijpeg  # noqa: E402
+import recipes  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
+K1_BYTES_PER_PX = 6.0      # 3 B BGR read + 1.5 int16 coefficients written
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=256)
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--quality", type=int, default=50)
+    ap.add_argument("--distinct", type=int, default=16,
+                    help="distinct synthetic frames cycled through the batch")
+    ap.add_argument("--mode", choices=["encode", "dct"], default="encode",
+                    help="dct = K1 only (used for rocprof roofline runs)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="bound on the CPU-baseline sample (rank 0, N=1)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify", type=int, default=2,
+                    help="frames re-checked against the oracle after timing")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+        return world, rank, local, dist, torch
+    return 1, 0, 0, None, None
+
+
+def make_frames(args, rank):
+    """Distinct config-3 frames (recipe in tests/recipes.py), rank-offset so
+    ranks encode different content."""
+    out = []
+    for i in range(args.distinct):
+        f = rank * args.distinct + i
+        if (args.width, args.height) == (3840, 2160):
+            out.append(recipes.config3_frame(f))
+        else:
+            out.append(recipes.config3_frame(f, args.height, args.width)
+                       if args.width <= 3840 and args.height <= 2160
+                       else recipes.config4_frame(f, args.height, args.width))
+    return out
+
+
+def cpu_baseline(frames, seconds):
+    """The reference encoder.c itself (oracle/_ref, compiled from the
+    reference sources) when present, else the C restatement; 1 thread."""
+    import oracle as O
+    use_ref = O.ref_available()
+    enc = (lambda f: O.ref_stages(f)[4]) if use_ref else (lambda f: O.cref_encode(f))
+    n_px, n, t0 = 0, 0, time.perf_counter()
+    while True:
+        f = frames[n % len(frames)]
+        enc(f)
+        n += 1
+        n_px += f.shape[0] * f.shape[1]
+        el = time.perf_counter() - t0
+        if el >= seconds and n >= 2:
+            break
+    import platform
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    h, w = frames[0].shape[:2]
+    return {"value": round(n_px / el / 1e6, 3), "unit": "Mpixels/s", "cores": 1,
+            "kind": "reference" if use_ref else "port",
+            "sample": f"{n} frames of {w}x{h} (config-3 recipe), {el:.1f} s, 1 thread, "
+                      f"{'reference main/encoder.c via oracle/_ref' if use_ref else 'oracle/cpu_ref.c'}"
+                      f", output to memory, on {cpu}"}
+
+
+def main():
+    args = parse()
+    world, rank, local, dist, torch = dist_setup(args)
+    W, H, F = args.width, args.height, args.frames
+    frames = make_frames(args, rank)
+    batch = mijpeg.Batch(W, H, F, args.quality, device=local)
+    for i in range(F):
+        batch.upload(frames[i % len(frames)], first=i)
+    run = batch.encode if args.mode == "encode" else batch.dct
+
+    for _ in range(args.warmup):
+        run(F)
+    batch.sync()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    batch.set_timing(True)
+    barrier()
+    batch.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run(F)
+    batch.sync()
+    el = time.perf_counter() - t0
+    barrier()
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    hist = batch.stage_history(args.steps)
+    k1_ms = float(np.mean([h["k1_colour_dct_quant"] for h in hist]))
+    stage_avg = {k: round(float(np.mean([h[k] for h in hist])), 4) for k in mijpeg.Batch.STAGES}
+    if args.mode == "dct":
+        stage_avg = {"k1_colour_dct_quant": stage_avg["k1_colour_dct_quant"]}
+
+    # correctness spot check after timing (not timed): frames vs the oracle
+    verified = 0
+    if args.verify and args.mode == "encode":
+        import oracle as O
+        for i in range(min(args.verify, F)):
+            if batch.output(i) != O.cref_encode(frames[i % len(frames)], args.quality):
+                raise SystemExit(f"bench: frame {i} differs from the oracle")
+            verified += 1
+
+    px_step = W * H * F
+    value = world * px_step * args.steps / el / 1e6
+    k1_gbs = K1_BYTES_PER_PX * px_step / (k1_ms * 1e-3) / 1e9
+    res = {
+        "metric": "Mpixels/s encoded (device-resident BGR888 -> JFIF bytes)",
+        "value": round(value, 1),
+        "unit": "Mpixels/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int8",
+        "data": f"synthetic: SURVEY §8(d) config-3 recipe, {args.distinct} distinct frames "
+                f"cycled over the batch",
+        "config": {"workload": f"config 3: {F} x {W}x{H} BGR888 frames per GPU, 4:2:0, "
+                               f"Q={args.quality}, one independent JFIF per frame",
+                   "frames_per_gpu": F, "width": W, "height": H, "quality": args.quality,
+                   "mode": args.mode, "parallelism": f"frame-parallel x{world}"},
+        "roofline": {"bound": "hbm", "kernel": "k_mcu_dct (K1: colour+DCT+quant+zigzag)",
+                     "achieved": round(k1_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(k1_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                     "k1_ms_per_launch": round(k1_ms, 4),
+                     "algorithmic_bytes_per_launch": int(K1_BYTES_PER_PX * px_step)},
+        "stages_ms": stage_avg,
+        "verified_frames": verified,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(frames[:4], args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    batch.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

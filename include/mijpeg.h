@@ -1,0 +1,152 @@
+/*
+ * mijpeg.h -- C ABI of the MI355X-native (gfx950) JPEG block-encode path.
+ *
+ * Drop-in replacement for the reference's encoder
+ * (MattiaDallaCosta/JPEG-encoder-decoder include/encoder.h:10-12,
+ * include/structs.h:5-18): a C host that includes this header instead of
+ * encoder.h and links libmijpeg.so gets the same three entry points with the
+ * same signatures, argument meaning, buffer ownership and output bytes; the
+ * work runs as HIP kernels on the GPU.  See INTEGRATION.md.
+ *
+ * Plain C types only: no HIP/torch types cross this boundary.
+ */
+#ifndef MIJPEG_H
+#define MIJPEG_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- types: layout-identical to the reference --------------------------- */
+
+/* include/structs.h:5-13 (ISO/IEC 10918-1 K.2 table state). */
+typedef struct __huff_code {
+    int sym_freq[257];
+    int code_len[257];
+    int next[257];
+    int code_len_freq[32];
+    int sym_sorted[256];
+    int sym_code_len[256];
+    int sym_code[256];
+} huff_code;
+
+/* include/structs.h:15-18: a sub-rectangle of the input frame; w and h must
+ * be multiples of 16 (the reference silently produced garbage otherwise,
+ * this library rejects them, see mij_last_error). */
+typedef struct {
+    int x, y;
+    int w, h;
+} area_t;
+
+/* ---- drop-in entry points ------------------------------------------------ */
+
+/* Replaces encoder.h:10 / encoder.c:158-178.  `in` is a BGR888 frame whose
+ * row stride is the reference's compile-time WIDTH (define.h:3, 320 px) or
+ * the value set with mij_set_input_stride().  Writes the quantized, zigzagged
+ * coefficients with DC differences into Y[w*h], Cb[w*h/4], Cr[w*h/4] (block
+ * raster order per component). */
+void rgb_to_dct(uint8_t *in, int16_t *Y, int16_t *Cb, int16_t *Cr, area_t dims);
+
+/* Replaces encoder.h:11 / encoder.c:360-381: fills the four optimized
+ * Huffman tables (Luma[0]=DC, Luma[1]=AC, Chroma[0]=DC, Chroma[1]=AC);
+ * every field ends in the state the reference leaves it in. */
+void init_huffman(int16_t *Y, int16_t *Cb, int16_t *Cr, area_t dims,
+                  huff_code Luma[2], huff_code Chroma[2]);
+
+/* Replaces encoder.h:12 / encoder.c:549-644: writes the JFIF stream to `f`
+ * (may be NULL here, unlike the reference) and to jpg[], returns its size
+ * (0 on error).  jpg must hold mij_max_jpg_bytes(w, h) bytes to be safe. */
+size_t write_jpg(FILE *f, uint8_t *jpg, int16_t *Y, int16_t *Cb, int16_t *Cr,
+                 area_t dims, huff_code Luma[2], huff_code Chroma[2]);
+
+/* ---- extensions ----------------------------------------------------------- */
+
+/* Runtime replacement for define.h:3 WIDTH (input row stride in pixels used
+ * by rgb_to_dct).  Default 320.  Returns 0 or an error code. */
+int mij_set_input_stride(int stride_px);
+
+/* Quality factor for the drop-in calls, scaled like utils/original.c:504-509.
+ * Default 50 == the reference's fixed tables (encoder.c:18-36). */
+int mij_set_quality(int quality);
+
+/* Error reporting (the reference has none: encoder.c returns void). */
+enum {
+    MIJ_OK = 0,
+    MIJ_EINVAL = 1,     /* dims not multiples of 16, bad stride/quality, ... */
+    MIJ_ENODEV = 2,     /* no usable HIP device / runtime */
+    MIJ_EHIP = 3,       /* a HIP runtime call failed */
+    MIJ_ENOSPC = 4,     /* output capacity too small */
+    MIJ_ETABLE = 5      /* Huffman construction outside the reference's
+                           defined behaviour (code length >= 32 etc.) */
+};
+int mij_last_error(void);
+const char *mij_strerror(int code);
+
+/* Worst-case size of an encoded w x h frame (all 63 AC coefficients coded at
+ * 27 bits, every byte stuffed). */
+size_t mij_max_jpg_bytes(int w, int h);
+
+/* Whole path host->host (rgb_to_dct -> init_huffman -> write_jpg without the
+ * host round trips of the three-call split).  `bgr` + stride_px describe the
+ * frame, dims the region.  Returns MIJ_OK and the size in *out_len. */
+int mij_encode(const uint8_t *bgr, int stride_px, area_t dims, int quality,
+               uint8_t *out, size_t cap, size_t *out_len);
+
+/* ---- device-resident batch pipeline (throughput path) ---------------------
+ * A batch object owns the device buffers for up to max_frames frames of one
+ * geometry; frames are independent (own tables, own JFIF stream).  All work
+ * is queued on the batch's HIP stream; outputs stay in HBM until fetched. */
+typedef struct mij_batch mij_batch;
+
+mij_batch *mij_batch_create(int device, int width, int height, int max_frames,
+                            int quality);
+void mij_batch_destroy(mij_batch *b);
+/* packed BGR888 frames (width*height*3 bytes each) from host memory into
+ * batch slots first .. first+nframes-1 */
+int mij_batch_upload(mij_batch *b, const uint8_t *bgr, int first, int nframes);
+/* or point the batch at frames already in device memory (not owned):
+ * frame i starts at d_bgr + i*frame_stride, rows pitch bytes apart
+ * (pointer and pitch 4-byte aligned) */
+int mij_batch_set_input(mij_batch *b, const void *d_bgr, long long frame_stride,
+                        int pitch);
+int mij_batch_encode(mij_batch *b, int nframes);     /* full path, async */
+int mij_batch_dct(mij_batch *b, int nframes);        /* K1 only, async */
+int mij_batch_sync(mij_batch *b);
+int mij_batch_output(mij_batch *b, int frame, uint8_t *dst, size_t cap,
+                     size_t *len);
+int mij_batch_lengths(mij_batch *b, size_t *lens, int nframes);
+/* quantized zigzag coefficient planes of a frame; diffed != 0 applies the DC
+ * differencing of encoder.c:168-177 (as rgb_to_dct returns them) */
+int mij_batch_coefs(mij_batch *b, int frame, int16_t *Y, int16_t *Cb,
+                    int16_t *Cr, int diffed);
+int mij_batch_tables(mij_batch *b, int frame, huff_code out[4]);
+/* timing: when enabled, HIP events bracket each stage of the next encode;
+ * mij_batch_stage_ms returns up to n stage durations (ms) of the last one:
+ * [0]=K1 colour+DCT+quant, [1]=stats, [2]=tables, [3]=bits, [4]=scan,
+ * [5]=pack, [6]=emit, [7]=whole encode */
+int mij_batch_set_timing(mij_batch *b, int on);
+int mij_batch_stage_ms(mij_batch *b, float *ms, int n);
+/* the same for each of the last `steps` encodes (<= 64) issued while timing
+ * was on, oldest first: ms[step*8 + stage]; returns the count filled */
+int mij_batch_stage_history(mij_batch *b, float *ms, int steps);
+/* coefficients recomputed in FP64 since creation (hazard replays) */
+unsigned long long mij_batch_replays(mij_batch *b);
+/* the batch's hipStream_t, as an opaque pointer */
+void *mij_batch_stream(mij_batch *b);
+
+/* ---- diagnostics used by the test-suite -----------------------------------*/
+/* 16x16x64 i8 MFMA layout probe: A, B are 64 lanes x 16 int8, D 64 x 4 int32 */
+int mij_probe_mfma(const int8_t *A, const int8_t *B, int32_t *D);
+/* colour-exception bitmaps as built on the device: 3 x 2048 words */
+int mij_colour_lut(uint32_t *out);
+/* name of the code object target the library was built for ("gfx950") */
+const char *mij_build_target(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MIJPEG_H */

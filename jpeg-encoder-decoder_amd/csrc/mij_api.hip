@@ -1,0 +1,738 @@
+// mij_api.hip -- host runtime and C ABI of libmijpeg.so (include/mijpeg.h).
+//
+// The drop-in entry points rgb_to_dct / init_huffman / write_jpg keep the
+// reference's signatures (include/encoder.h:10-12) and run every stage as a
+// HIP kernel (mij_kernels.hip).  The batch API keeps frames, coefficients and
+// bitstreams resident in HBM and is what bench.py measures.
+#include <math.h>
+#include <stdarg.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+#include "mij_internal.h"
+#include "mijpeg.h"
+
+namespace mij {
+// launch wrappers (mij_kernels.hip)
+int k1_grid(int device, long long ntiles);
+hipError_t launch_colour_lut(uint32_t *lut, hipStream_t s);
+hipError_t launch_k1(const K1Args &a, int grid, hipStream_t s);
+hipError_t launch_dc_diff(int16_t *coef, const int16_t *dc, const Geom &g, int nframes,
+                          hipStream_t s);
+hipError_t launch_stats(const EntArgs &a, hipStream_t s);
+hipError_t launch_tables(const EntArgs &a, hipStream_t s);
+hipError_t launch_ehuf_struct(const HuffCode *hc, uint32_t *ehuf, hipStream_t s);
+hipError_t launch_bits(const EntArgs &a, hipStream_t s);
+hipError_t launch_scan(const EntArgs &a, hipStream_t s);
+hipError_t launch_pack(const EntArgs &a, hipStream_t s);
+hipError_t launch_emit(const EntArgs &a, hipStream_t s);
+hipError_t launch_mfma_probe(const int4 *A, const int4 *B, int4 *D, hipStream_t s);
+}  // namespace mij
+
+using namespace mij;
+
+// ---------------------------------------------------------------------------
+// error state
+// ---------------------------------------------------------------------------
+static thread_local int g_err = MIJ_OK;
+
+static int fail(int code, const char *fmt, ...) {
+  g_err = code;
+  va_list ap;
+  va_start(ap, fmt);
+  fprintf(stderr, "mijpeg: ");
+  vfprintf(stderr, fmt, ap);
+  fprintf(stderr, "\n");
+  va_end(ap);
+  return code;
+}
+
+#define HIP_TRY(x)                                                          \
+  do {                                                                      \
+    hipError_t e_ = (x);                                                    \
+    if (e_ != hipSuccess)                                                   \
+      return fail(MIJ_EHIP, "%s failed: %s", #x, hipGetErrorString(e_));    \
+  } while (0)
+
+extern "C" int mij_last_error(void) { return g_err; }
+
+extern "C" const char *mij_strerror(int code) {
+  switch (code) {
+    case MIJ_OK: return "ok";
+    case MIJ_EINVAL: return "invalid argument";
+    case MIJ_ENODEV: return "no usable HIP device";
+    case MIJ_EHIP: return "HIP runtime error";
+    case MIJ_ENOSPC: return "output buffer too small";
+    case MIJ_ETABLE: return "Huffman table outside the reference's defined behaviour";
+  }
+  return "unknown error";
+}
+
+extern "C" const char *mij_build_target(void) { return "gfx950"; }
+
+// ---------------------------------------------------------------------------
+// geometry and constant tables
+// ---------------------------------------------------------------------------
+static const int k_luma_q[64] = {  // encoder.c:18-26
+    16, 11, 10, 16, 24,  40,  51,  61,  12, 12, 14, 19, 26,  58,  60,  55,
+    14, 13, 16, 24, 40,  57,  69,  56,  14, 17, 22, 29, 51,  87,  80,  62,
+    18, 22, 37, 56, 68,  109, 103, 77,  24, 35, 55, 64, 81,  104, 113, 92,
+    49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99};
+static const int k_chroma_q[64] = {  // encoder.c:28-36
+    17, 18, 24, 47, 99, 99, 99, 99, 18, 21, 26, 66, 99, 99, 99, 99,
+    24, 26, 56, 99, 99, 99, 99, 99, 47, 66, 99, 99, 99, 99, 99, 99,
+    99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99,
+    99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99};
+static const int k_zz[64] = {  // encoder.c:38-46
+    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+    12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+    35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+    58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+static long long round_up(long long v, long long m) { return (v + m - 1) / m * m; }
+
+static bool valid_dims(int w, int h) { return w > 0 && h > 0 && w % 16 == 0 && h % 16 == 0; }
+
+static Geom make_geom(int w, int h) {
+  Geom g;
+  memset(&g, 0, sizeof(g));
+  g.w = w;
+  g.h = h;
+  g.nY = w * h / 64;
+  g.nC = w * h / 256;
+  g.nblk = g.nY + 2 * g.nC;
+  g.tiles_x = (w + TILE_W - 1) / TILE_W;
+  g.tiles_per_frame = g.tiles_x * (h / TILE_H);
+  g.cy = (g.nY + CHUNK - 1) / CHUNK;
+  g.cc = (g.nC + CHUNK - 1) / CHUNK;
+  g.cpf = g.cy + 2 * g.cc;
+  g.coef_fs = (long long)g.nblk * 64;
+  g.raw_words[0] = round_up((long long)g.nY * MAX_BLOCK_BITS / 32 + 16, 64);
+  g.raw_words[1] = round_up((long long)g.nC * MAX_BLOCK_BITS / 32 + 16, 64);
+  g.raw_words[2] = g.raw_words[1];
+  g.raw_fs = g.raw_words[0] + g.raw_words[1] + g.raw_words[2];
+  g.out_cap = round_up((long long)g.nblk * 434 + 4096, 256);
+  return g;
+}
+
+extern "C" size_t mij_max_jpg_bytes(int w, int h) {
+  if (!valid_dims(w, h)) return 0;
+  return (size_t)make_geom(w, h).out_cap;
+}
+
+// original.c:504-509
+static void quality_tables(int quality, int lq[64], int cq[64]) {
+  for (int i = 0; i < 64; i++) {
+    double l = (100 - quality) / 50.0 * k_luma_q[i];
+    double c = (100 - quality) / 50.0 * k_chroma_q[i];
+    l = l < 1 ? 1 : (l > 255 ? 255 : l);
+    c = c < 1 ? 1 : (c > 255 ? 255 : c);
+    lq[i] = (int)l;
+    cq[i] = (int)c;
+  }
+}
+
+// Host-built constant tables (A-operand digits, quantizer factors/bounds,
+// cosines); the colour-exception bitmaps are built on the device.
+static void fill_tables(int quality, Tables *t) {
+  memset(t, 0, sizeof(*t));
+  for (int i = 0; i < 64; i++)  // utils/lookup.c:10 == encoder.c:8-16
+    t->cosd[i] = cos((double)(2 * (i / 8) + 1) * (i % 8) * M_PI / 16);
+  int q[2][64];
+  quality_tables(quality, q[0], q[1]);
+  for (int c = 0; c < 2; c++)
+    for (int z = 0; z < 64; z++) {
+      const int qz = q[c][k_zz[z]];
+      t->qint[c][z] = qz;
+      t->dqt[c][z] = qz;
+      t->qfac[c][z] = (float)(1.0 / (2097152.0 * qz));
+      // |N - 2^19*sum(K'X)| <= 0.5*sum|X| <= 4096, float(N) <= 64 more;
+      // t rounding <= 3 * 2^-24 * 1024; 25% margin (DESIGN.md §K1 exactness)
+      t->qtau[c][z] = (float)(1.25 * (4160.0 / (2097152.0 * qz) + 2.0e-4));
+    }
+  // A fragments of v_mfma_i32_16x16x64_i8: lane l holds row (l & 15) and the
+  // 16 k-values 16*(l>>4) .. +15.  Row r of M-tile m is zigzag coefficient
+  // z = 16*(r>>2) + 4m + (r&3); k = pixel index y*8+x of the block.
+  for (int m = 0; m < 4; m++)
+    for (int lane = 0; lane < 64; lane++) {
+      const int row = lane & 15, kg = lane >> 4;
+      const int z = 16 * (row >> 2) + 4 * m + (row & 3);
+      const int rz = k_zz[z], v = rz >> 3, u = rz & 7;
+      int8_t dig[3][16];
+      for (int j = 0; j < 16; j++) {
+        const int p = 16 * kg + j, y = p >> 3, x = p & 7;
+        long long W;
+        if (z == 0) {
+          dig[0][j] = 0;
+          dig[1][j] = 0;
+          dig[2][j] = 1;  // DC row: exact pixel sum in digit 0
+          continue;
+        }
+        double k = t->cosd[y * 8 + v] * t->cosd[x * 8 + u];
+        if (u == 0) k *= M_SQRT1_2;
+        if (v == 0) k *= M_SQRT1_2;
+        W = llround(k * 524288.0);  // 2^19
+        const long long d0 = ((W + 64) & 127) - 64;
+        const long long w1 = (W - d0) >> 7;
+        const long long d1 = ((w1 + 64) & 127) - 64;
+        const long long d2 = (w1 - d1) >> 7;
+        dig[0][j] = (int8_t)d2;
+        dig[1][j] = (int8_t)d1;
+        dig[2][j] = (int8_t)d0;
+      }
+      for (int d = 0; d < 3; d++) memcpy(&t->mfma_a[(m * 3 + d) * 64 + lane], dig[d], 16);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// batch pipeline
+// ---------------------------------------------------------------------------
+struct mij_batch {
+  int dev = 0;
+  hipStream_t stream = nullptr;
+  Geom g;
+  int cap = 0, quality = 50;
+  Tables *d_tab = nullptr;
+  uint8_t *d_in = nullptr;
+  bool own_in = false;
+  long long in_fs = 0;
+  int pitch = 0;
+  int16_t *d_coef = nullptr, *d_dc = nullptr;
+  uint32_t *d_hist = nullptr, *d_ehuf = nullptr, *d_bits = nullptr, *d_raw = nullptr;
+  uint64_t *d_chunk_bits = nullptr, *d_chunk_off = nullptr, *d_scan_bits = nullptr,
+           *d_out_len = nullptr;
+  HuffCode *d_hc = nullptr;
+  uint8_t *d_out = nullptr;
+  int *d_err = nullptr;
+  unsigned *d_replays = nullptr;
+  bool timing = false;
+  static constexpr int HIST = 64;
+  hipEvent_t evh[HIST][8] = {};  // per-step events while timing is on
+  hipEvent_t *ev = evh[0];       // current step's events
+  long long steps = 0;
+  int last_frames = 0;
+};
+
+template <class T>
+static hipError_t dalloc(T **p, size_t count) {
+  return hipMalloc((void **)p, count * sizeof(T) + 256);
+}
+
+static void batch_free(mij_batch *b) {
+  if (!b) return;
+  hipSetDevice(b->dev);
+  if (b->stream) hipStreamSynchronize(b->stream);
+  void *ptrs[] = {b->d_tab, b->own_in ? b->d_in : nullptr, b->d_coef, b->d_dc, b->d_hist,
+                  b->d_ehuf, b->d_bits, b->d_raw, b->d_chunk_bits, b->d_chunk_off,
+                  b->d_scan_bits, b->d_out_len, b->d_hc, b->d_out, b->d_err, b->d_replays};
+  for (void *p : ptrs)
+    if (p) hipFree(p);
+  for (auto &row : b->evh)
+    for (auto &e : row)
+      if (e) hipEventDestroy(e);
+  if (b->stream) hipStreamDestroy(b->stream);
+  delete b;
+}
+
+static int check_device(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+    return fail(MIJ_ENODEV, "no HIP device visible (the HIP path has no CPU fallback)");
+  if (device < 0 || device >= n) return fail(MIJ_ENODEV, "device %d out of range (%d)", device, n);
+  return MIJ_OK;
+}
+
+static int batch_init(mij_batch *b, int device, int w, int h, int frames, int quality) {
+  if (check_device(device)) return g_err;
+  b->dev = device;
+  HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+  b->g = make_geom(w, h);
+  b->cap = frames;
+  b->quality = quality;
+  const Geom &g = b->g;
+  const long long F = frames;
+  HIP_TRY(dalloc(&b->d_tab, 1));
+  {
+    Tables *t = new Tables;
+    fill_tables(quality, t);
+    hipError_t e = hipMemcpy(b->d_tab, t, sizeof(Tables), hipMemcpyHostToDevice);
+    delete t;
+    HIP_TRY(e);
+    uint32_t *lut = &b->d_tab->lut[0][0];
+    HIP_TRY(hipMemsetAsync(lut, 0, sizeof(uint32_t) * 3 * 2048, b->stream));
+    HIP_TRY(launch_colour_lut(lut, b->stream));
+  }
+  b->pitch = w * 3;
+  b->in_fs = (long long)w * h * 3;
+  HIP_TRY(dalloc(&b->d_in, F * b->in_fs));
+  b->own_in = true;
+  HIP_TRY(dalloc(&b->d_coef, F * g.coef_fs));
+  HIP_TRY(dalloc(&b->d_dc, F * g.nblk));
+  HIP_TRY(dalloc(&b->d_hist, F * 4 * 257));
+  HIP_TRY(dalloc(&b->d_ehuf, F * 4 * 256));
+  HIP_TRY(dalloc(&b->d_bits, F * g.nblk));
+  HIP_TRY(dalloc(&b->d_raw, F * g.raw_fs));
+  HIP_TRY(dalloc(&b->d_chunk_bits, F * g.cpf));
+  HIP_TRY(dalloc(&b->d_chunk_off, F * g.cpf));
+  HIP_TRY(dalloc(&b->d_scan_bits, F * 3));
+  HIP_TRY(dalloc(&b->d_out_len, F));
+  HIP_TRY(dalloc(&b->d_hc, F * 4));
+  HIP_TRY(dalloc(&b->d_out, F * g.out_cap));
+  HIP_TRY(dalloc(&b->d_err, F));
+  HIP_TRY(dalloc(&b->d_replays, 1));
+  HIP_TRY(hipMemsetAsync(b->d_replays, 0, sizeof(unsigned), b->stream));
+  for (auto &row : b->evh)
+    for (auto &e : row) HIP_TRY(hipEventCreate(&e));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  return MIJ_OK;
+}
+
+extern "C" mij_batch *mij_batch_create(int device, int width, int height, int max_frames,
+                                       int quality) {
+  if (!valid_dims(width, height) || max_frames < 1 || quality < 1 || quality > 100) {
+    fail(MIJ_EINVAL, "batch_create: bad geometry %dx%d x%d or quality %d", width, height,
+         max_frames, quality);
+    return nullptr;
+  }
+  mij_batch *b = new mij_batch;
+  if (batch_init(b, device, width, height, max_frames, quality)) {
+    batch_free(b);
+    return nullptr;
+  }
+  g_err = MIJ_OK;
+  return b;
+}
+
+extern "C" void mij_batch_destroy(mij_batch *b) { batch_free(b); }
+
+extern "C" void *mij_batch_stream(mij_batch *b) { return b ? (void *)b->stream : nullptr; }
+
+extern "C" int mij_batch_upload(mij_batch *b, const uint8_t *bgr, int first, int nframes) {
+  if (!b || !bgr || first < 0 || nframes < 1 || first + nframes > b->cap)
+    return fail(MIJ_EINVAL, "upload: bad args");
+  if (!b->own_in) return fail(MIJ_EINVAL, "upload: batch reads external device input");
+  HIP_TRY(hipSetDevice(b->dev));
+  HIP_TRY(hipMemcpyAsync(b->d_in + (long long)first * b->in_fs, bgr, (size_t)nframes * b->in_fs,
+                         hipMemcpyHostToDevice, b->stream));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  return MIJ_OK;
+}
+
+extern "C" int mij_batch_set_input(mij_batch *b, const void *d_bgr, long long frame_stride,
+                                   int pitch) {
+  if (!b || !d_bgr || ((uintptr_t)d_bgr & 3) || (pitch & 3) || pitch < b->g.w * 3)
+    return fail(MIJ_EINVAL, "set_input: pointer/pitch must be 4-byte aligned, pitch >= 3*w");
+  HIP_TRY(hipSetDevice(b->dev));
+  if (b->own_in && b->d_in) HIP_TRY(hipFree(b->d_in));
+  b->own_in = false;
+  b->d_in = (uint8_t *)d_bgr;
+  b->in_fs = frame_stride;
+  b->pitch = pitch;
+  return MIJ_OK;
+}
+
+static EntArgs ent_args(mij_batch *b, int nframes, int dc_mode) {
+  EntArgs a;
+  a.g = b->g;
+  a.nframes = nframes;
+  a.coef = b->d_coef;
+  a.dc = b->d_dc;
+  a.dc_mode = dc_mode;
+  a.hist = b->d_hist;
+  a.ehuf = b->d_ehuf;
+  a.bits = b->d_bits;
+  a.chunk_bits = b->d_chunk_bits;
+  a.chunk_off = b->d_chunk_off;
+  a.scan_bits = b->d_scan_bits;
+  a.raw = b->d_raw;
+  a.hc = b->d_hc;
+  a.tab = b->d_tab;
+  a.out = b->d_out;
+  a.out_len = b->d_out_len;
+  a.err = b->d_err;
+  return a;
+}
+
+static int run_k1(mij_batch *b, int nframes) {
+  K1Args k;
+  k.in = b->d_in;
+  k.in_fs = b->in_fs;
+  k.pitch = b->pitch;
+  k.nframes = nframes;
+  k.g = b->g;
+  k.coef = b->d_coef;
+  k.dc = b->d_dc;
+  k.tab = b->d_tab;
+  k.replays = b->d_replays;
+  const long long ntiles = (long long)nframes * b->g.tiles_per_frame;
+  HIP_TRY(launch_k1(k, k1_grid(b->dev, ntiles), b->stream));
+  return MIJ_OK;
+}
+
+// stages after K1; dc_mode 0 = coefficients from K1 (raw DC + dc array)
+static int run_entropy(mij_batch *b, int nframes, int dc_mode, bool tables_given) {
+  EntArgs a = ent_args(b, nframes, dc_mode);
+  const bool t = b->timing;
+  if (!tables_given) {
+    HIP_TRY(hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * nframes * 4 * 257, b->stream));
+    HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * nframes, b->stream));
+    HIP_TRY(launch_stats(a, b->stream));
+    if (t) HIP_TRY(hipEventRecord(b->ev[2], b->stream));
+    HIP_TRY(launch_tables(a, b->stream));
+    if (t) HIP_TRY(hipEventRecord(b->ev[3], b->stream));
+  }
+  HIP_TRY(launch_bits(a, b->stream));
+  if (t) HIP_TRY(hipEventRecord(b->ev[4], b->stream));
+  HIP_TRY(launch_scan(a, b->stream));
+  if (t) HIP_TRY(hipEventRecord(b->ev[5], b->stream));
+  HIP_TRY(launch_pack(a, b->stream));
+  if (t) HIP_TRY(hipEventRecord(b->ev[6], b->stream));
+  HIP_TRY(launch_emit(a, b->stream));
+  if (t) HIP_TRY(hipEventRecord(b->ev[7], b->stream));
+  return MIJ_OK;
+}
+
+static void next_slot(mij_batch *b) {
+  if (b->timing) b->ev = b->evh[b->steps++ % mij_batch::HIST];
+}
+
+extern "C" int mij_batch_encode(mij_batch *b, int nframes) {
+  if (!b || nframes < 1 || nframes > b->cap) return fail(MIJ_EINVAL, "encode: bad frame count");
+  HIP_TRY(hipSetDevice(b->dev));
+  next_slot(b);
+  if (b->timing) HIP_TRY(hipEventRecord(b->ev[0], b->stream));
+  if (run_k1(b, nframes)) return g_err;
+  if (b->timing) HIP_TRY(hipEventRecord(b->ev[1], b->stream));
+  if (run_entropy(b, nframes, 0, false)) return g_err;
+  b->last_frames = nframes;
+  return MIJ_OK;
+}
+
+extern "C" int mij_batch_dct(mij_batch *b, int nframes) {
+  if (!b || nframes < 1 || nframes > b->cap) return fail(MIJ_EINVAL, "dct: bad frame count");
+  HIP_TRY(hipSetDevice(b->dev));
+  next_slot(b);
+  if (b->timing) HIP_TRY(hipEventRecord(b->ev[0], b->stream));
+  if (run_k1(b, nframes)) return g_err;
+  if (b->timing) HIP_TRY(hipEventRecord(b->ev[1], b->stream));
+  return MIJ_OK;
+}
+
+extern "C" int mij_batch_sync(mij_batch *b) {
+  if (!b) return fail(MIJ_EINVAL, "sync: null batch");
+  HIP_TRY(hipSetDevice(b->dev));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  return MIJ_OK;
+}
+
+extern "C" int mij_batch_set_timing(mij_batch *b, int on) {
+  if (!b) return fail(MIJ_EINVAL, "set_timing: null batch");
+  b->timing = on != 0;
+  b->steps = 0;
+  b->ev = b->evh[0];
+  return MIJ_OK;
+}
+
+static float elapsed(hipEvent_t a, hipEvent_t z) {
+  float v = -1.0f;
+  if (hipEventElapsedTime(&v, a, z) != hipSuccess) v = -1.0f;
+  return v;
+}
+
+static const int k_stage_pairs[8][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4},
+                                        {4, 5}, {5, 6}, {6, 7}, {0, 7}};
+
+extern "C" int mij_batch_stage_history(mij_batch *b, float *ms, int steps) {
+  if (!b || !ms || steps < 1) return fail(MIJ_EINVAL, "stage_history: bad args");
+  HIP_TRY(hipSetDevice(b->dev));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  long long have = b->steps < mij_batch::HIST ? b->steps : mij_batch::HIST;
+  int n = (int)(steps < have ? steps : have);
+  for (int i = 0; i < n; i++) {
+    const long long step = b->steps - n + i;
+    hipEvent_t *e = b->evh[step % mij_batch::HIST];
+    for (int k = 0; k < 8; k++) ms[i * 8 + k] = elapsed(e[k_stage_pairs[k][0]], e[k_stage_pairs[k][1]]);
+  }
+  return n;
+}
+
+extern "C" int mij_batch_stage_ms(mij_batch *b, float *ms, int n) {
+  if (!b || !ms) return fail(MIJ_EINVAL, "stage_ms: bad args");
+  HIP_TRY(hipSetDevice(b->dev));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  for (int i = 0; i < n && i < 8; i++) ms[i] = elapsed(b->ev[k_stage_pairs[i][0]], b->ev[k_stage_pairs[i][1]]);
+  return MIJ_OK;
+}
+
+extern "C" unsigned long long mij_batch_replays(mij_batch *b) {
+  if (!b) return 0;
+  unsigned v = 0;
+  hipSetDevice(b->dev);
+  hipStreamSynchronize(b->stream);
+  hipMemcpy(&v, b->d_replays, sizeof(v), hipMemcpyDeviceToHost);
+  return v;
+}
+
+extern "C" int mij_batch_lengths(mij_batch *b, size_t *lens, int nframes) {
+  if (!b || !lens || nframes < 1 || nframes > b->cap) return fail(MIJ_EINVAL, "lengths: bad args");
+  HIP_TRY(hipSetDevice(b->dev));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  std::vector<uint64_t> v(nframes);
+  HIP_TRY(hipMemcpy(v.data(), b->d_out_len, sizeof(uint64_t) * nframes, hipMemcpyDeviceToHost));
+  for (int i = 0; i < nframes; i++) lens[i] = (size_t)v[i];
+  return MIJ_OK;
+}
+
+extern "C" int mij_batch_output(mij_batch *b, int frame, uint8_t *dst, size_t cap, size_t *len) {
+  if (!b || frame < 0 || frame >= b->cap) return fail(MIJ_EINVAL, "output: bad frame");
+  HIP_TRY(hipSetDevice(b->dev));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  uint64_t n = 0;
+  int err = 0;
+  HIP_TRY(hipMemcpy(&n, b->d_out_len + frame, sizeof(n), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&err, b->d_err + frame, sizeof(err), hipMemcpyDeviceToHost));
+  if (err) return fail(MIJ_ETABLE, "frame %d: Huffman table construction failed", frame);
+  if (len) *len = (size_t)n;
+  if (dst) {
+    if (cap < n) return fail(MIJ_ENOSPC, "output: need %llu bytes", (unsigned long long)n);
+    HIP_TRY(hipMemcpy(dst, b->d_out + (long long)frame * b->g.out_cap, n, hipMemcpyDeviceToHost));
+  }
+  return MIJ_OK;
+}
+
+extern "C" int mij_batch_coefs(mij_batch *b, int frame, int16_t *Y, int16_t *Cb, int16_t *Cr,
+                               int diffed) {
+  if (!b || frame < 0 || frame >= b->cap) return fail(MIJ_EINVAL, "coefs: bad frame");
+  HIP_TRY(hipSetDevice(b->dev));
+  const Geom &g = b->g;
+  int16_t *base = b->d_coef + (long long)frame * g.coef_fs;
+  int16_t *tmp = nullptr;
+  if (diffed) {  // differenced copy, leaving the batch's planes raw
+    HIP_TRY(hipMalloc((void **)&tmp, sizeof(int16_t) * g.coef_fs));
+    HIP_TRY(hipMemcpyAsync(tmp, base, sizeof(int16_t) * g.coef_fs, hipMemcpyDeviceToDevice,
+                           b->stream));
+    HIP_TRY(launch_dc_diff(tmp, b->d_dc + (long long)frame * g.nblk, g, 1, b->stream));
+    base = tmp;
+  }
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  hipError_t e = hipMemcpy(Y, base, sizeof(int16_t) * g.nY * 64, hipMemcpyDeviceToHost);
+  if (e == hipSuccess)
+    e = hipMemcpy(Cb, base + (long long)g.nY * 64, sizeof(int16_t) * g.nC * 64,
+                  hipMemcpyDeviceToHost);
+  if (e == hipSuccess)
+    e = hipMemcpy(Cr, base + (long long)(g.nY + g.nC) * 64, sizeof(int16_t) * g.nC * 64,
+                  hipMemcpyDeviceToHost);
+  if (tmp) hipFree(tmp);
+  HIP_TRY(e);
+  return MIJ_OK;
+}
+
+extern "C" int mij_batch_tables(mij_batch *b, int frame, huff_code out[4]) {
+  if (!b || !out || frame < 0 || frame >= b->cap) return fail(MIJ_EINVAL, "tables: bad args");
+  HIP_TRY(hipSetDevice(b->dev));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  HIP_TRY(hipMemcpy(out, b->d_hc + (long long)frame * 4, sizeof(HuffCode) * 4,
+                    hipMemcpyDeviceToHost));
+  return MIJ_OK;
+}
+
+// ---------------------------------------------------------------------------
+// drop-in entry points: one lazily created single-frame pipeline
+// ---------------------------------------------------------------------------
+static std::mutex g_mu;
+static mij_batch *g_ctx = nullptr;
+static int g_stride = 320;  // define.h:3 WIDTH
+static int g_quality = 50;
+
+static int drop_device() {
+  const char *e = getenv("MIJ_DEVICE");
+  return e ? atoi(e) : 0;
+}
+
+static mij_batch *ctx_for(int w, int h, int quality) {
+  if (g_ctx && g_ctx->g.w == w && g_ctx->g.h == h && g_ctx->quality == quality) return g_ctx;
+  batch_free(g_ctx);
+  g_ctx = mij_batch_create(drop_device(), w, h, 1, quality);
+  return g_ctx;
+}
+
+extern "C" int mij_set_input_stride(int stride_px) {
+  if (stride_px < 16) return fail(MIJ_EINVAL, "stride %d", stride_px);
+  std::lock_guard<std::mutex> l(g_mu);
+  g_stride = stride_px;
+  return MIJ_OK;
+}
+
+extern "C" int mij_set_quality(int quality) {
+  if (quality < 1 || quality > 100) return fail(MIJ_EINVAL, "quality %d", quality);
+  std::lock_guard<std::mutex> l(g_mu);
+  g_quality = quality;
+  return MIJ_OK;
+}
+
+static int upload_region(mij_batch *b, const uint8_t *in, int stride, area_t d) {
+  if (d.x < 0 || d.y < 0 || d.x + d.w > stride)
+    return fail(MIJ_EINVAL, "region x=%d w=%d outside stride %d", d.x, d.w, stride);
+  const uint8_t *src = in + ((size_t)d.y * stride + d.x) * 3;
+  HIP_TRY(hipMemcpy2DAsync(b->d_in, (size_t)d.w * 3, src, (size_t)stride * 3, (size_t)d.w * 3,
+                           d.h, hipMemcpyHostToDevice, b->stream));
+  return MIJ_OK;
+}
+
+static int upload_planes(mij_batch *b, const int16_t *Y, const int16_t *Cb, const int16_t *Cr) {
+  const Geom &g = b->g;
+  HIP_TRY(hipMemcpyAsync(b->d_coef, Y, sizeof(int16_t) * g.nY * 64, hipMemcpyHostToDevice,
+                         b->stream));
+  HIP_TRY(hipMemcpyAsync(b->d_coef + (long long)g.nY * 64, Cb, sizeof(int16_t) * g.nC * 64,
+                         hipMemcpyHostToDevice, b->stream));
+  HIP_TRY(hipMemcpyAsync(b->d_coef + (long long)(g.nY + g.nC) * 64, Cr,
+                         sizeof(int16_t) * g.nC * 64, hipMemcpyHostToDevice, b->stream));
+  return MIJ_OK;
+}
+
+extern "C" void rgb_to_dct(uint8_t *in, int16_t *Y, int16_t *Cb, int16_t *Cr, area_t dims) {
+  std::lock_guard<std::mutex> l(g_mu);
+  g_err = MIJ_OK;
+  if (!in || !Y || !Cb || !Cr || !valid_dims(dims.w, dims.h)) {
+    fail(MIJ_EINVAL, "rgb_to_dct: null buffer or dims %dx%d not multiples of 16", dims.w, dims.h);
+    return;
+  }
+  mij_batch *b = ctx_for(dims.w, dims.h, g_quality);
+  if (!b) return;
+  if (upload_region(b, in, g_stride, dims)) return;
+  if (run_k1(b, 1)) return;
+  if (launch_dc_diff(b->d_coef, b->d_dc, b->g, 1, b->stream) != hipSuccess) {
+    fail(MIJ_EHIP, "dc_diff launch failed");
+    return;
+  }
+  const Geom &g = b->g;
+  if (hipStreamSynchronize(b->stream) != hipSuccess ||
+      hipMemcpy(Y, b->d_coef, sizeof(int16_t) * g.nY * 64, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(Cb, b->d_coef + (long long)g.nY * 64, sizeof(int16_t) * g.nC * 64,
+                hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(Cr, b->d_coef + (long long)(g.nY + g.nC) * 64, sizeof(int16_t) * g.nC * 64,
+                hipMemcpyDeviceToHost) != hipSuccess)
+    fail(MIJ_EHIP, "rgb_to_dct: device copy failed");
+}
+
+extern "C" void init_huffman(int16_t *Y, int16_t *Cb, int16_t *Cr, area_t dims,
+                             huff_code Luma[2], huff_code Chroma[2]) {
+  std::lock_guard<std::mutex> l(g_mu);
+  g_err = MIJ_OK;
+  if (!Y || !Cb || !Cr || !Luma || !Chroma || !valid_dims(dims.w, dims.h)) {
+    fail(MIJ_EINVAL, "init_huffman: bad arguments");
+    return;
+  }
+  mij_batch *b = ctx_for(dims.w, dims.h, g_quality);
+  if (!b || upload_planes(b, Y, Cb, Cr)) return;
+  EntArgs a = ent_args(b, 1, 1);
+  if (hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * 4 * 257, b->stream) != hipSuccess ||
+      hipMemsetAsync(b->d_err, 0, sizeof(int), b->stream) != hipSuccess ||
+      launch_stats(a, b->stream) != hipSuccess || launch_tables(a, b->stream) != hipSuccess) {
+    fail(MIJ_EHIP, "init_huffman: launch failed");
+    return;
+  }
+  HuffCode t[4];
+  int err = 0;
+  if (hipStreamSynchronize(b->stream) != hipSuccess ||
+      hipMemcpy(t, b->d_hc, sizeof(t), hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) {
+    fail(MIJ_EHIP, "init_huffman: device copy failed");
+    return;
+  }
+  if (err) fail(MIJ_ETABLE, "init_huffman: table construction outside defined behaviour");
+  memcpy(&Luma[0], &t[0], sizeof(HuffCode));
+  memcpy(&Luma[1], &t[1], sizeof(HuffCode));
+  memcpy(&Chroma[0], &t[2], sizeof(HuffCode));
+  memcpy(&Chroma[1], &t[3], sizeof(HuffCode));
+}
+
+extern "C" size_t write_jpg(FILE *f, uint8_t *jpg, int16_t *Y, int16_t *Cb, int16_t *Cr,
+                            area_t dims, huff_code Luma[2], huff_code Chroma[2]) {
+  std::lock_guard<std::mutex> l(g_mu);
+  g_err = MIJ_OK;
+  if (!jpg || !Y || !Cb || !Cr || !Luma || !Chroma || !valid_dims(dims.w, dims.h)) {
+    fail(MIJ_EINVAL, "write_jpg: bad arguments");
+    return 0;
+  }
+  mij_batch *b = ctx_for(dims.w, dims.h, g_quality);
+  if (!b || upload_planes(b, Y, Cb, Cr)) return 0;
+  HuffCode t[4];
+  memcpy(&t[0], &Luma[0], sizeof(HuffCode));
+  memcpy(&t[1], &Luma[1], sizeof(HuffCode));
+  memcpy(&t[2], &Chroma[0], sizeof(HuffCode));
+  memcpy(&t[3], &Chroma[1], sizeof(HuffCode));
+  if (hipMemcpyAsync(b->d_hc, t, sizeof(t), hipMemcpyHostToDevice, b->stream) != hipSuccess ||
+      hipMemsetAsync(b->d_err, 0, sizeof(int), b->stream) != hipSuccess ||
+      launch_ehuf_struct(b->d_hc, b->d_ehuf, b->stream) != hipSuccess) {
+    fail(MIJ_EHIP, "write_jpg: table upload failed");
+    return 0;
+  }
+  if (run_entropy(b, 1, 1, true)) return 0;
+  size_t n = 0;
+  if (hipStreamSynchronize(b->stream) != hipSuccess) {
+    fail(MIJ_EHIP, "write_jpg: stream failed");
+    return 0;
+  }
+  uint64_t n64 = 0;
+  if (hipMemcpy(&n64, b->d_out_len, sizeof(n64), hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(jpg, b->d_out, n64, hipMemcpyDeviceToHost) != hipSuccess) {
+    fail(MIJ_EHIP, "write_jpg: device copy failed");
+    return 0;
+  }
+  n = (size_t)n64;
+  if (f && fwrite(jpg, 1, n, f) != n) fail(MIJ_EINVAL, "write_jpg: short write to FILE*");
+  return n;
+}
+
+extern "C" int mij_encode(const uint8_t *bgr, int stride_px, area_t dims, int quality,
+                          uint8_t *out, size_t cap, size_t *out_len) {
+  std::lock_guard<std::mutex> l(g_mu);
+  g_err = MIJ_OK;
+  if (!bgr || !out || !valid_dims(dims.w, dims.h) || quality < 1 || quality > 100)
+    return fail(MIJ_EINVAL, "mij_encode: bad arguments");
+  mij_batch *b = ctx_for(dims.w, dims.h, quality);
+  if (!b) return g_err;
+  if (upload_region(b, bgr, stride_px, dims)) return g_err;
+  if (run_k1(b, 1) || run_entropy(b, 1, 0, false)) return g_err;
+  size_t n = 0;
+  if (mij_batch_output(b, 0, nullptr, 0, &n)) return g_err;
+  if (n > cap) return fail(MIJ_ENOSPC, "mij_encode: need %zu bytes", n);
+  if (mij_batch_output(b, 0, out, cap, &n)) return g_err;
+  if (out_len) *out_len = n;
+  return MIJ_OK;
+}
+
+// ---------------------------------------------------------------------------
+// diagnostics
+// ---------------------------------------------------------------------------
+extern "C" int mij_probe_mfma(const int8_t *A, const int8_t *B, int32_t *D) {
+  if (check_device(drop_device())) return g_err;
+  HIP_TRY(hipSetDevice(drop_device()));
+  int4 *dA, *dB, *dD;
+  HIP_TRY(hipMalloc((void **)&dA, 64 * 16));
+  HIP_TRY(hipMalloc((void **)&dB, 64 * 16));
+  HIP_TRY(hipMalloc((void **)&dD, 64 * 16));
+  HIP_TRY(hipMemcpy(dA, A, 64 * 16, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dB, B, 64 * 16, hipMemcpyHostToDevice));
+  HIP_TRY(launch_mfma_probe(dA, dB, dD, nullptr));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(D, dD, 64 * 16, hipMemcpyDeviceToHost));
+  hipFree(dA);
+  hipFree(dB);
+  hipFree(dD);
+  return MIJ_OK;
+}
+
+extern "C" int mij_colour_lut(uint32_t *out) {
+  std::lock_guard<std::mutex> l(g_mu);
+  mij_batch *b = ctx_for(16, 16, g_quality);
+  if (!b) return g_err;
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  HIP_TRY(hipMemcpy(out, &b->d_tab->lut[0][0], sizeof(uint32_t) * 3 * 2048,
+                    hipMemcpyDeviceToHost));
+  return MIJ_OK;
+}

@@ -1,0 +1,276 @@
+"""ctypes binding of libmijpeg.so (include/mijpeg.h) for tests and bench.py.
+
+The product is the C ABI; this module only marshals numpy buffers across it.
+There is deliberately no CPU fallback: if the HIP library is missing or no
+GPU is visible, every call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmijpeg.so")
+
+EXPORTS = [
+    # drop-in (reference include/encoder.h:10-12)
+    "rgb_to_dct", "init_huffman", "write_jpg",
+    # extensions
+    "mij_set_input_stride", "mij_set_quality", "mij_last_error", "mij_strerror",
+    "mij_max_jpg_bytes", "mij_encode",
+    "mij_batch_create", "mij_batch_destroy", "mij_batch_upload", "mij_batch_set_input",
+    "mij_batch_encode", "mij_batch_dct", "mij_batch_sync", "mij_batch_output",
+    "mij_batch_lengths", "mij_batch_coefs", "mij_batch_tables", "mij_batch_set_timing",
+    "mij_batch_stage_ms", "mij_batch_stage_history", "mij_batch_replays", "mij_batch_stream",
+    "mij_probe_mfma", "mij_colour_lut", "mij_build_target",
+]
+
+
+class Huff(C.Structure):
+    """huff_code (reference include/structs.h:5-13)."""
+    _fields_ = [
+        ("sym_freq", C.c_int * 257),
+        ("code_len", C.c_int * 257),
+        ("next", C.c_int * 257),
+        ("code_len_freq", C.c_int * 32),
+        ("sym_sorted", C.c_int * 256),
+        ("sym_code_len", C.c_int * 256),
+        ("sym_code", C.c_int * 256),
+    ]
+
+
+class Area(C.Structure):
+    """area_t (reference include/structs.h:15-18)."""
+    _fields_ = [("x", C.c_int), ("y", C.c_int), ("w", C.c_int), ("h", C.c_int)]
+
+
+class MijError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MijError(f"{LIB_PATH} missing: build it with `make -C {HERE}` "
+                       "(there is no CPU fallback)")
+    lib = C.CDLL(LIB_PATH)
+    p, i, sz = C.c_void_p, C.c_int, C.c_size_t
+    lib.rgb_to_dct.argtypes = [p, p, p, p, Area]
+    lib.rgb_to_dct.restype = None
+    lib.init_huffman.argtypes = [p, p, p, Area, p, p]
+    lib.init_huffman.restype = None
+    lib.write_jpg.argtypes = [p, p, p, p, p, Area, p, p]
+    lib.write_jpg.restype = sz
+    lib.mij_set_input_stride.argtypes = [i]
+    lib.mij_set_quality.argtypes = [i]
+    lib.mij_last_error.restype = i
+    lib.mij_strerror.restype = C.c_char_p
+    lib.mij_strerror.argtypes = [i]
+    lib.mij_max_jpg_bytes.restype = sz
+    lib.mij_max_jpg_bytes.argtypes = [i, i]
+    lib.mij_encode.argtypes = [p, i, Area, i, p, sz, C.POINTER(sz)]
+    lib.mij_batch_create.restype = p
+    lib.mij_batch_create.argtypes = [i, i, i, i, i]
+    lib.mij_batch_destroy.argtypes = [p]
+    lib.mij_batch_destroy.restype = None
+    lib.mij_batch_upload.argtypes = [p, p, i, i]
+    lib.mij_batch_set_input.argtypes = [p, p, C.c_longlong, i]
+    lib.mij_batch_encode.argtypes = [p, i]
+    lib.mij_batch_dct.argtypes = [p, i]
+    lib.mij_batch_sync.argtypes = [p]
+    lib.mij_batch_output.argtypes = [p, i, p, sz, C.POINTER(sz)]
+    lib.mij_batch_lengths.argtypes = [p, C.POINTER(sz), i]
+    lib.mij_batch_coefs.argtypes = [p, i, p, p, p, i]
+    lib.mij_batch_tables.argtypes = [p, i, p]
+    lib.mij_batch_set_timing.argtypes = [p, i]
+    lib.mij_batch_stage_ms.argtypes = [p, p, i]
+    lib.mij_batch_stage_history.argtypes = [p, p, i]
+    lib.mij_batch_replays.restype = C.c_ulonglong
+    lib.mij_batch_replays.argtypes = [p]
+    lib.mij_batch_stream.restype = p
+    lib.mij_batch_stream.argtypes = [p]
+    lib.mij_probe_mfma.argtypes = [p, p, p]
+    lib.mij_colour_lut.argtypes = [p]
+    lib.mij_build_target.restype = C.c_char_p
+    _lib = lib
+    return lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        lib = load()
+        raise MijError(f"{what}: {lib.mij_strerror(rc).decode()} ({rc})")
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def max_jpg_bytes(w: int, h: int) -> int:
+    return int(load().mij_max_jpg_bytes(w, h))
+
+
+# ---- drop-in three-call path (main.c:144-152 call sequence) -----------------
+
+def set_input_stride(px: int) -> None:
+    _check(load().mij_set_input_stride(px), "mij_set_input_stride")
+
+
+def set_quality(q: int) -> None:
+    _check(load().mij_set_quality(q), "mij_set_quality")
+
+
+def rgb_to_dct(frame_bgr: np.ndarray, region):
+    """encoder.h:10 on a BGR frame; returns (Y, Cb, Cr) int16 planes."""
+    lib = load()
+    frame_bgr = np.ascontiguousarray(frame_bgr, np.uint8)
+    x, y, w, h = region
+    set_input_stride(frame_bgr.shape[1])
+    Y = np.zeros(w * h, np.int16)
+    Cb = np.zeros(w * h // 4, np.int16)
+    Cr = np.zeros(w * h // 4, np.int16)
+    lib.rgb_to_dct(_ptr(frame_bgr), _ptr(Y), _ptr(Cb), _ptr(Cr), Area(x, y, w, h))
+    _check(lib.mij_last_error(), "rgb_to_dct")
+    return Y, Cb, Cr
+
+
+def init_huffman(Y, Cb, Cr, region):
+    lib = load()
+    x, y, w, h = region
+    t = (Huff * 4)()
+    lib.init_huffman(_ptr(Y), _ptr(Cb), _ptr(Cr), Area(x, y, w, h), C.addressof(t),
+                     C.addressof(t) + 2 * C.sizeof(Huff))
+    _check(lib.mij_last_error(), "init_huffman")
+    return list(t)
+
+
+def write_jpg(Y, Cb, Cr, region, tables) -> bytes:
+    lib = load()
+    x, y, w, h = region
+    t = (Huff * 4)(*tables)
+    out = np.zeros(max_jpg_bytes(w, h), np.uint8)
+    n = lib.write_jpg(None, _ptr(out), _ptr(Y), _ptr(Cb), _ptr(Cr), Area(x, y, w, h),
+                      C.addressof(t), C.addressof(t) + 2 * C.sizeof(Huff))
+    _check(lib.mij_last_error(), "write_jpg")
+    return out[:n].tobytes()
+
+
+def encode(frame_bgr: np.ndarray, quality: int = 50, region=None) -> bytes:
+    """mij_encode: whole path host->host."""
+    lib = load()
+    frame_bgr = np.ascontiguousarray(frame_bgr, np.uint8)
+    H, W = frame_bgr.shape[:2]
+    x, y, w, h = region if region else (0, 0, W, H)
+    cap = max_jpg_bytes(w, h)
+    out = np.zeros(cap, np.uint8)
+    n = C.c_size_t(0)
+    _check(lib.mij_encode(_ptr(frame_bgr), W, Area(x, y, w, h), quality, _ptr(out), cap,
+                          C.byref(n)), "mij_encode")
+    return out[:n.value].tobytes()
+
+
+# ---- device-resident batch ---------------------------------------------------
+
+class Batch:
+    STAGES = ["k1_colour_dct_quant", "stats", "tables", "bits", "scan", "pack", "emit", "total"]
+
+    def __init__(self, w: int, h: int, max_frames: int, quality: int = 50, device: int = 0):
+        self.lib = load()
+        self.w, self.h, self.max_frames = w, h, max_frames
+        self.h_ = self.lib.mij_batch_create(device, w, h, max_frames, quality)
+        if not self.h_:
+            raise MijError(f"mij_batch_create failed: "
+                           f"{self.lib.mij_strerror(self.lib.mij_last_error()).decode()}")
+
+    def close(self) -> None:
+        if self.h_:
+            self.lib.mij_batch_destroy(self.h_)
+            self.h_ = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, frames_bgr: np.ndarray, first: int = 0) -> None:
+        frames_bgr = np.ascontiguousarray(frames_bgr, np.uint8)
+        n = frames_bgr.shape[0] if frames_bgr.ndim == 4 else 1
+        _check(self.lib.mij_batch_upload(self.h_, _ptr(frames_bgr), first, n), "upload")
+
+    def set_input(self, dev_ptr: int, frame_stride: int, pitch: int) -> None:
+        _check(self.lib.mij_batch_set_input(self.h_, dev_ptr, frame_stride, pitch), "set_input")
+
+    def encode(self, n: int) -> None:
+        _check(self.lib.mij_batch_encode(self.h_, n), "encode")
+
+    def dct(self, n: int) -> None:
+        _check(self.lib.mij_batch_dct(self.h_, n), "dct")
+
+    def sync(self) -> None:
+        _check(self.lib.mij_batch_sync(self.h_), "sync")
+
+    def output(self, frame: int) -> bytes:
+        n = C.c_size_t(0)
+        _check(self.lib.mij_batch_output(self.h_, frame, None, 0, C.byref(n)), "output")
+        buf = np.zeros(max(n.value, 1), np.uint8)
+        _check(self.lib.mij_batch_output(self.h_, frame, _ptr(buf), buf.size, C.byref(n)),
+               "output")
+        return buf[:n.value].tobytes()
+
+    def lengths(self, n: int) -> np.ndarray:
+        arr = (C.c_size_t * n)()
+        _check(self.lib.mij_batch_lengths(self.h_, arr, n), "lengths")
+        return np.array(arr[:], np.int64)
+
+    def coefs(self, frame: int, diffed: bool = True):
+        Y = np.zeros(self.w * self.h, np.int16)
+        Cb = np.zeros(self.w * self.h // 4, np.int16)
+        Cr = np.zeros(self.w * self.h // 4, np.int16)
+        _check(self.lib.mij_batch_coefs(self.h_, frame, _ptr(Y), _ptr(Cb), _ptr(Cr),
+                                        int(diffed)), "coefs")
+        return Y, Cb, Cr
+
+    def tables(self, frame: int):
+        t = (Huff * 4)()
+        _check(self.lib.mij_batch_tables(self.h_, frame, C.addressof(t)), "tables")
+        return list(t)
+
+    def set_timing(self, on: bool) -> None:
+        _check(self.lib.mij_batch_set_timing(self.h_, int(on)), "set_timing")
+
+    def stage_ms(self) -> dict:
+        ms = np.zeros(8, np.float32)
+        _check(self.lib.mij_batch_stage_ms(self.h_, _ptr(ms), 8), "stage_ms")
+        return dict(zip(self.STAGES, [float(v) for v in ms]))
+
+    def stage_history(self, steps: int) -> list:
+        ms = np.zeros((steps, 8), np.float32)
+        n = self.lib.mij_batch_stage_history(self.h_, _ptr(ms), steps)
+        if n < 0:
+            _check(self.lib.mij_last_error(), "stage_history")
+        return [dict(zip(self.STAGES, [float(v) for v in row])) for row in ms[:n]]
+
+    def replays(self) -> int:
+        return int(self.lib.mij_batch_replays(self.h_))
+
+
+def probe_mfma(A: np.ndarray, B: np.ndarray) -> np.ndarray:
+    A = np.ascontiguousarray(A, np.int8).reshape(64, 16)
+    B = np.ascontiguousarray(B, np.int8).reshape(64, 16)
+    D = np.zeros((64, 4), np.int32)
+    _check(load().mij_probe_mfma(_ptr(A), _ptr(B), _ptr(D)), "probe_mfma")
+    return D
+
+
+def colour_lut() -> np.ndarray:
+    out = np.zeros(3 * 2048, np.uint32)
+    _check(load().mij_colour_lut(_ptr(out)), "colour_lut")
+    return out.reshape(3, 2048)

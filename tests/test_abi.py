@@ -1,0 +1,75 @@
+"""CPU tests of the C-ABI boundary: the library builds for gfx950, loads, and
+exports every function include/mijpeg.h declares with the reference's
+signatures (encoder.h:10-12) and struct layouts (structs.h:5-18).  No GPU
+compute is attempted here."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+import mijpeg
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "mijpeg.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"\b([a-z_][a-z0-9_]*)\s*\([^;{]*\)\s*;", src)
+    return sorted(set(n for n in names if n not in ("sizeof",)))
+
+
+def test_header_declares_reference_entry_points():
+    names = declared_functions()
+    for fn in ("rgb_to_dct", "init_huffman", "write_jpg"):
+        assert fn in names
+    src = open(HEADER).read()
+    # exact reference prototypes (encoder.h:10-12), modulo whitespace
+    norm = re.sub(r"\s+", " ", src)
+    assert "void rgb_to_dct(uint8_t *in, int16_t *Y, int16_t *Cb, int16_t *Cr, area_t dims);" in norm
+    assert ("void init_huffman(int16_t *Y, int16_t *Cb, int16_t *Cr, area_t dims, "
+            "huff_code Luma[2], huff_code Chroma[2]);") in norm
+    assert ("size_t write_jpg(FILE *f, uint8_t *jpg, int16_t *Y, int16_t *Cb, int16_t *Cr, "
+            "area_t dims, huff_code Luma[2], huff_code Chroma[2]);") in norm
+
+
+def test_library_exports_every_declared_symbol():
+    lib = mijpeg.load()
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(declared_functions()) <= set(mijpeg.EXPORTS)
+
+
+def test_code_object_targets_gfx950():
+    blob = open(mijpeg.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob  # offload bundle of the code object
+    assert mijpeg.load().mij_build_target() == b"gfx950"
+
+
+def test_struct_layouts():
+    assert C.sizeof(mijpeg.Huff) == 6284
+    assert mijpeg.Huff.sym_sorted.offset + 256 * 4 == mijpeg.Huff.sym_code_len.offset
+    assert C.sizeof(mijpeg.Area) == 16
+
+
+def test_max_jpg_bytes_bounds():
+    assert mijpeg.max_jpg_bytes(64, 64) >= 566
+    assert mijpeg.max_jpg_bytes(15, 16) == 0
+    assert mijpeg.max_jpg_bytes(0, 16) == 0
+
+
+def test_validation_precedes_device_use():
+    lib = mijpeg.load()
+    assert lib.mij_set_quality(0) == 1 and lib.mij_set_quality(101) == 1
+    assert lib.mij_set_input_stride(3) == 1
+    assert not lib.mij_batch_create(0, 30, 16, 1, 50)
+    assert lib.mij_last_error() == 1
+
+
+def test_c_host_builds():
+    pkg = os.path.dirname(mijpeg.LIB_PATH)
+    subprocess.check_call(["make", "-s", "-C", pkg, "host/encode_ppm"])
+    assert os.access(os.path.join(pkg, "host", "encode_ppm"), os.X_OK)
