@@ -201,6 +201,8 @@ struct mij_batch {
   int pitch = 0;
   int16_t *d_coef = nullptr, *d_dc = nullptr;
   uint32_t *d_hist = nullptr, *d_ehuf = nullptr, *d_bits = nullptr, *d_raw = nullptr;
+  uint32_t *d_tok = nullptr;
+  uint8_t *d_hdr = nullptr;
   uint64_t *d_chunk_bits = nullptr, *d_chunk_off = nullptr, *d_scan_bits = nullptr,
            *d_out_len = nullptr;
   HuffCode *d_hc = nullptr;
@@ -225,7 +227,7 @@ static void batch_free(mij_batch *b) {
   hipSetDevice(b->dev);
   if (b->stream) hipStreamSynchronize(b->stream);
   void *ptrs[] = {b->d_tab, b->own_in ? b->d_in : nullptr, b->d_coef, b->d_dc, b->d_hist,
-                  b->d_ehuf, b->d_bits, b->d_raw, b->d_chunk_bits, b->d_chunk_off,
+                  b->d_ehuf, b->d_bits, b->d_raw, b->d_tok, b->d_hdr, b->d_chunk_bits, b->d_chunk_off,
                   b->d_scan_bits, b->d_out_len, b->d_hc, b->d_out, b->d_err, b->d_replays};
   for (void *p : ptrs)
     if (p) hipFree(p);
@@ -274,6 +276,8 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
   HIP_TRY(dalloc(&b->d_hist, F * 4 * 257));
   HIP_TRY(dalloc(&b->d_ehuf, F * 4 * 256));
   HIP_TRY(dalloc(&b->d_bits, F * g.nblk));
+  HIP_TRY(dalloc(&b->d_tok, F * g.nblk * 64));
+  HIP_TRY(dalloc(&b->d_hdr, F * g.nblk));
   HIP_TRY(dalloc(&b->d_raw, F * g.raw_fs));
   HIP_TRY(dalloc(&b->d_chunk_bits, F * g.cpf));
   HIP_TRY(dalloc(&b->d_chunk_off, F * g.cpf));
@@ -344,6 +348,8 @@ static EntArgs ent_args(mij_batch *b, int nframes, int dc_mode) {
   a.hist = b->d_hist;
   a.ehuf = b->d_ehuf;
   a.bits = b->d_bits;
+  a.tok = b->d_tok;
+  a.hdr = b->d_hdr;
   a.chunk_bits = b->d_chunk_bits;
   a.chunk_off = b->d_chunk_off;
   a.scan_bits = b->d_scan_bits;
@@ -376,14 +382,15 @@ static int run_k1(mij_batch *b, int nframes) {
 static int run_entropy(mij_batch *b, int nframes, int dc_mode, bool tables_given) {
   EntArgs a = ent_args(b, nframes, dc_mode);
   const bool t = b->timing;
+  // tokens + histograms (the histograms are unused when tables are given)
+  HIP_TRY(hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * nframes * 4 * 257, b->stream));
+  HIP_TRY(launch_stats(a, b->stream));
+  if (t) HIP_TRY(hipEventRecord(b->ev[2], b->stream));
   if (!tables_given) {
-    HIP_TRY(hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * nframes * 4 * 257, b->stream));
     HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * nframes, b->stream));
-    HIP_TRY(launch_stats(a, b->stream));
-    if (t) HIP_TRY(hipEventRecord(b->ev[2], b->stream));
     HIP_TRY(launch_tables(a, b->stream));
-    if (t) HIP_TRY(hipEventRecord(b->ev[3], b->stream));
   }
+  if (t) HIP_TRY(hipEventRecord(b->ev[3], b->stream));
   HIP_TRY(launch_bits(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[4], b->stream));
   HIP_TRY(launch_scan(a, b->stream));

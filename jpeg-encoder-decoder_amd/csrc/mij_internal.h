@@ -81,6 +81,8 @@ struct EntArgs {
   int dc_mode;              // 0: DC raw, diff from dc[]; 1: coef holds DC diff
   uint32_t *hist;           // per frame [4][257]
   const uint32_t *ehuf;     // per frame [4][256] = len << 16 | code
+  uint32_t *tok;            // per block 64 tokens (k_tokens)
+  uint8_t *hdr;             // per block: #AC tokens | EOB << 7
   uint32_t *bits;           // per block (frame-major)
   uint64_t *chunk_bits;     // per chunk
   uint64_t *chunk_off;      // per chunk: bit offset inside its scan

@@ -6,7 +6,7 @@
 //                  -> quantize/trunc (+FP64 replay near boundaries) -> zigzag
 //                  (encoder.c:121-150, :81-112, :65-70)
 //   k_dc_diff      DC differencing into the coefficient planes (:168-177)
-//   k_stats        symbol histograms (:315-358, :364-375)
+//   k_tokens       per-block symbol lists + histograms (:315-358, :462-502)
 //   k_tables       optimized Huffman tables, wave-parallel (:180-301)
 //   k_ehuf_struct  code tables from caller-owned huff_code structs
 //   k_bits         bits per block
@@ -377,72 +377,99 @@ __device__ __forceinline__ Chunk chunk_of(const Geom &G, int q) {
   return c;
 }
 
-// Symbol walk of one block by one wave: lane k owns zigzag coefficient k.
-// Mirrors encoder.c:321-358 / :462-502: a nonzero AC coefficient at k with
-// run r of zeros since the previous nonzero (or since the DC) emits r/16 ZRL
-// symbols then ((r%16)<<4)|class; an EOB follows unless coefficient 63 != 0.
-struct BlockSyms {
-  int c;          // this lane's coefficient
-  int cls;        // magnitude class of c (lane 0: of the DC difference)
-  int run;        // lanes > 0 with c != 0: zero run before c
-  bool has_sym;   // lane > 0 and c != 0
-  bool eob;       // uniform: block ends with EOB
-  int dcdiff;     // lane 0 only
-};
-
-__device__ __forceinline__ BlockSyms walk_block(const int16_t *blk, int lane, int dcdiff_lane0) {
-  BlockSyms s;
-  s.c = blk[lane];
-  const unsigned long long nz = __ballot(lane > 0 && s.c != 0);
-  s.eob = !((nz >> 63) & 1ull);
-  s.has_sym = lane > 0 && s.c != 0;
-  s.run = 0;
-  if (s.has_sym) {
-    const unsigned long long below = (nz & ((1ull << lane) - 1ull)) | 1ull;
-    s.run = lane - (63 - __clzll(below)) - 1;
-  }
-  s.dcdiff = dcdiff_lane0;
-  s.cls = mag_class(lane == 0 ? dcdiff_lane0 : s.c);
-  return s;
-}
-
-__device__ __forceinline__ int block_dcdiff(const EntArgs &a, const Chunk &c, int j,
-                                            const int16_t *blk) {
-  if (a.dc_mode) return blk[0];
-  const int16_t *dcf = a.dc + (long long)c.f * a.g.nblk;
-  return (int)dcf[j] - (j == c.cstart ? 0 : (int)dcf[j - 1]);
+// Magnitude bits of a value of class cls (encoder.c:442-444 / :456-458:
+// negative values are written as ~|v|, i.e. the low cls bits of v-1).
+__device__ __forceinline__ uint32_t mag_bits(int v, int cls) {
+  uint32_t id = (uint32_t)(v < 0 ? -v : v);
+  if (v < 0) id = ~id;
+  return id & ((1u << cls) - 1u);
 }
 
 // ===========================================================================
-// k_stats: symbol histograms, one workgroup per chunk.
+// k_tokens: coefficient planes -> per-block symbol lists + histograms.
+//
+// Token = symbol (bits 0-7) | ZRL count before it (bits 8-9) | magnitude
+// bits (16-27).  Block slot: token 0 = DC difference (symbol = its class,
+// encoder.c:434-446), tokens 1..n = the AC run/size symbols in zigzag order
+// exactly as encoder.c:321-358 / :462-502 visit them (a nonzero at zigzag k
+// after r zeros emits r/16 ZRLs, then ((r%16)<<4)|class); hdr = n | EOB<<7
+// (EOB unless coefficient 63 is nonzero).  Histograms: DC classes and AC
+// symbols per table (:315-319, :321-358), ZRLs and EOBs included.
+//
+// One workgroup per chunk; lane (g, b) of a wave holds zigzag coefficients
+// 16g..16g+15 of block b, so a wave covers 16 blocks per iteration and the
+// 64-bit nonzero mask of a block is assembled from its 4 lanes.
 // ===========================================================================
-__global__ __launch_bounds__(256) void k_stats(EntArgs a) {
+__global__ __launch_bounds__(256) void k_tokens(EntArgs a) {
   __shared__ uint32_t h[2][257];
+  __shared__ __attribute__((aligned(16))) int16_t s_coef[4][64][16];
   const Chunk c = chunk_of(a.g, blockIdx.x);
   for (int i = threadIdx.x; i < 2 * 257; i += 256) h[i / 257][i % 257] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int i = wave; i < c.n; i += 4) {
+  const int g = lane >> 4, bcol = lane & 15;
+  const long long fb = (long long)c.f * a.g.nblk;
+  for (int base = wave * 16; base < c.n; base += 64) {
+    const int i = base + bcol;
+    const bool v = i < c.n;
     const int j = c.first + i;
-    const int16_t *blk = a.coef + (long long)c.f * a.g.coef_fs + (long long)j * 64;
-    const int dd = lane == 0 ? block_dcdiff(a, c, j, blk) : 0;
-    const BlockSyms s = walk_block(blk, lane, dd);
-    if (lane == 0) {
-      atomicAdd(&h[0][s.cls], 1u);
-      if (s.eob) atomicAdd(&h[1][0x00], 1u);
+    u4v w0 = {0, 0, 0, 0}, w1 = {0, 0, 0, 0};
+    if (v) {
+      const int16_t *blk = a.coef + (long long)c.f * a.g.coef_fs + (long long)j * 64 + 16 * g;
+      w0 = *(const u4v *)blk;
+      w1 = *(const u4v *)(blk + 8);
     }
-    if (s.has_sym) {
-      atomicAdd(&h[1][((s.run & 15) << 4) | s.cls], 1u);
-      if (s.run >= 16) atomicAdd(&h[1][0xF0], (unsigned)(s.run >> 4));
+    *(u4v *)&s_coef[wave][lane][0] = w0;
+    *(u4v *)&s_coef[wave][lane][8] = w1;
+    uint32_t m16 = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t wd = k < 4 ? w0[k] : w1[k - 4];
+      m16 |= ((wd & 0xFFFFu) != 0u ? 1u : 0u) << (2 * k);
+      m16 |= ((wd >> 16) != 0u ? 1u : 0u) << (2 * k + 1);
     }
+    if (g == 0) m16 &= ~1u;  // the DC is not part of the AC run structure
+    unsigned long long M = (unsigned long long)m16 << (16 * g);
+    M |= __shfl_xor(M, 16);
+    M |= __shfl_xor(M, 32);
+    uint32_t *tok = a.tok + (fb + j) * 64;
+    if (g == 0 && v) {
+      const int dc = (int16_t)(w0[0] & 0xFFFFu);
+      const int diff =
+          a.dc_mode ? dc : dc - (j == c.cstart ? 0 : (int)a.dc[fb + j - 1]);  // :168-177
+      const int cls = mag_class(diff);
+      tok[0] = (uint32_t)cls | (mag_bits(diff, cls) << 16);
+      atomicAdd(&h[0][cls], 1u);
+      const int eob = !((M >> 63) & 1ull);
+      a.hdr[fb + j] = (uint8_t)(__popcll(M) | (eob << 7));
+      if (eob) atomicAdd(&h[1][0x00], 1u);
+    }
+    wave_lds_sync();
+    uint32_t mm = v ? m16 : 0u;
+    while (mm) {
+      const int k = __ffs(mm) - 1;
+      mm &= mm - 1u;
+      const int z = 16 * g + k;
+      const int cz = s_coef[wave][lane][k];
+      const unsigned long long before = M & ((1ull << z) - 1ull);
+      const int run = z - (63 - __clzll(before | 1ull)) - 1;
+      const int cls = mag_class(cz);
+      const int sym = ((run & 15) << 4) | cls;
+      tok[1 + __popcll(before)] = (uint32_t)sym | ((uint32_t)(run >> 4) << 8) |
+                                  (mag_bits(cz, cls) << 16);
+      atomicAdd(&h[1][sym], 1u);
+      if (run >= 16) atomicAdd(&h[1][0xF0], (unsigned)(run >> 4));
+    }
+    wave_lds_sync();
   }
   __syncthreads();
   uint32_t *gh = a.hist + ((long long)c.f * 4 + (c.comp ? 2 : 0)) * 257;
   for (int i = threadIdx.x; i < 2 * 257; i += 256) {
-    const uint32_t v = h[i / 257][i % 257];
-    if (v) atomicAdd(&gh[i], v);
+    const uint32_t hv = h[i / 257][i % 257];
+    if (hv) atomicAdd(&gh[i], hv);
   }
 }
+
 
 // ===========================================================================
 // k_tables: the four optimized Huffman tables of a frame (encoder.c:180-301),
@@ -656,50 +683,42 @@ __global__ void k_ehuf_struct(const HuffCode *hc, uint32_t *ehuf) {
 }
 
 // ===========================================================================
-// k_bits: bits of every block with the frame's tables; chunk totals.
+// k_bits: bits of every block from its tokens and the frame's code lengths;
+// chunk totals.  One thread per block.
 // ===========================================================================
-__device__ __forceinline__ int lane_bits(const BlockSyms &s, int lane, const uint32_t *dc_t,
-                                         const uint32_t *ac_t) {
-  int b = 0;
-  if (lane == 0) b = (int)(dc_t[s.cls] >> 16) + s.cls;
-  if (s.has_sym)
-    b = (int)(ac_t[((s.run & 15) << 4) | s.cls] >> 16) + s.cls +
-        (s.run >> 4) * (int)(ac_t[0xF0] >> 16);
-  if (lane == 63 && s.eob) b += (int)(ac_t[0x00] >> 16);
-  return b;
-}
-
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-  return v;
-}
-
 __global__ __launch_bounds__(256) void k_bits(EntArgs a) {
   __shared__ uint32_t tab[2][256];
-  __shared__ unsigned long long total;
+  __shared__ uint32_t wsum[4];
   const Chunk c = chunk_of(a.g, blockIdx.x);
   const uint32_t *et = a.ehuf + ((long long)c.f * 4 + (c.comp ? 2 : 0)) * 256;
   for (int i = threadIdx.x; i < 512; i += 256) tab[i >> 8][i & 255] = et[i];
-  if (threadIdx.x == 0) total = 0;
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  unsigned long long mine = 0;
-  for (int i = wave; i < c.n; i += 4) {
-    const int j = c.first + i;
-    const int16_t *blk = a.coef + (long long)c.f * a.g.coef_fs + (long long)j * 64;
-    const int dd = lane == 0 ? block_dcdiff(a, c, j, blk) : 0;
-    const BlockSyms s = walk_block(blk, lane, dd);
-    const int b = wave_sum(lane_bits(s, lane, tab[0], tab[1]));
-    if (lane == 0) {
-      a.bits[(long long)c.f * a.g.nblk + j] = (uint32_t)b;
-      mine += (unsigned long long)b;
+  const int t = threadIdx.x;
+  uint32_t bits = 0;
+  if (t < c.n) {
+    const long long gb = (long long)c.f * a.g.nblk + c.first + t;
+    const uint32_t *tok = a.tok + gb * 64;
+    const int hd = a.hdr[gb];
+    const int n = hd & 63;
+    const int dcls = (int)(tok[0] & 255u);
+    bits = (tab[0][dcls] >> 16) + (uint32_t)dcls;
+    const uint32_t lz = tab[1][0xF0] >> 16;
+    for (int i = 1; i <= n; i++) {
+      const uint32_t tk = tok[i];
+      const uint32_t sym = tk & 255u;
+      bits += (tab[1][sym] >> 16) + (sym & 15u) + ((tk >> 8) & 3u) * lz;
     }
+    if (hd & 128) bits += tab[1][0x00] >> 16;
+    a.bits[gb] = bits;
   }
-  if (lane == 0) atomicAdd(&total, mine);
+  uint32_t x = bits;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off);
+  if ((t & 63) == 0) wsum[t >> 6] = x;
   __syncthreads();
-  if (threadIdx.x == 0) a.chunk_bits[blockIdx.x] = total;
+  if (t == 0) a.chunk_bits[blockIdx.x] = (unsigned long long)wsum[0] + wsum[1] + wsum[2] + wsum[3];
 }
+
 
 // ===========================================================================
 // k_scan: per scan (frame, component) exclusive scan of chunk bit totals;
@@ -736,10 +755,11 @@ __global__ void k_scan(EntArgs a) {
 }
 
 // ===========================================================================
-// k_pack: bit-pack one chunk into LDS, then store it.  Each lane's symbols of
-// a block are placed at block offset + wave-exclusive-prefix of lane bits;
-// pieces are OR-ed into LDS words (big-endian bit order), interior words are
-// stored plainly, the two words shared with neighbouring chunks atomically.
+// k_pack: bit-pack one chunk into LDS, then store it.  Thread t writes block
+// t's tokens at the block's offset (chunk offset + exclusive scan of block
+// bits); pieces are OR-ed into LDS words in big-endian bit order.  Interior
+// words are stored plainly, the two words shared with neighbouring chunks
+// atomically (k_scan zeroed them).
 // ===========================================================================
 __device__ __forceinline__ void put_bits(uint32_t *buf, uint32_t pos, uint32_t val, int len) {
   // len in 1..28, val < 2^len
@@ -753,24 +773,16 @@ __device__ __forceinline__ void put_bits(uint32_t *buf, uint32_t pos, uint32_t v
   }
 }
 
-__device__ __forceinline__ uint32_t mag_bits(int v, int cls) {  // encoder.c:442-444
-  uint32_t id = (uint32_t)(v < 0 ? -v : v);
-  if (v < 0) id = ~id;
-  return id & ((1u << cls) - 1u);
-}
-
 __global__ __launch_bounds__(256) void k_pack(EntArgs a) {
   __shared__ uint32_t buf[CHUNK_WORDS];
   __shared__ uint32_t tab[2][256];
-  __shared__ uint32_t boff[CHUNK];
   __shared__ uint32_t wsum[4];
   const Chunk c = chunk_of(a.g, blockIdx.x);
   const uint32_t *et = a.ehuf + ((long long)c.f * 4 + (c.comp ? 2 : 0)) * 256;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < 512; i += 256) tab[i >> 8][i & 255] = et[i];
-
-  // block offsets inside the chunk: exclusive scan of bits (CHUNK == 256)
-  const uint32_t mybits = tid < c.n ? a.bits[(long long)c.f * a.g.nblk + c.first + tid] : 0u;
+  const long long gb = (long long)c.f * a.g.nblk + c.first + tid;
+  const uint32_t mybits = tid < c.n ? a.bits[gb] : 0u;
   uint32_t x = mybits;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -781,48 +793,40 @@ __global__ __launch_bounds__(256) void k_pack(EntArgs a) {
   __syncthreads();
   uint32_t wbase = 0;
   for (int w = 0; w < wave; w++) wbase += wsum[w];
-  boff[tid] = wbase + x - mybits;
   const uint32_t chunk_bits = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-
   const unsigned long long base = a.chunk_off[blockIdx.x];
   const uint32_t bit0 = (uint32_t)(base & 31);
   const uint32_t nw = (bit0 + chunk_bits + 31) >> 5;
   for (uint32_t i = tid; i < nw; i += 256) buf[i] = 0;
   __syncthreads();
-
-  const uint32_t zrl = tab[1][0xF0];
-  for (int i = wave; i < c.n; i += 4) {
-    const int j = c.first + i;
-    const int16_t *blk = a.coef + (long long)c.f * a.g.coef_fs + (long long)j * 64;
-    const int dd = lane == 0 ? block_dcdiff(a, c, j, blk) : 0;
-    const BlockSyms s = walk_block(blk, lane, dd);
-    const int nb = lane_bits(s, lane, tab[0], tab[1]);
-    int xs = nb;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int y = __shfl_up(xs, off);
-      if (lane >= off) xs += y;
-    }
-    uint32_t pos = bit0 + boff[i] + (uint32_t)(xs - nb);
-    if (lane == 0) {
-      const uint32_t e = tab[0][s.cls];
-      const int L = (int)(e >> 16);
-      put_bits(buf, pos, ((e & 0xFFFFu) << s.cls) | mag_bits(s.dcdiff, s.cls), L + s.cls);
-      pos += L + s.cls;
-    }
-    if (s.has_sym) {
-      const int Lz = (int)(zrl >> 16);
-      for (int k = 0; k < (s.run >> 4); k++) {
+  if (tid < c.n) {
+    uint32_t pos = bit0 + wbase + x - mybits;
+    const uint32_t *tok = a.tok + gb * 64;
+    const int hd = a.hdr[gb];
+    const int n = hd & 63;
+    uint32_t tk = tok[0];
+    int cls = (int)(tk & 255u);
+    uint32_t e = tab[0][cls];
+    int L = (int)(e >> 16);
+    put_bits(buf, pos, ((e & 0xFFFFu) << cls) | (tk >> 16), L + cls);  // :434-446
+    pos += L + cls;
+    const uint32_t zrl = tab[1][0xF0];
+    const int Lz = (int)(zrl >> 16);
+    for (int i = 1; i <= n; i++) {
+      tk = tok[i];
+      for (uint32_t k = (tk >> 8) & 3u; k; k--) {  // :490-494 ZRL
         put_bits(buf, pos, zrl & 0xFFFFu, Lz);
         pos += Lz;
       }
-      const uint32_t e = tab[1][((s.run & 15) << 4) | s.cls];
-      const int L = (int)(e >> 16);
-      put_bits(buf, pos, ((e & 0xFFFFu) << s.cls) | mag_bits(s.c, s.cls), L + s.cls);
-      pos += L + s.cls;
+      const uint32_t sym = tk & 255u;
+      cls = (int)(sym & 15u);
+      e = tab[1][sym];
+      L = (int)(e >> 16);
+      put_bits(buf, pos, ((e & 0xFFFFu) << cls) | (tk >> 16), L + cls);  // :448-460
+      pos += L + cls;
     }
-    if (lane == 63 && s.eob) {
-      const uint32_t e = tab[1][0x00];
+    if (hd & 128) {  // :479-484 EOB
+      e = tab[1][0x00];
       put_bits(buf, pos, e & 0xFFFFu, (int)(e >> 16));
     }
   }
@@ -835,6 +839,7 @@ __global__ __launch_bounds__(256) void k_pack(EntArgs a) {
     else raw[i] = buf[i];
   }
 }
+
 
 // ===========================================================================
 // k_emit: one workgroup per frame assembles the JFIF stream (encoder.c
@@ -996,7 +1001,7 @@ hipError_t launch_dc_diff(int16_t *coef, const int16_t *dc, const Geom &g, int n
   return hipGetLastError();
 }
 hipError_t launch_stats(const EntArgs &a, hipStream_t s) {
-  hipLaunchKernelGGL(k_stats, dim3(a.nframes * a.g.cpf), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_tokens, dim3(a.nframes * a.g.cpf), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_tables(const EntArgs &a, hipStream_t s) {
