@@ -157,7 +157,7 @@ def main():
 
     # correctness spot check after timing (not timed): frames vs the oracle
     verified = 0
-    if args.verify and args.mode == "encode":
+    if args.verify and args.mode == "encode" and not os.environ.get("MIJ_K1_FLAGS"):
         import oracle as O
         for i in range(min(args.verify, F)):
             if batch.output(i) != O.cref_encode(frames[i % len(frames)], args.quality):
@@ -192,7 +192,10 @@ def main():
                      "algorithmic_bytes_per_launch": int(K1_BYTES_PER_PX * px_step)},
         "stages_ms": stage_avg,
         "verified_frames": verified,
+        "fp64_replays_per_frame": round(batch.replays() / (F * (args.warmup + args.steps)), 2),
     }
+    if os.environ.get("MIJ_K1_FLAGS"):
+        res["diagnostic_k1_flags"] = int(os.environ["MIJ_K1_FLAGS"])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(frames[:4], args.cpu_seconds)
     if rank == 0:

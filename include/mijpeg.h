@@ -110,10 +110,14 @@ void mij_batch_destroy(mij_batch *b);
 int mij_batch_upload(mij_batch *b, const uint8_t *bgr, int first, int nframes);
 /* or point the batch at frames already in device memory (not owned):
  * frame i starts at d_bgr + i*frame_stride, rows pitch bytes apart
- * (pointer and pitch 4-byte aligned) */
+ * (pointer, pitch and frame stride 16-byte aligned: K1 streams rows with
+ * 16-byte LDS-DMA loads) */
 int mij_batch_set_input(mij_batch *b, const void *d_bgr, long long frame_stride,
                         int pitch);
 int mij_batch_encode(mij_batch *b, int nframes);     /* full path, async */
+/* encode also keeps the coefficient planes (for mij_batch_coefs); off by
+ * default: the fused K1 then emits symbol tokens instead of coefficients */
+int mij_batch_keep_coefs(mij_batch *b, int on);
 int mij_batch_dct(mij_batch *b, int nframes);        /* K1 only, async */
 int mij_batch_sync(mij_batch *b);
 int mij_batch_output(mij_batch *b, int frame, uint8_t *dst, size_t cap,
@@ -141,7 +145,9 @@ void *mij_batch_stream(mij_batch *b);
 /* ---- diagnostics used by the test-suite -----------------------------------*/
 /* 16x16x64 i8 MFMA layout probe: A, B are 64 lanes x 16 int8, D 64 x 4 int32 */
 int mij_probe_mfma(const int8_t *A, const int8_t *B, int32_t *D);
-/* colour-exception bitmaps as built on the device: 3 x 2048 words */
+/* colour-exception bitmaps as built on the device: 3 x 1024 words; bit
+ * (R<<7 | G>>1) of table 0 (Y), (G<<7 | B>>1) of table 1 (Cb, R == G),
+ * (G<<7 | R>>1) of table 2 (Cr, B == G); see DESIGN.md */
 int mij_colour_lut(uint32_t *out);
 /* name of the code object target the library was built for ("gfx950") */
 const char *mij_build_target(void);

@@ -18,10 +18,10 @@ namespace mij {
 // launch wrappers (mij_kernels.hip)
 int k1_grid(int device, long long ntiles);
 hipError_t launch_colour_lut(uint32_t *lut, hipStream_t s);
-hipError_t launch_k1(const K1Args &a, int grid, hipStream_t s);
+hipError_t launch_k1(const K1Args &a, int grid, int mode, hipStream_t s);
+hipError_t launch_seg_dc(const EntArgs &a, hipStream_t s);
 hipError_t launch_dc_diff(int16_t *coef, const int16_t *dc, const Geom &g, int nframes,
                           hipStream_t s);
-hipError_t launch_stats(const EntArgs &a, hipStream_t s);
 hipError_t launch_tables(const EntArgs &a, hipStream_t s);
 hipError_t launch_ehuf_struct(const HuffCode *hc, uint32_t *ehuf, hipStream_t s);
 hipError_t launch_bits(const EntArgs &a, hipStream_t s);
@@ -105,9 +105,9 @@ static Geom make_geom(int w, int h) {
   g.nblk = g.nY + 2 * g.nC;
   g.tiles_x = (w + TILE_W - 1) / TILE_W;
   g.tiles_per_frame = g.tiles_x * (h / TILE_H);
-  g.cy = (g.nY + CHUNK - 1) / CHUNK;
-  g.cc = (g.nC + CHUNK - 1) / CHUNK;
-  g.cpf = g.cy + 2 * g.cc;
+  g.nsy = (h / 8) * g.tiles_x;
+  g.nsc = (h / 16) * g.tiles_x;
+  g.nseg = g.nsy + 2 * g.nsc;
   g.coef_fs = (long long)g.nblk * 64;
   g.raw_words[0] = round_up((long long)g.nY * MAX_BLOCK_BITS / 32 + 16, 64);
   g.raw_words[1] = round_up((long long)g.nC * MAX_BLOCK_BITS / 32 + 16, 64);
@@ -147,10 +147,14 @@ static void fill_tables(int quality, Tables *t) {
       const int qz = q[c][k_zz[z]];
       t->qint[c][z] = qz;
       t->dqt[c][z] = qz;
-      t->qfac[c][z] = (float)(1.0 / (2097152.0 * qz));
-      // |N - 2^19*sum(K'X)| <= 0.5*sum|X| <= 4096, float(N) <= 64 more;
-      // t rounding <= 3 * 2^-24 * 1024; 25% margin (DESIGN.md §K1 exactness)
-      t->qtau[c][z] = (float)(1.25 * (4160.0 / (2097152.0 * qz) + 2.0e-4));
+      // z = 0 (DC) is computed exactly from the pixel sum: no fast path
+      const double fac = 1.0 / (2097152.0 * qz);
+      t->qfac[c][z] = z ? (float)fac : 0.0f;
+      // |N - 2^19*sum(K'X)| <= 0.5*sum|X| <= 4096 (+64 for float(N)), 25%
+      // margin, +1e-6 for the FP64 reference; fp32 roundings of t = N*fac and
+      // of t -+ tau stay below 1.8e-7*|t|, covered by 3e-7*|t|
+      t->qtau[c][z] = z ? (float)(1.25 * 4160.0 * fac + 1.0e-6) : 0.0f;
+      t->qrel[c][z] = z ? (float)(3.0e-7 * fac) : 0.0f;
     }
   // A fragments of v_mfma_i32_16x16x64_i8: lane l holds row (l & 15) and the
   // 16 k-values 16*(l>>4) .. +15.  Row r of M-tile m is zigzag coefficient
@@ -200,15 +204,14 @@ struct mij_batch {
   long long in_fs = 0;
   int pitch = 0;
   int16_t *d_coef = nullptr, *d_dc = nullptr;
-  uint32_t *d_hist = nullptr, *d_ehuf = nullptr, *d_bits = nullptr, *d_raw = nullptr;
-  uint32_t *d_tok = nullptr;
-  uint8_t *d_hdr = nullptr;
-  uint64_t *d_chunk_bits = nullptr, *d_chunk_off = nullptr, *d_scan_bits = nullptr,
-           *d_out_len = nullptr;
+  uint32_t *d_hist = nullptr, *d_ehuf = nullptr, *d_raw = nullptr;
+  uint32_t *d_tok = nullptr, *d_seg_ntok = nullptr, *d_seg_bits = nullptr;
+  uint64_t *d_seg_off = nullptr, *d_scan_bits = nullptr, *d_out_len = nullptr;
   HuffCode *d_hc = nullptr;
   uint8_t *d_out = nullptr;
   int *d_err = nullptr;
   unsigned *d_replays = nullptr;
+  bool keep_coefs = false;  // encode also writes coefficient planes
   bool timing = false;
   static constexpr int HIST = 64;
   hipEvent_t evh[HIST][8] = {};  // per-step events while timing is on
@@ -227,7 +230,7 @@ static void batch_free(mij_batch *b) {
   hipSetDevice(b->dev);
   if (b->stream) hipStreamSynchronize(b->stream);
   void *ptrs[] = {b->d_tab, b->own_in ? b->d_in : nullptr, b->d_coef, b->d_dc, b->d_hist,
-                  b->d_ehuf, b->d_bits, b->d_raw, b->d_tok, b->d_hdr, b->d_chunk_bits, b->d_chunk_off,
+                  b->d_ehuf, b->d_raw, b->d_tok, b->d_seg_ntok, b->d_seg_bits, b->d_seg_off,
                   b->d_scan_bits, b->d_out_len, b->d_hc, b->d_out, b->d_err, b->d_replays};
   for (void *p : ptrs)
     if (p) hipFree(p);
@@ -264,7 +267,7 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
     delete t;
     HIP_TRY(e);
     uint32_t *lut = &b->d_tab->lut[0][0];
-    HIP_TRY(hipMemsetAsync(lut, 0, sizeof(uint32_t) * 3 * 2048, b->stream));
+    HIP_TRY(hipMemsetAsync(lut, 0, sizeof(uint32_t) * 3 * LUT_WORDS, b->stream));
     HIP_TRY(launch_colour_lut(lut, b->stream));
   }
   b->pitch = w * 3;
@@ -275,12 +278,11 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
   HIP_TRY(dalloc(&b->d_dc, F * g.nblk));
   HIP_TRY(dalloc(&b->d_hist, F * 4 * 257));
   HIP_TRY(dalloc(&b->d_ehuf, F * 4 * 256));
-  HIP_TRY(dalloc(&b->d_bits, F * g.nblk));
-  HIP_TRY(dalloc(&b->d_tok, F * g.nblk * 64));
-  HIP_TRY(dalloc(&b->d_hdr, F * g.nblk));
+  HIP_TRY(dalloc(&b->d_tok, F * g.nseg * SEG_TOK));
+  HIP_TRY(dalloc(&b->d_seg_ntok, F * g.nseg));
+  HIP_TRY(dalloc(&b->d_seg_bits, F * g.nseg));
+  HIP_TRY(dalloc(&b->d_seg_off, F * g.nseg));
   HIP_TRY(dalloc(&b->d_raw, F * g.raw_fs));
-  HIP_TRY(dalloc(&b->d_chunk_bits, F * g.cpf));
-  HIP_TRY(dalloc(&b->d_chunk_off, F * g.cpf));
   HIP_TRY(dalloc(&b->d_scan_bits, F * 3));
   HIP_TRY(dalloc(&b->d_out_len, F));
   HIP_TRY(dalloc(&b->d_hc, F * 4));
@@ -327,8 +329,10 @@ extern "C" int mij_batch_upload(mij_batch *b, const uint8_t *bgr, int first, int
 
 extern "C" int mij_batch_set_input(mij_batch *b, const void *d_bgr, long long frame_stride,
                                    int pitch) {
-  if (!b || !d_bgr || ((uintptr_t)d_bgr & 3) || (pitch & 3) || pitch < b->g.w * 3)
-    return fail(MIJ_EINVAL, "set_input: pointer/pitch must be 4-byte aligned, pitch >= 3*w");
+  if (!b || !d_bgr || ((uintptr_t)d_bgr & 15) || (pitch & 15) || (frame_stride & 15) ||
+      pitch < b->g.w * 3)
+    return fail(MIJ_EINVAL, "set_input: pointer, pitch and frame stride must be 16-byte "
+                            "aligned, pitch >= 3*w");
   HIP_TRY(hipSetDevice(b->dev));
   if (b->own_in && b->d_in) HIP_TRY(hipFree(b->d_in));
   b->own_in = false;
@@ -338,20 +342,19 @@ extern "C" int mij_batch_set_input(mij_batch *b, const void *d_bgr, long long fr
   return MIJ_OK;
 }
 
-static EntArgs ent_args(mij_batch *b, int nframes, int dc_mode) {
+static EntArgs ent_args(mij_batch *b, int nframes) {
   EntArgs a;
+  memset(&a, 0, sizeof(a));
   a.g = b->g;
   a.nframes = nframes;
   a.coef = b->d_coef;
   a.dc = b->d_dc;
-  a.dc_mode = dc_mode;
   a.hist = b->d_hist;
   a.ehuf = b->d_ehuf;
-  a.bits = b->d_bits;
   a.tok = b->d_tok;
-  a.hdr = b->d_hdr;
-  a.chunk_bits = b->d_chunk_bits;
-  a.chunk_off = b->d_chunk_off;
+  a.seg_ntok = b->d_seg_ntok;
+  a.seg_bits = b->d_seg_bits;
+  a.seg_off = b->d_seg_off;
   a.scan_bits = b->d_scan_bits;
   a.raw = b->d_raw;
   a.hc = b->d_hc;
@@ -362,8 +365,11 @@ static EntArgs ent_args(mij_batch *b, int nframes, int dc_mode) {
   return a;
 }
 
-static int run_k1(mij_batch *b, int nframes) {
+// mode: K1 mode bits (1 coefficient planes out, 2 tokens + histograms out,
+// 4 coefficient planes in)
+static int run_k1(mij_batch *b, int nframes, int mode) {
   K1Args k;
+  memset(&k, 0, sizeof(k));
   k.in = b->d_in;
   k.in_fs = b->in_fs;
   k.pitch = b->pitch;
@@ -373,18 +379,29 @@ static int run_k1(mij_batch *b, int nframes) {
   k.dc = b->d_dc;
   k.tab = b->d_tab;
   k.replays = b->d_replays;
+  k.tok = b->d_tok;
+  k.seg_ntok = b->d_seg_ntok;
+  k.hist = b->d_hist;
+  static const int k1_flags = getenv("MIJ_K1_FLAGS") ? atoi(getenv("MIJ_K1_FLAGS")) : 0;
+  k.flags = k1_flags;
   const long long ntiles = (long long)nframes * b->g.tiles_per_frame;
-  HIP_TRY(launch_k1(k, k1_grid(b->dev, ntiles), b->stream));
+  long long grid = k1_grid(b->dev, ntiles);
+  long long per_wg = (ntiles + grid - 1) / grid;
+  if (per_wg > b->g.tiles_per_frame) per_wg = b->g.tiles_per_frame;  // <= 2 frames per WG
+  grid = (ntiles + per_wg - 1) / per_wg;
+  k.per_wg = (int)per_wg;
+  HIP_TRY(launch_k1(k, (int)grid, mode, b->stream));
   return MIJ_OK;
 }
 
-// stages after K1; dc_mode 0 = coefficients from K1 (raw DC + dc array)
-static int run_entropy(mij_batch *b, int nframes, int dc_mode, bool tables_given) {
-  EntArgs a = ent_args(b, nframes, dc_mode);
+// Stages after K1 emitted the token streams and histograms (the histograms
+// must have been zeroed before K1).  dc_fix: the segments' first DC tokens
+// are still to compute (K1 from pixels); tables_given: the caller's huff_code
+// structs are already in d_hc and d_ehuf (drop-in write_jpg).
+static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given) {
+  EntArgs a = ent_args(b, nframes);
   const bool t = b->timing;
-  // tokens + histograms (the histograms are unused when tables are given)
-  HIP_TRY(hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * nframes * 4 * 257, b->stream));
-  HIP_TRY(launch_stats(a, b->stream));
+  if (dc_fix) HIP_TRY(launch_seg_dc(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[2], b->stream));
   if (!tables_given) {
     HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * nframes, b->stream));
@@ -402,6 +419,14 @@ static int run_entropy(mij_batch *b, int nframes, int dc_mode, bool tables_given
   return MIJ_OK;
 }
 
+static int encode_frames(mij_batch *b, int nframes) {
+  HIP_TRY(hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * nframes * 4 * 257, b->stream));
+  if (b->timing) HIP_TRY(hipEventRecord(b->ev[0], b->stream));
+  if (run_k1(b, nframes, b->keep_coefs ? 3 : 2)) return g_err;
+  if (b->timing) HIP_TRY(hipEventRecord(b->ev[1], b->stream));
+  return run_entropy(b, nframes, true, false);
+}
+
 static void next_slot(mij_batch *b) {
   if (b->timing) b->ev = b->evh[b->steps++ % mij_batch::HIST];
 }
@@ -410,11 +435,14 @@ extern "C" int mij_batch_encode(mij_batch *b, int nframes) {
   if (!b || nframes < 1 || nframes > b->cap) return fail(MIJ_EINVAL, "encode: bad frame count");
   HIP_TRY(hipSetDevice(b->dev));
   next_slot(b);
-  if (b->timing) HIP_TRY(hipEventRecord(b->ev[0], b->stream));
-  if (run_k1(b, nframes)) return g_err;
-  if (b->timing) HIP_TRY(hipEventRecord(b->ev[1], b->stream));
-  if (run_entropy(b, nframes, 0, false)) return g_err;
+  if (encode_frames(b, nframes)) return g_err;
   b->last_frames = nframes;
+  return MIJ_OK;
+}
+
+extern "C" int mij_batch_keep_coefs(mij_batch *b, int on) {
+  if (!b) return fail(MIJ_EINVAL, "keep_coefs: null batch");
+  b->keep_coefs = on != 0;
   return MIJ_OK;
 }
 
@@ -423,7 +451,7 @@ extern "C" int mij_batch_dct(mij_batch *b, int nframes) {
   HIP_TRY(hipSetDevice(b->dev));
   next_slot(b);
   if (b->timing) HIP_TRY(hipEventRecord(b->ev[0], b->stream));
-  if (run_k1(b, nframes)) return g_err;
+  if (run_k1(b, nframes, 1)) return g_err;
   if (b->timing) HIP_TRY(hipEventRecord(b->ev[1], b->stream));
   return MIJ_OK;
 }
@@ -610,7 +638,7 @@ extern "C" void rgb_to_dct(uint8_t *in, int16_t *Y, int16_t *Cb, int16_t *Cr, ar
   mij_batch *b = ctx_for(dims.w, dims.h, g_quality);
   if (!b) return;
   if (upload_region(b, in, g_stride, dims)) return;
-  if (run_k1(b, 1)) return;
+  if (run_k1(b, 1, 1)) return;
   if (launch_dc_diff(b->d_coef, b->d_dc, b->g, 1, b->stream) != hipSuccess) {
     fail(MIJ_EHIP, "dc_diff launch failed");
     return;
@@ -635,10 +663,10 @@ extern "C" void init_huffman(int16_t *Y, int16_t *Cb, int16_t *Cr, area_t dims,
   }
   mij_batch *b = ctx_for(dims.w, dims.h, g_quality);
   if (!b || upload_planes(b, Y, Cb, Cr)) return;
-  EntArgs a = ent_args(b, 1, 1);
+  EntArgs a = ent_args(b, 1);
   if (hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * 4 * 257, b->stream) != hipSuccess ||
-      hipMemsetAsync(b->d_err, 0, sizeof(int), b->stream) != hipSuccess ||
-      launch_stats(a, b->stream) != hipSuccess || launch_tables(a, b->stream) != hipSuccess) {
+      hipMemsetAsync(b->d_err, 0, sizeof(int), b->stream) != hipSuccess || run_k1(b, 1, 6) ||
+      launch_tables(a, b->stream) != hipSuccess) {
     fail(MIJ_EHIP, "init_huffman: launch failed");
     return;
   }
@@ -678,7 +706,9 @@ extern "C" size_t write_jpg(FILE *f, uint8_t *jpg, int16_t *Y, int16_t *Cb, int1
     fail(MIJ_EHIP, "write_jpg: table upload failed");
     return 0;
   }
-  if (run_entropy(b, 1, 1, true)) return 0;
+  if (hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * 4 * 257, b->stream) != hipSuccess ||
+      run_k1(b, 1, 6) || run_entropy(b, 1, false, true))
+    return 0;
   size_t n = 0;
   if (hipStreamSynchronize(b->stream) != hipSuccess) {
     fail(MIJ_EHIP, "write_jpg: stream failed");
@@ -704,7 +734,7 @@ extern "C" int mij_encode(const uint8_t *bgr, int stride_px, area_t dims, int qu
   mij_batch *b = ctx_for(dims.w, dims.h, quality);
   if (!b) return g_err;
   if (upload_region(b, bgr, stride_px, dims)) return g_err;
-  if (run_k1(b, 1) || run_entropy(b, 1, 0, false)) return g_err;
+  if (encode_frames(b, 1)) return g_err;
   size_t n = 0;
   if (mij_batch_output(b, 0, nullptr, 0, &n)) return g_err;
   if (n > cap) return fail(MIJ_ENOSPC, "mij_encode: need %zu bytes", n);
@@ -739,7 +769,7 @@ extern "C" int mij_colour_lut(uint32_t *out) {
   mij_batch *b = ctx_for(16, 16, g_quality);
   if (!b) return g_err;
   HIP_TRY(hipStreamSynchronize(b->stream));
-  HIP_TRY(hipMemcpy(out, &b->d_tab->lut[0][0], sizeof(uint32_t) * 3 * 2048,
+  HIP_TRY(hipMemcpy(out, &b->d_tab->lut[0][0], sizeof(uint32_t) * 3 * LUT_WORDS,
                     hipMemcpyDeviceToHost));
   return MIJ_OK;
 }

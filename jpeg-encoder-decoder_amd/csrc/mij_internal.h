@@ -16,15 +16,19 @@ constexpr int TILE_H = 16;
 constexpr int LDS_BLK = 80;          // bytes per staged 8x8 block (64 + pad)
 constexpr int LDS_WAVE = 48 * LDS_BLK;  // 32 Y + 16 chroma blocks per wave
 constexpr int K1_WAVES = 4;
+constexpr int LUT_WORDS = 1024;      // 2^15 bits per colour-exception table
 
-// ---- entropy stage chunking -----------------------------------------------
-// A chunk is CHUNK consecutive blocks of ONE component of ONE frame; it is the
-// work unit of the statistics / bit-count / pack kernels and the unit of the
-// per-scan offset scan.
-constexpr int CHUNK = 256;
-constexpr int MAX_BLOCK_BITS = 1729;  // 28 DC + 63 * 27 AC bits
-// LDS words a chunk may need when packed (+2 for the unaligned head/tail)
-constexpr int CHUNK_WORDS = (CHUNK * MAX_BLOCK_BITS + 31) / 32 + 2;
+// ---- entropy stage: segments ---------------------------------------------
+// A segment is the run of blocks one K1 N-tile covers in a component's scan
+// order: 16 luma blocks of a block row, or 8 Cb / 8 Cr blocks of an MCU row.
+// K1 writes each segment's tokens compacted into a slot of SEG_TOK tokens;
+// k_pack packs PACK_SEGS consecutive segments of a scan per workgroup.
+constexpr int MAX_BLOCK_TOK = 65;                 // DC + 63 AC + EOB
+constexpr int SEG_TOK = 16 * MAX_BLOCK_TOK;       // 1040 tokens per segment slot
+constexpr int SEG_PER_WG = 64;                    // k_seg_bits segments per workgroup
+constexpr int PACK_SEGS = 16;                     // segments per k_pack workgroup
+constexpr int MAX_BLOCK_BITS = 1729;              // 28 DC + 63 * 27 AC bits
+constexpr int PACK_WORDS = (PACK_SEGS * 16 * MAX_BLOCK_BITS + 31) / 32 + 2;
 
 // Layout-identical to the reference huff_code (include/structs.h:5-13).
 struct HuffCode {
@@ -43,7 +47,7 @@ struct Geom {
   int w, h;             // multiples of 16
   int nY, nC, nblk;     // 8x8 blocks: luma, per chroma plane, total
   int tiles_x, tiles_per_frame;
-  int cy, cc, cpf;      // chunks: luma, per chroma plane, per frame
+  int nsy, nsc, nseg;   // segments: luma, per chroma plane, per frame
   long long coef_fs;    // coefficient elements per frame = nblk * 64
   long long raw_words[3];   // raw bit-buffer capacity per component (words)
   long long raw_fs;         // words per frame
@@ -54,11 +58,12 @@ struct Geom {
 struct Tables {
   int4 mfma_a[12 * 64];   // A fragments: 4 M-tiles x 3 digits x 64 lanes
   float qfac[2][64];      // zigzag order: 1 / (2^21 * q)
-  float qtau[2][64];      // zigzag order: proven error bound (t units)
+  float qtau[2][64];      // zigzag order: proven error bound, constant part (t units)
+  float qrel[2][64];      // zigzag order: error bound per unit |N| (fp32 rounding)
   int qint[2][64];        // zigzag order: integer quantizer
   int dqt[2][64];         // zigzag order: DQT bytes
   double cosd[64];        // encoder.c:8-16 constants
-  uint32_t lut[3][2048];  // colour-exception bitmaps (Y by R,G; Cb by G,B; Cr by G,R)
+  uint32_t lut[3][1024];  // colour-exception bitmaps (Y by R,G/2; Cb by G,B/2; Cr by G,R/2)
 };
 
 struct K1Args {
@@ -71,21 +76,27 @@ struct K1Args {
   int16_t *dc;              // per frame: raw (un-differenced) DC per block
   const Tables *tab;
   unsigned int *replays;    // count of coefficients replayed in FP64
+  int flags;                // diagnostics only (MIJ_K1_FLAGS): K1F_* bits
+  int per_wg;               // tiles per workgroup (<= tiles_per_frame)
+  uint32_t *tok;            // token mode: per segment SEG_TOK tokens
+  uint32_t *seg_ntok;       // token mode: tokens per segment
+  uint32_t *hist;           // token mode: per frame [4][257] histograms
 };
+// K1 diagnostic switches (timing attribution; outputs are wrong when set)
+constexpr int K1F_NO_LUT = 1, K1F_NO_REPLAY = 2, K1F_NO_COLOUR = 4, K1F_NO_DCT = 8,
+              K1F_NO_STORE = 16;
 
 struct EntArgs {
   Geom g;
   int nframes;
   const int16_t *coef;
-  const int16_t *dc;        // raw DCs (dc_mode 0)
-  int dc_mode;              // 0: DC raw, diff from dc[]; 1: coef holds DC diff
+  const int16_t *dc;        // raw DC per block (K1)
   uint32_t *hist;           // per frame [4][257]
   const uint32_t *ehuf;     // per frame [4][256] = len << 16 | code
-  uint32_t *tok;            // per block 64 tokens (k_tokens)
-  uint8_t *hdr;             // per block: #AC tokens | EOB << 7
-  uint32_t *bits;           // per block (frame-major)
-  uint64_t *chunk_bits;     // per chunk
-  uint64_t *chunk_off;      // per chunk: bit offset inside its scan
+  uint32_t *tok;            // per segment SEG_TOK tokens
+  const uint32_t *seg_ntok; // per segment token count
+  uint32_t *seg_bits;       // per segment bits
+  uint64_t *seg_off;        // per segment bit offset inside its scan
   uint64_t *scan_bits;      // per frame [3]
   uint32_t *raw;            // per frame: 3 component bit buffers (big-endian words)
   const HuffCode *hc;       // per frame [4]

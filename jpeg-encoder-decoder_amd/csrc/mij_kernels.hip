@@ -6,12 +6,14 @@
 //                  -> quantize/trunc (+FP64 replay near boundaries) -> zigzag
 //                  (encoder.c:121-150, :81-112, :65-70)
 //   k_dc_diff      DC differencing into the coefficient planes (:168-177)
-//   k_tokens       per-block symbol lists + histograms (:315-358, :462-502)
+//                  and (token mode) per-segment symbol streams + histograms
+//                  (:315-358, :462-502)
+//   k_seg_dc       DC token of each segment's first block (:168-177)
 //   k_tables       optimized Huffman tables, wave-parallel (:180-301)
 //   k_ehuf_struct  code tables from caller-owned huff_code structs
-//   k_bits         bits per block
-//   k_scan         per-scan offsets of each chunk
-//   k_pack         bit packing of each chunk in LDS (:434-502)
+//   k_seg_bits     bits per segment
+//   k_scan         per-scan offsets of each segment
+//   k_pack         bit packing of segment groups in LDS (:434-502)
 //   k_emit         JFIF assembly + 0xFF stuffing + pad quirks (:383-432,
 //                  :504-644)
 //
@@ -44,50 +46,62 @@ __device__ __forceinline__ int mag_class(int v) {  // encoder.c:303-313
   return 32 - __clz(v);
 }
 
+// Magnitude bits of a value of class cls (encoder.c:442-444 / :456-458:
+// negative values are written as ~|v|, i.e. the low cls bits of v-1).
+__device__ __forceinline__ uint32_t mag_bits(int v, int cls) {
+  uint32_t id = (uint32_t)(v < 0 ? -v : v);
+  if (v < 0) id = ~id;
+  return id & ((1u << cls) - 1u);
+}
+
 // ===========================================================================
 // Colour-exception bitmaps.  Exact-integer colour values for which the FP64
 // expression of encoder.c:133-135 lands one ulp-ish below the integer, so the
 // uint8_t truncation yields value-1.  Y indexed by (R,G) (the B of an integer
 // point is unique), Cb by (G,B) with R==G, Cr by (G,R) with B==G.
 // ===========================================================================
-__global__ void k_colour_lut(uint32_t *lut /* [3][2048] */) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;  // 0 .. 65535
-  if (i >= 65536) return;
-  int hi = i >> 8, lo = i & 255;
+__global__ void k_colour_lut(uint32_t *lut /* [3][LUT_WORDS] */) {
+  // An exact-integer colour value needs equal parities: Y: 299R+587G+114B
+  // == 0 (mod 1000) forces R == G (mod 2); Cb needs R == G and B == G (mod
+  // 2); Cr needs B == G and R == G (mod 2).  So each table has 2^15 entries:
+  // Y by (R, G>>1), Cb by (G, B>>1), Cr by (G, R>>1).
+  int i = blockIdx.x * blockDim.x + threadIdx.x;  // 0 .. 32767
+  if (i >= 32768) return;
+  const int hi = i >> 7, lo = i & 127;
   bool ey = false, ecb = false, ecr = false;
-  {  // Y: (R,G) = (hi,lo)
-    int R = hi, G = lo;
+  {  // Y: R = hi, G = 2*lo + (R & 1)
+    const int R = hi, G = 2 * lo + (R & 1);
     for (int B = 0; B < 256; B++) {
-      int n = 299 * R + 587 * G + 114 * B;
+      const int n = 299 * R + 587 * G + 114 * B;
       if (n % 1000) continue;
-      double y = __dadd_rn(__dadd_rn(__dmul_rn(0.299, (double)R), __dmul_rn(0.587, (double)G)),
-                           __dmul_rn(0.114, (double)B));
+      const double y = __dadd_rn(__dadd_rn(__dmul_rn(0.299, (double)R), __dmul_rn(0.587, (double)G)),
+                                 __dmul_rn(0.114, (double)B));
       ey = (int)y != n / 1000;
     }
   }
-  {  // Cb: (G,B) = (hi,lo), R = G
-    int G = hi, B = lo, R = G;
-    long long n = 128000000LL - 168736LL * R - 331264LL * G + 500000LL * B;
+  {  // Cb: G = hi, B = 2*lo + (G & 1), R = G
+    const int G = hi, B = 2 * lo + (G & 1), R = G;
+    const long long n = 128000000LL - 168736LL * R - 331264LL * G + 500000LL * B;
     if (n % 1000000 == 0) {
-      double cb = __dadd_rn(__dadd_rn(__dadd_rn(128.0, -__dmul_rn(0.168736, (double)R)),
-                                      -__dmul_rn(0.331264, (double)G)),
-                            __dmul_rn(0.5, (double)B));
+      const double cb = __dadd_rn(__dadd_rn(__dadd_rn(128.0, -__dmul_rn(0.168736, (double)R)),
+                                            -__dmul_rn(0.331264, (double)G)),
+                                  __dmul_rn(0.5, (double)B));
       ecb = (int)cb != (int)(n / 1000000);
     }
   }
-  {  // Cr: (G,R) = (hi,lo), B = G
-    int G = hi, R = lo, B = G;
-    long long n = 128000000LL + 500000LL * R - 418688LL * G - 81312LL * B;
+  {  // Cr: G = hi, R = 2*lo + (G & 1), B = G
+    const int G = hi, R = 2 * lo + (G & 1), B = G;
+    const long long n = 128000000LL + 500000LL * R - 418688LL * G - 81312LL * B;
     if (n % 1000000 == 0) {
-      double cr = __dadd_rn(__dadd_rn(__dadd_rn(128.0, __dmul_rn(0.5, (double)R)),
-                                      -__dmul_rn(0.418688, (double)G)),
-                            -__dmul_rn(0.081312, (double)B));
+      const double cr = __dadd_rn(__dadd_rn(__dadd_rn(128.0, __dmul_rn(0.5, (double)R)),
+                                            -__dmul_rn(0.418688, (double)G)),
+                                  -__dmul_rn(0.081312, (double)B));
       ecr = (int)cr != (int)(n / 1000000);
     }
   }
-  if (ey) atomicOr(&lut[0 * 2048 + (i >> 5)], 1u << (i & 31));
-  if (ecb) atomicOr(&lut[1 * 2048 + (i >> 5)], 1u << (i & 31));
-  if (ecr) atomicOr(&lut[2 * 2048 + (i >> 5)], 1u << (i & 31));
+  if (ey) atomicOr(&lut[0 * LUT_WORDS + (i >> 5)], 1u << (i & 31));
+  if (ecb) atomicOr(&lut[1 * LUT_WORDS + (i >> 5)], 1u << (i & 31));
+  if (ecr) atomicOr(&lut[2 * LUT_WORDS + (i >> 5)], 1u << (i & 31));
 }
 
 // ===========================================================================
@@ -101,24 +115,25 @@ __global__ void k_colour_lut(uint32_t *lut /* [3][2048] */) {
 // precomputed bitmaps say whether the FP64 reference lands one below.
 __device__ __forceinline__ void pixel_ycc(uint32_t B, uint32_t G, uint32_t R,
                                           const uint32_t *__restrict__ lut,
-                                          int &y, int &cb, int &cr) {
+                                          int &y, int &cb, int &cr, bool use_lut = true) {
   float fb = (float)B, fg = (float)G, fr = (float)R;
   float dr = fr - fg, db = fb - fg;
   float yf = fmaf(0.114f, db, fmaf(0.299f, dr, fg)) + 0.0005f;
   y = (int)yf;
   cb = (int)fmaf(-0.168736f, dr, fmaf(0.5f, db, 128.0f));
   cr = (int)fmaf(-0.081312f, db, fmaf(0.5f, dr, 128.0f));
-  if (yf - (float)y < 0.001f) {
-    uint32_t i = (R << 8) | G;
+  if (!use_lut) return;
+  if (__builtin_amdgcn_fractf(yf) < 0.001f) {  // exact-integer Y: R, G same parity
+    const uint32_t i = (R << 7) | (G >> 1);
     y -= (lut[i >> 5] >> (i & 31)) & 1;
   }
-  if (dr == 0.0f) {
-    uint32_t i = (G << 8) | B;
-    cb -= (lut[2048 + (i >> 5)] >> (i & 31)) & 1;
+  if (dr == 0.0f) {  // only R == G can give an integer Cb
+    const uint32_t i = (G << 7) | (B >> 1);
+    cb -= (lut[LUT_WORDS + (i >> 5)] >> (i & 31)) & ((B ^ G) & 1 ? 0u : 1u);
   }
-  if (db == 0.0f) {
-    uint32_t i = (G << 8) | R;
-    cr -= (lut[4096 + (i >> 5)] >> (i & 31)) & 1;
+  if (db == 0.0f) {  // only B == G can give an integer Cr
+    const uint32_t i = (G << 7) | (R >> 1);
+    cr -= (lut[2 * LUT_WORDS + (i >> 5)] >> (i & 31)) & ((R ^ G) & 1 ? 0u : 1u);
   }
 }
 
@@ -134,206 +149,403 @@ __device__ __forceinline__ int dc_exact(int S, int q) {
 
 // One AC coefficient replayed exactly as encoder.c:87-109 computes it
 // (column pass summed from 0 in y order, row pass in x order, FP64, no FMA).
-__device__ __noinline__ int ac_exact(const uint8_t *blk, int z, int q,
-                                     const double *__restrict__ C) {
-  int rz = c_zigzag[z];
-  int v = rz >> 3, u = rz & 7;
+// C = the 64 cosines (LDS), blk = the block's 64 staged pixels (LDS).
+__device__ __forceinline__ int ac_exact(const uint8_t *blk, int z, int q, const double *C) {
+  const int rz = c_zigzag[z];
+  const int v = rz >> 3, u = rz & 7;
+  double cv[8];
+#pragma unroll
+  for (int y = 0; y < 8; y++) cv[y] = C[y * 8 + v];
+  uint64_t rows[8];
+#pragma unroll
+  for (int y = 0; y < 8; y++) rows[y] = *(const uint64_t *)(blk + y * 8);
   double freq = 0.0;
-  for (int x = 0; x < 8; x++) {
+#pragma unroll 1
+  for (int x = 0; x < 8; x++) {  // rare path: keep register pressure low
     double inner = 0.0;
+#pragma unroll
     for (int y = 0; y < 8; y++)
-      inner = __dadd_rn(inner, __dmul_rn((double)((int)blk[y * 8 + x] - 128), C[y * 8 + v]));
+      inner = __dadd_rn(inner, __dmul_rn((double)((int)((rows[y] >> (8 * x)) & 255) - 128), cv[y]));
     freq = __dadd_rn(freq, __dmul_rn(inner, C[x * 8 + u]));
   }
   if (u == 0) freq = __dmul_rn(freq, SQRT1_2);
   if (v == 0) freq = __dmul_rn(freq, SQRT1_2);
   freq = __dmul_rn(freq, 0.25);
-  int t = (int)__ddiv_rn(freq, (double)q);
+  const int t = (int)__ddiv_rn(freq, (double)q);
   return t < -2048 ? -2048 : (t > 2047 ? 2047 : t);
 }
 
 // ===========================================================================
 // K1: fused colour conversion + 4:2:0 + DCT + quantization + zigzag.
 //
-// Persistent grid; each wave owns one 128x16 tile at a time:
-//   1. 64 lanes load the tile's 16 rows of BGR888 (12 B = 4 px per lane and
-//      row, coalesced), convert two 4x1 pixel runs (a 4x2 patch) per step,
-//      average the two 2x2 chroma quads, and stage Y/Cb/Cr bytes in LDS in
-//      block-major order (64 px per 8x8 block, LDS_BLK stride).
+// Persistent grid; workgroup w owns a contiguous range of 128x16 tiles and
+// its 4 waves take every 4th tile of it.  Per tile a wave:
+//   1. the tile's 16 rows of BGR888 arrive in LDS by LDS-DMA, issued while
+//      the previous tile was in its DCT phase; each lane reads 12 B = 4 px
+//      per row, converts a 4x2 patch per step, averages the
+//      two 2x2 chroma quads, and stages Y/Cb/Cr bytes in LDS in block-major
+//      order (64 px per 8x8 block, LDS_BLK stride).
 //   2. three MFMA N-tiles of 16 blocks (Y block row 0, Y block row 1,
 //      Cb|Cr): v_mfma_i32_16x16x64_i8 with B = the blocks' pixels - 128
 //      (exact int8) and A = the 64x64 DCT matrix (rows in zigzag order,
-//      cos*cos*scale * 2^19 rounded) split into three base-128 digits.  The
-//      int32 sum N is exact; N / 2^21 is the un-quantized coefficient to
-//      within 0.002, and the DC row holds the exact pixel sum.
+//      cos*cos*scale * 2^19 rounded) split into three base-128 digits, read
+//      from LDS.  The int32 sum N is exact; N / 2^21 is the un-quantized
+//      coefficient to within 0.002, and the DC row holds the
+//      exact pixel sum.
 //   3. quantize with trunc; a coefficient whose +-tau interval straddles a
 //      truncation boundary is recomputed in FP64 exactly like the reference.
 //   4. lane (g, b) owns zigzag coefficients 16g..16g+15 of block b: two
 //      16-byte stores per lane.
 // ===========================================================================
-__global__ __launch_bounds__(256) void k_mcu_dct(K1Args a) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_tile[K1_WAVES][LDS_WAVE];
-  __shared__ uint32_t s_lut[3 * 2048];
+struct TilePos {
+  int f, tx, ty, valid_px;
+};
+
+__device__ __forceinline__ TilePos tile_pos(const Geom &G, int t) {
+  TilePos p;
+  p.f = t / G.tiles_per_frame;
+  const int rem = t - p.f * G.tiles_per_frame;
+  p.ty = rem / G.tiles_x;
+  p.tx = rem - p.ty * G.tiles_x;
+  p.valid_px = min(TILE_W, G.w - p.tx * TILE_W);
+  return p;
+}
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void global_void_t;
+constexpr int TILE_RAW = TILE_W * 3 * TILE_H;  // 6144 B of BGR888 per tile
+
+// Streams a tile's 16 rows x 384 B into LDS with global_load_lds_dwordx4 (no
+// VGPRs): instruction k moves LDS bytes [1024k, 1024k+1024), lane i the 16 B
+// at tile offset 1024k + 16i (a 384-B row holds exactly 24 such pieces).
+__device__ __forceinline__ void issue_tile_dma(const K1Args &a, const TilePos &p, int lane,
+                                               uint8_t *raw) {
+  const uint8_t *src = a.in + (long long)p.f * a.in_fs + (long long)(p.ty * TILE_H) * a.pitch +
+                       p.tx * TILE_W * 3;
+  const int vb = p.valid_px * 3;
+#pragma unroll
+  for (int k = 0; k < TILE_RAW / 1024; k++) {
+    const int pos = 1024 * k + 16 * lane;
+    const int row = pos / (TILE_W * 3), col = pos - row * (TILE_W * 3);
+    if (col < vb)
+      __builtin_amdgcn_global_load_lds((global_void_t *)(src + (long long)row * a.pitch + col),
+                                       (lds_void_t *)(raw + 1024 * k), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int c4, int pr,
+                                             const uint32_t *__restrict__ lut, bool use_lut) {
+#pragma unroll
+  for (int it = 0; it < 4; it++) {
+    const int rp = 2 * it + pr;  // row pair 0..7 == chroma row
+    int cbs[2][4], crs[2][4];
+#pragma unroll
+    for (int dy = 0; dy < 2; dy++) {
+      const uint32_t *rw = (const uint32_t *)(raw + (2 * rp + dy) * (TILE_W * 3) + 12 * c4);
+      const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2];
+      int y0, y1, y2, y3;
+      pixel_ycc(w0 & 255, (w0 >> 8) & 255, (w0 >> 16) & 255, lut, y0, cbs[dy][0], crs[dy][0], use_lut);
+      pixel_ycc(w0 >> 24, w1 & 255, (w1 >> 8) & 255, lut, y1, cbs[dy][1], crs[dy][1], use_lut);
+      pixel_ycc((w1 >> 16) & 255, w1 >> 24, w2 & 255, lut, y2, cbs[dy][2], crs[dy][2], use_lut);
+      pixel_ycc((w2 >> 8) & 255, (w2 >> 16) & 255, w2 >> 24, lut, y3, cbs[dy][3], crs[dy][3], use_lut);
+      const int yrow = 2 * rp + dy;  // 0..15
+      const int by = yrow >> 3, bx = c4 >> 1;
+      const uint32_t packed = (uint32_t)y0 | ((uint32_t)y1 << 8) | ((uint32_t)y2 << 16) |
+                              ((uint32_t)y3 << 24);
+      *(uint32_t *)(L + (by * 16 + bx) * LDS_BLK + (yrow & 7) * 8 + (c4 & 1) * 4) = packed;
+    }
+    // encoder.c:137-138 -- floor((a+b+c+d)/4) of the truncated values
+    const uint32_t cb0 = (uint32_t)(cbs[0][0] + cbs[0][1] + cbs[1][0] + cbs[1][1]) >> 2;
+    const uint32_t cb1 = (uint32_t)(cbs[0][2] + cbs[0][3] + cbs[1][2] + cbs[1][3]) >> 2;
+    const uint32_t cr0 = (uint32_t)(crs[0][0] + crs[0][1] + crs[1][0] + crs[1][1]) >> 2;
+    const uint32_t cr1 = (uint32_t)(crs[0][2] + crs[0][3] + crs[1][2] + crs[1][3]) >> 2;
+    uint8_t *C0 = L + (32 + (c4 >> 2)) * LDS_BLK + rp * 8 + ((2 * c4) & 7);
+    *(uint16_t *)C0 = (uint16_t)(cb0 | (cb1 << 8));
+    *(uint16_t *)(C0 + 8 * LDS_BLK) = (uint16_t)(cr0 | (cr1 << 8));
+  }
+}
+
+// Token of the per-segment streams: symbol (bits 0-7) | ZRL count before it
+// (bits 8-9) | TOK_AC for the AC table (bit 10) | magnitude bits (16-27).
+// Bit length = code length + (symbol & 15) + ZRLs * ZRL code length for
+// every token kind (DC: symbol = class <= 11; EOB: symbol 0x00).
+constexpr uint32_t TOK_AC = 1u << 10;
+
+// One N-tile of coefficients -> compacted token stream of its segment(s).
+// o[k] = zigzag coefficient 16g+k of block bcol (DC raw in o[0] of g == 0,
+// or the DC difference when dc_diffed).  Every lane of the wave calls this.
+// Tokens of a block, in bitstream order (encoder.c:462-502): its DC
+// difference (:434-446), the AC run/size symbols (:448-460, ZRLs folded in,
+// :490-494), then EOB unless coefficient 63 is nonzero (:479-484).  The DC of
+// a segment's first block depends on the previous segment, so unless
+// dc_diffed it is left for k_seg_dc.
+__device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g, int bcol,
+                                            bool valid, bool chroma, bool dc_diffed,
+                                            uint32_t *segtok, uint32_t *segcnt, uint32_t *hDC,
+                                            uint32_t *hAC, int16_t (*st)[16]) {
+  u4v c0, c1;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    c0[k] = (uint32_t)(uint16_t)o[2 * k] | ((uint32_t)o[2 * k + 1] << 16);
+    c1[k] = (uint32_t)(uint16_t)o[8 + 2 * k] | ((uint32_t)o[9 + 2 * k] << 16);
+  }
+  *(u4v *)&st[lane][0] = c0;
+  *(u4v *)&st[lane][8] = c1;
+  uint32_t m16 = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) m16 |= (o[k] != 0 ? 1u : 0u) << k;
+  if (g == 0) m16 &= ~1u;  // the DC is not part of the AC run structure
+  unsigned long long M = (unsigned long long)m16 << (16 * g);
+  M |= __shfl_xor(M, 16);
+  M |= __shfl_xor(M, 32);
+  const int eob = !((M >> 63) & 1ull);
+  const int n = valid ? 1 + __popcll(M) + eob : 0;
+  // token offsets of the blocks inside their segment (chroma rows hold two
+  // 8-block segments: Cb | Cr)
+  const int pos = chroma ? (bcol & 7) : bcol;
+  int incl = n;
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1) {
+    const int y = __shfl_up(incl, off, 16);
+    if (pos >= off) incl += y;
+  }
+  const int base = incl - n;
+  const int dc0 = o[0];
+  const int prev = __shfl_up(dc0, 1, 16);
+  wave_lds_sync();
+  if (g == 0) {
+    if (pos == (chroma ? 7 : 15)) *segcnt = (uint32_t)incl;
+    if (valid) {
+      if (dc_diffed || pos != 0) {
+        const int diff = dc_diffed ? dc0 : dc0 - prev;  // :168-177
+        const int cls = mag_class(diff);
+        segtok[base] = (uint32_t)cls | (mag_bits(diff, cls) << 16);
+        atomicAdd(&hDC[cls], 1u);
+      }
+      if (eob) {
+        segtok[base + n - 1] = TOK_AC;
+        atomicAdd(&hAC[0x00], 1u);
+      }
+    }
+  }
+  if (valid) {  // lane (g, b) takes the zigzag positions z == g (mod 4)
+    unsigned long long mm = M & (0x1111111111111111ull << g);
+    while (mm) {
+      const int z = __ffsll((long long)mm) - 1;
+      mm &= mm - 1ull;
+      const int cz = st[(z >> 4) * 16 + bcol][z & 15];
+      const unsigned long long before = M & ((1ull << z) - 1ull);
+      const int run = z - (63 - __clzll(before | 1ull)) - 1;
+      const int cls = mag_class(cz);
+      const int sym = ((run & 15) << 4) | cls;
+      segtok[base + 1 + __popcll(before)] =
+          (uint32_t)sym | ((uint32_t)(run >> 4) << 8) | TOK_AC | (mag_bits(cz, cls) << 16);
+      atomicAdd(&hAC[sym], 1u);
+      if (run >= 16) atomicAdd(&hAC[0xF0], (unsigned)(run >> 4));
+    }
+  }
+  wave_lds_sync();
+}
+
+// K1 modes
+constexpr int K1M_COEF_OUT = 1;  // write zigzag coefficient planes
+constexpr int K1M_TOK_OUT = 2;   // write per-segment token streams + histograms
+constexpr int K1M_COEF_IN = 4;   // read coefficient planes (DC differences) instead of pixels
+
+template <int MODE>
+__global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
+  constexpr bool PIX = !(MODE & K1M_COEF_IN);
+  constexpr bool TOK = MODE & K1M_TOK_OUT;
+  __shared__ __attribute__((aligned(16))) uint8_t s_raw[PIX ? K1_WAVES : 1][TILE_RAW];
+  __shared__ __attribute__((aligned(16))) uint8_t s_tile[PIX ? K1_WAVES : 1][LDS_WAVE];
+  __shared__ __attribute__((aligned(16))) int4 s_A[PIX ? 12 * 64 : 1];
   __shared__ __attribute__((aligned(16))) float s_fac[2][64];
   __shared__ __attribute__((aligned(16))) float s_tau[2][64];
+  __shared__ __attribute__((aligned(16))) float s_rel[2][64];
+  __shared__ uint32_t s_lut[PIX ? 3 * LUT_WORDS : 1];
+  __shared__ double s_cos[64];
+  __shared__ int s_qint[2][64];
+  __shared__ __attribute__((aligned(16))) int16_t s_st[K1_WAVES][64][16];  // replays / tokens
+  // per-frame histograms of this workgroup: [frame slot][luma, chroma][symbol]
+  __shared__ uint32_t s_hac[TOK ? 2 : 1][2][256];
+  __shared__ uint32_t s_hdc[TOK ? 2 : 1][2][16];
 
   const Tables *__restrict__ T = a.tab;
-  for (int i = threadIdx.x; i < 3 * 2048; i += 256) s_lut[i] = (&T->lut[0][0])[i];
+  if (threadIdx.x < 64) s_cos[threadIdx.x] = T->cosd[threadIdx.x];
+  if (TOK) {
+    for (int i = threadIdx.x; i < 2 * 2 * 256; i += 256) (&s_hac[0][0][0])[i] = 0;
+    if (threadIdx.x < 64) (&s_hdc[0][0][0])[threadIdx.x] = 0;
+  }
+  if (threadIdx.x < 128) s_qint[threadIdx.x >> 6][threadIdx.x & 63] = T->qint[threadIdx.x >> 6][threadIdx.x & 63];
+  if (PIX) {
+    for (int i = threadIdx.x; i < 12 * 64; i += 256) s_A[i] = T->mfma_a[i];
+    for (int i = threadIdx.x; i < 3 * LUT_WORDS; i += 256) s_lut[i] = (&T->lut[0][0])[i];
+  }
   for (int i = threadIdx.x; i < 128; i += 256) {
     s_fac[i >> 6][i & 63] = T->qfac[i >> 6][i & 63];
     s_tau[i >> 6][i & 63] = T->qtau[i >> 6][i & 63];
+    s_rel[i >> 6][i & 63] = T->qrel[i >> 6][i & 63];
   }
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint8_t *L = s_tile[wave];
+  uint8_t *L = s_tile[PIX ? wave : 0];
   const int g = lane >> 4, bcol = lane & 15;
+  const int c4 = lane & 31, pr = lane >> 5;
   const int q_dc[2] = {T->qint[0][0], T->qint[1][0]};
-
-  v4i A[12];
-#pragma unroll
-  for (int i = 0; i < 12; i++) {
-    int4 t = T->mfma_a[i * 64 + lane];
-    A[i] = v4i{t.x, t.y, t.z, t.w};
-  }
-
   const Geom G = a.g;
   const int bw = G.w >> 3, mw = G.w >> 4;
-  const long long ntiles = (long long)a.nframes * G.tiles_per_frame;
-  const int c4 = lane & 31, pr = lane >> 5;
-
-  for (long long t = (long long)blockIdx.x * K1_WAVES + wave; t < ntiles;
-       t += (long long)gridDim.x * K1_WAVES) {
-    const int f = (int)(t / G.tiles_per_frame);
-    const int rem = (int)(t - (long long)f * G.tiles_per_frame);
-    const int ty = rem / G.tiles_x, tx = rem - ty * G.tiles_x;
-    const int valid_px = min(TILE_W, G.w - tx * TILE_W);
-    const uint8_t *src = a.in + (long long)f * a.in_fs + (long long)(ty * TILE_H) * a.pitch +
-                         tx * TILE_W * 3;
-
-    // ---- 1. load + colour convert + subsample + stage --------------------
-    const bool colv = 4 * c4 < valid_px;
-    uint32_t d[4][2][3];
-#pragma unroll
-    for (int it = 0; it < 4; it++)
-#pragma unroll
-      for (int dy = 0; dy < 2; dy++) {
-        const int row = 2 * (2 * it + pr) + dy;
-        if (colv) {
-          const uint32_t *p = (const uint32_t *)(src + (long long)row * a.pitch + 12 * c4);
-          d[it][dy][0] = __builtin_nontemporal_load(p);
-          d[it][dy][1] = __builtin_nontemporal_load(p + 1);
-          d[it][dy][2] = __builtin_nontemporal_load(p + 2);
-        } else {
-          d[it][dy][0] = d[it][dy][1] = d[it][dy][2] = 0;
+  const int ntiles = a.nframes * G.tiles_per_frame;
+  const int t0 = (int)blockIdx.x * a.per_wg;  // per_wg <= tiles_per_frame:
+  const int f0 = t0 / G.tiles_per_frame;      // a workgroup spans <= 2 frames
+  const int tend = min(ntiles, t0 + a.per_wg);
+  int t = t0 + wave;
+  if (t < tend) {
+    uint8_t *raw = s_raw[PIX ? wave : 0];
+    TilePos p = tile_pos(G, t);
+    if (PIX) issue_tile_dma(a, p, lane, raw);
+    for (; t < tend; t += K1_WAVES) {
+      TilePos pn = p;
+      if (PIX) {
+        // ---- 1. colour convert + subsample + stage (waits for this tile's DMA)
+        if (!(a.flags & K1F_NO_COLOUR)) colour_stage(raw, L, c4, pr, s_lut, !(a.flags & K1F_NO_LUT));
+        wave_lds_sync();
+        // ---- stream the wave's next tile into the freed raw buffer -----------
+        if (t + K1_WAVES < tend) {
+          pn = tile_pos(G, t + K1_WAVES);
+          issue_tile_dma(a, pn, lane, raw);
         }
+      } else if (t + K1_WAVES < tend) {
+        pn = tile_pos(G, t + K1_WAVES);
       }
-#pragma unroll
-    for (int it = 0; it < 4; it++) {
-      const int rp = 2 * it + pr;  // row pair 0..7 == chroma row
-      int cbs[2][4], crs[2][4];
-#pragma unroll
-      for (int dy = 0; dy < 2; dy++) {
-        const uint32_t w0 = d[it][dy][0], w1 = d[it][dy][1], w2 = d[it][dy][2];
-        int y0, y1, y2, y3;
-        pixel_ycc(w0 & 255, (w0 >> 8) & 255, (w0 >> 16) & 255, s_lut, y0, cbs[dy][0], crs[dy][0]);
-        pixel_ycc(w0 >> 24, w1 & 255, (w1 >> 8) & 255, s_lut, y1, cbs[dy][1], crs[dy][1]);
-        pixel_ycc((w1 >> 16) & 255, w1 >> 24, w2 & 255, s_lut, y2, cbs[dy][2], crs[dy][2]);
-        pixel_ycc((w2 >> 8) & 255, (w2 >> 16) & 255, w2 >> 24, s_lut, y3, cbs[dy][3], crs[dy][3]);
-        const int yrow = 2 * rp + dy;  // 0..15
-        const int by = yrow >> 3, bx = c4 >> 1;
-        uint32_t packed = (uint32_t)y0 | ((uint32_t)y1 << 8) | ((uint32_t)y2 << 16) |
-                          ((uint32_t)y3 << 24);
-        *(uint32_t *)(L + (by * 16 + bx) * LDS_BLK + (yrow & 7) * 8 + (c4 & 1) * 4) = packed;
-      }
-      // encoder.c:137-138 -- floor((a+b+c+d)/4) of the truncated values
-      const uint32_t cb0 = (uint32_t)(cbs[0][0] + cbs[0][1] + cbs[1][0] + cbs[1][1]) >> 2;
-      const uint32_t cb1 = (uint32_t)(cbs[0][2] + cbs[0][3] + cbs[1][2] + cbs[1][3]) >> 2;
-      const uint32_t cr0 = (uint32_t)(crs[0][0] + crs[0][1] + crs[1][0] + crs[1][1]) >> 2;
-      const uint32_t cr1 = (uint32_t)(crs[0][2] + crs[0][3] + crs[1][2] + crs[1][3]) >> 2;
-      const int cblk = c4 >> 2, ccol = (2 * c4) & 7;
-      uint8_t *C0 = L + (32 + cblk) * LDS_BLK + rp * 8 + ccol;
-      *(uint16_t *)C0 = (uint16_t)(cb0 | (cb1 << 8));
-      *(uint16_t *)(C0 + 8 * LDS_BLK) = (uint16_t)(cr0 | (cr1 << 8));
-    }
-    wave_lds_sync();
 
-    // ---- 2-4. DCT on MFMA, quantize, store -------------------------------
+      // ---- 2-4. DCT on MFMA, quantize, emit ----------------------------------
 #pragma unroll 1
-    for (int nt = 0; nt < 3; nt++) {
-      const int comp = nt == 2 ? 1 : 0;
-      const uint8_t *Pb = L + (nt * 16 + bcol) * LDS_BLK;
-      v4i Bf = *(const v4i *)(Pb + 16 * g);
-      Bf ^= (int)0x80808080;  // pixel - 128 as int8
-
-      bool valid;
-      long long blk;  // block index inside the frame's coefficient space
-      if (nt < 2) {
-        const int bx = tx * 16 + bcol;
-        valid = bx < bw;
-        blk = (long long)(2 * ty + nt) * bw + bx;
-      } else {
-        const int mx = tx * 8 + (bcol & 7);
-        valid = mx < mw;
-        blk = (long long)G.nY + (bcol >= 8 ? G.nC : 0) + (long long)ty * mw + mx;
-      }
-
-      int out[16];
-#pragma unroll
-      for (int m = 0; m < 4; m++) {
-        const v4i zero = {0, 0, 0, 0};
-        v4i a2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[3 * m + 0], Bf, zero, 0, 0, 0);
-        v4i a1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[3 * m + 1], Bf, zero, 0, 0, 0);
-        v4i a0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[3 * m + 2], Bf, zero, 0, 0, 0);
-        const float4 fac = *(const float4 *)&s_fac[comp][16 * g + 4 * m];
-        const float4 tau = *(const float4 *)&s_tau[comp][16 * g + 4 * m];
-        const float fa[4] = {fac.x, fac.y, fac.z, fac.w};
-        const float ta[4] = {tau.x, tau.y, tau.z, tau.w};
-        int haz = 0;
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int N = (a2[r] << 14) + (a1[r] << 7) + a0[r];
-          const float nf = (float)N;
-          const int lo = (int)fmaf(nf, fa[r], -ta[r]);
-          const int hi = (int)fmaf(nf, fa[r], ta[r]);
-          out[4 * m + r] = lo;
-          haz |= (lo != hi) << r;
+      for (int nt = 0; nt < ((a.flags & K1F_NO_DCT) ? 0 : 3); nt++) {
+        const int comp = nt == 2 ? 1 : 0;
+        bool valid;
+        int blk;  // block index inside the frame's coefficient space
+        int seg;  // segment index inside the frame
+        if (nt < 2) {
+          const int bx = p.tx * 16 + bcol;
+          valid = bx < bw;
+          blk = (2 * p.ty + nt) * bw + bx;
+          seg = (2 * p.ty + nt) * G.tiles_x + p.tx;
+        } else {
+          const int mx = p.tx * 8 + (bcol & 7);
+          valid = mx < mw;
+          blk = G.nY + (bcol >= 8 ? G.nC : 0) + p.ty * mw + mx;
+          seg = G.nsy + (bcol >= 8 ? G.nsc : 0) + p.ty * G.tiles_x + p.tx;
         }
-        if (m == 0) {  // DC: the DC row of A is all-ones in digit 0 -> exact sum
-          const int dcq = dc_exact(a0[0], q_dc[comp]);
-          if (g == 0) {
-            out[0] = dcq;
-            haz &= ~1;
+        int o[16];
+        if (PIX) {
+          const uint8_t *Pb = L + (nt * 16 + bcol) * LDS_BLK;
+          v4i Bf = *(const v4i *)(Pb + 16 * g);
+          Bf ^= (int)0x80808080;  // pixel - 128 as int8
+          // N = ((D2.X << 7) + D1.X << 7) + D0.X, accumulated in place: each
+          // digit's MFMA takes the shifted partial sum as its C input
+          v4i acc[4];
+#pragma unroll
+          for (int m = 0; m < 4; m++) {
+            const int4 F2 = s_A[(3 * m + 0) * 64 + lane];
+            const int4 F1 = s_A[(3 * m + 1) * 64 + lane];
+            const int4 F0 = s_A[(3 * m + 2) * 64 + lane];
+            const v4i zero = {0, 0, 0, 0};
+            v4i tt = __builtin_amdgcn_mfma_i32_16x16x64_i8(v4i{F2.x, F2.y, F2.z, F2.w}, Bf, zero, 0, 0, 0);
+            tt = __builtin_amdgcn_mfma_i32_16x16x64_i8(v4i{F1.x, F1.y, F1.z, F1.w}, Bf, tt << 7, 0, 0, 0);
+            acc[m] = __builtin_amdgcn_mfma_i32_16x16x64_i8(v4i{F0.x, F0.y, F0.z, F0.w}, Bf, tt << 7, 0, 0, 0);
+          }
+          uint32_t hz = 0;  // coefficients whose +-tau interval straddles a boundary
+#pragma unroll
+          for (int m = 0; m < 4; m++) {
+            const float4 fac = *(const float4 *)&s_fac[comp][16 * g + 4 * m];
+            const float4 tau = *(const float4 *)&s_tau[comp][16 * g + 4 * m];
+            const float4 rel = *(const float4 *)&s_rel[comp][16 * g + 4 * m];
+            const float fa[4] = {fac.x, fac.y, fac.z, fac.w};
+            const float ta[4] = {tau.x, tau.y, tau.z, tau.w};
+            const float ra[4] = {rel.x, rel.y, rel.z, rel.w};
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+              const int k = 4 * m + r;
+              const float nf = (float)acc[m][r];
+              const float tv = fmaf(fabsf(nf), ra[r], ta[r]);  // tau for this value
+              const int lo = (int)fmaf(nf, fa[r], -tv);
+              const int hi = (int)fmaf(nf, fa[r], tv);
+              o[k] = lo;
+              hz |= (uint32_t)(hi - lo) << k;  // hi - lo is 0 or 1 (2*tau < 1)
+            }
+          }
+          if (g == 0) o[0] = dc_exact(acc[0][0], q_dc[comp]);  // z = 0: fac = tau = 0
+          if (__ballot(hz != 0) && !(a.flags & K1F_NO_REPLAY)) {
+            int16_t *rep = s_st[wave][lane];
+            uint32_t mm = hz;
+            while (mm) {
+              const int k = __ffs(mm) - 1;
+              mm &= mm - 1u;
+              const int z = 16 * g + k;
+              rep[k] = (int16_t)ac_exact(Pb, z, s_qint[comp][z], s_cos);
+            }
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+              if ((hz >> k) & 1u) o[k] = rep[k];
+            if (hz) atomicAdd(a.replays, (unsigned)__popc(hz));
+          }
+        } else {  // coefficients from memory (drop-in write_jpg / init_huffman)
+          u4v c0 = {0, 0, 0, 0}, c1 = {0, 0, 0, 0};
+          if (valid) {
+            const int16_t *src = a.coef + (long long)p.f * G.coef_fs + (long long)blk * 64 + 16 * g;
+            c0 = *(const u4v *)src;
+            c1 = *(const u4v *)(src + 8);
+          }
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            o[2 * k] = (int16_t)(c0[k] & 0xFFFFu);
+            o[2 * k + 1] = (int16_t)(c0[k] >> 16);
+            o[8 + 2 * k] = (int16_t)(c1[k] & 0xFFFFu);
+            o[9 + 2 * k] = (int16_t)(c1[k] >> 16);
           }
         }
-        if (__ballot(haz != 0)) {
-          int nrep = 0;
+        if ((MODE & K1M_COEF_OUT) && valid && !(a.flags & K1F_NO_STORE)) {
+          int16_t *dst = a.coef + (long long)p.f * G.coef_fs + (long long)blk * 64 + 16 * g;
+          u4v s0, s1;
 #pragma unroll
-          for (int r = 0; r < 4; r++)
-            if ((haz >> r) & 1) {
-              out[4 * m + r] = ac_exact(Pb, 16 * g + 4 * m + r, T->qint[comp][16 * g + 4 * m + r],
-                                        T->cosd);
-              nrep++;
-            }
-          if (nrep) atomicAdd(a.replays, (unsigned)nrep);
+          for (int k = 0; k < 4; k++) {
+            s0[k] = (uint32_t)(uint16_t)o[2 * k] | ((uint32_t)o[2 * k + 1] << 16);
+            s1[k] = (uint32_t)(uint16_t)o[8 + 2 * k] | ((uint32_t)o[9 + 2 * k] << 16);
+          }
+          __builtin_nontemporal_store(s0, (u4v *)dst);
+          __builtin_nontemporal_store(s1, (u4v *)(dst + 8));
+        }
+        if (PIX && valid && g == 0) a.dc[(long long)p.f * G.nblk + blk] = (int16_t)o[0];
+        if (TOK) {
+          const long long fs = (long long)p.f * G.nseg + seg;
+          const int slot = p.f - f0;
+          emit_tokens(o, lane, g, bcol, valid, comp == 1, !PIX, a.tok + fs * SEG_TOK,
+                      a.seg_ntok + fs, s_hdc[TOK ? slot : 0][comp], s_hac[TOK ? slot : 0][comp],
+                      s_st[wave]);
         }
       }
-      if (valid) {
-        int16_t *dst = a.coef + (long long)f * G.coef_fs + blk * 64 + 16 * g;
-        u4v s0, s1;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          s0[k] = (uint32_t)(uint16_t)out[2 * k] | ((uint32_t)out[2 * k + 1] << 16);
-          s1[k] = (uint32_t)(uint16_t)out[8 + 2 * k] | ((uint32_t)out[9 + 2 * k] << 16);
-        }
-        __builtin_nontemporal_store(s0, (u4v *)dst);
-        __builtin_nontemporal_store(s1, (u4v *)(dst + 8));
-        if (g == 0) a.dc[(long long)f * G.nblk + blk] = (int16_t)out[0];
-      }
+      if (PIX) wave_lds_sync();
+      p = pn;
     }
-    wave_lds_sync();
+  }
+  if (TOK) {  // per-frame histograms of this workgroup
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * 2 * 256; i += 256) {
+      const int slot = i >> 9, tb = (i >> 8) & 1, sym = i & 255;
+      const uint32_t v = s_hac[slot][tb][sym];
+      if (v && f0 + slot < a.nframes)
+        atomicAdd(&a.hist[((long long)(f0 + slot) * 4 + (tb ? 3 : 1)) * 257 + sym], v);
+    }
+    if (threadIdx.x < 64) {
+      const int slot = threadIdx.x >> 5, tb = (threadIdx.x >> 4) & 1, sym = threadIdx.x & 15;
+      const uint32_t v = s_hdc[slot][tb][sym];
+      if (v && f0 + slot < a.nframes)
+        atomicAdd(&a.hist[((long long)(f0 + slot) * 4 + (tb ? 2 : 0)) * 257 + sym], v);
+    }
   }
 }
+
 
 // ===========================================================================
 // DC differencing in place (encoder.c:168-177), for the drop-in rgb_to_dct
@@ -351,122 +563,54 @@ __global__ void k_dc_diff(int16_t *coef, const int16_t *dc, Geom G, int nframes)
 }
 
 // ===========================================================================
-// Entropy helpers
+// Segments.  Segment s of a frame = the blocks of one K1 N-tile row run:
+//   Y  s in [0, nsy):           block row s / tiles_x, tile column s % tiles_x
+//   Cb s in [nsy, nsy+nsc):     MCU row, tile column (8 blocks)
+//   Cr s in [nsy+nsc, nseg):    likewise
+// so each scan's segments are contiguous and in scan order.
 // ===========================================================================
-struct Chunk {
-  int f, comp, first, n, cstart;  // first block (frame-relative), count, comp start
-};
-
-__device__ __forceinline__ Chunk chunk_of(const Geom &G, int q) {
-  Chunk c;
-  c.f = q / G.cpf;
-  int r = q - c.f * G.cpf;
-  if (r < G.cy) {
-    c.comp = 0;
-    c.cstart = 0;
-    c.first = r * CHUNK;
-    c.n = min(CHUNK, G.nY - c.first);
+__device__ __forceinline__ void seg_info(const Geom &G, int s, int &comp, int &first,
+                                         int &cstart, int &local) {
+  if (s < G.nsy) {
+    comp = 0;
+    local = s;
+    cstart = 0;
+    first = (s / G.tiles_x) * (G.w >> 3) + (s % G.tiles_x) * 16;
   } else {
-    r -= G.cy;
-    c.comp = 1 + (r >= G.cc);
-    if (r >= G.cc) r -= G.cc;
-    c.cstart = c.comp == 1 ? G.nY : G.nY + G.nC;
-    c.first = c.cstart + r * CHUNK;
-    c.n = min(CHUNK, G.nC - r * CHUNK);
+    const int c = s - G.nsy;
+    comp = 1 + (c >= G.nsc);
+    local = comp == 1 ? c : c - G.nsc;
+    cstart = comp == 1 ? G.nY : G.nY + G.nC;
+    first = cstart + (local / G.tiles_x) * (G.w >> 4) + (local % G.tiles_x) * 8;
   }
-  return c;
-}
-
-// Magnitude bits of a value of class cls (encoder.c:442-444 / :456-458:
-// negative values are written as ~|v|, i.e. the low cls bits of v-1).
-__device__ __forceinline__ uint32_t mag_bits(int v, int cls) {
-  uint32_t id = (uint32_t)(v < 0 ? -v : v);
-  if (v < 0) id = ~id;
-  return id & ((1u << cls) - 1u);
 }
 
 // ===========================================================================
-// k_tokens: coefficient planes -> per-block symbol lists + histograms.
-//
-// Token = symbol (bits 0-7) | ZRL count before it (bits 8-9) | magnitude
-// bits (16-27).  Block slot: token 0 = DC difference (symbol = its class,
-// encoder.c:434-446), tokens 1..n = the AC run/size symbols in zigzag order
-// exactly as encoder.c:321-358 / :462-502 visit them (a nonzero at zigzag k
-// after r zeros emits r/16 ZRLs, then ((r%16)<<4)|class); hdr = n | EOB<<7
-// (EOB unless coefficient 63 is nonzero).  Histograms: DC classes and AC
-// symbols per table (:315-319, :321-358), ZRLs and EOBs included.
-//
-// One workgroup per chunk; lane (g, b) of a wave holds zigzag coefficients
-// 16g..16g+15 of block b, so a wave covers 16 blocks per iteration and the
-// 64-bit nonzero mask of a block is assembled from its 4 lanes.
+// k_seg_dc: DC difference of every segment's first block (its predecessor
+// lies in another segment, encoder.c:168-177): token 0 of the segment and
+// the DC class histogram.  One thread per segment.
 // ===========================================================================
-__global__ __launch_bounds__(256) void k_tokens(EntArgs a) {
-  __shared__ uint32_t h[2][257];
-  __shared__ __attribute__((aligned(16))) int16_t s_coef[4][64][16];
-  const Chunk c = chunk_of(a.g, blockIdx.x);
-  for (int i = threadIdx.x; i < 2 * 257; i += 256) h[i / 257][i % 257] = 0;
+__global__ __launch_bounds__(256) void k_seg_dc(EntArgs a) {
+  __shared__ uint32_t h[2][16];
+  const int per = (a.g.nseg + 255) / 256;
+  const int f = blockIdx.x / per;
+  const int s = (blockIdx.x - f * per) * 256 + threadIdx.x;
+  if (threadIdx.x < 32) (&h[0][0])[threadIdx.x] = 0;
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g = lane >> 4, bcol = lane & 15;
-  const long long fb = (long long)c.f * a.g.nblk;
-  for (int base = wave * 16; base < c.n; base += 64) {
-    const int i = base + bcol;
-    const bool v = i < c.n;
-    const int j = c.first + i;
-    u4v w0 = {0, 0, 0, 0}, w1 = {0, 0, 0, 0};
-    if (v) {
-      const int16_t *blk = a.coef + (long long)c.f * a.g.coef_fs + (long long)j * 64 + 16 * g;
-      w0 = *(const u4v *)blk;
-      w1 = *(const u4v *)(blk + 8);
-    }
-    *(u4v *)&s_coef[wave][lane][0] = w0;
-    *(u4v *)&s_coef[wave][lane][8] = w1;
-    uint32_t m16 = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const uint32_t wd = k < 4 ? w0[k] : w1[k - 4];
-      m16 |= ((wd & 0xFFFFu) != 0u ? 1u : 0u) << (2 * k);
-      m16 |= ((wd >> 16) != 0u ? 1u : 0u) << (2 * k + 1);
-    }
-    if (g == 0) m16 &= ~1u;  // the DC is not part of the AC run structure
-    unsigned long long M = (unsigned long long)m16 << (16 * g);
-    M |= __shfl_xor(M, 16);
-    M |= __shfl_xor(M, 32);
-    uint32_t *tok = a.tok + (fb + j) * 64;
-    if (g == 0 && v) {
-      const int dc = (int16_t)(w0[0] & 0xFFFFu);
-      const int diff =
-          a.dc_mode ? dc : dc - (j == c.cstart ? 0 : (int)a.dc[fb + j - 1]);  // :168-177
-      const int cls = mag_class(diff);
-      tok[0] = (uint32_t)cls | (mag_bits(diff, cls) << 16);
-      atomicAdd(&h[0][cls], 1u);
-      const int eob = !((M >> 63) & 1ull);
-      a.hdr[fb + j] = (uint8_t)(__popcll(M) | (eob << 7));
-      if (eob) atomicAdd(&h[1][0x00], 1u);
-    }
-    wave_lds_sync();
-    uint32_t mm = v ? m16 : 0u;
-    while (mm) {
-      const int k = __ffs(mm) - 1;
-      mm &= mm - 1u;
-      const int z = 16 * g + k;
-      const int cz = s_coef[wave][lane][k];
-      const unsigned long long before = M & ((1ull << z) - 1ull);
-      const int run = z - (63 - __clzll(before | 1ull)) - 1;
-      const int cls = mag_class(cz);
-      const int sym = ((run & 15) << 4) | cls;
-      tok[1 + __popcll(before)] = (uint32_t)sym | ((uint32_t)(run >> 4) << 8) |
-                                  (mag_bits(cz, cls) << 16);
-      atomicAdd(&h[1][sym], 1u);
-      if (run >= 16) atomicAdd(&h[1][0xF0], (unsigned)(run >> 4));
-    }
-    wave_lds_sync();
+  if (s < a.g.nseg) {
+    int comp, first, cstart, local;
+    seg_info(a.g, s, comp, first, cstart, local);
+    const long long fb = (long long)f * a.g.nblk;
+    const int diff = (int)a.dc[fb + first] - (first == cstart ? 0 : (int)a.dc[fb + first - 1]);
+    const int cls = mag_class(diff);
+    a.tok[((long long)f * a.g.nseg + s) * SEG_TOK] = (uint32_t)cls | (mag_bits(diff, cls) << 16);
+    atomicAdd(&h[comp ? 1 : 0][cls], 1u);
   }
   __syncthreads();
-  uint32_t *gh = a.hist + ((long long)c.f * 4 + (c.comp ? 2 : 0)) * 257;
-  for (int i = threadIdx.x; i < 2 * 257; i += 256) {
-    const uint32_t hv = h[i / 257][i % 257];
-    if (hv) atomicAdd(&gh[i], hv);
+  if (threadIdx.x < 32) {
+    const uint32_t v = (&h[0][0])[threadIdx.x];
+    if (v)
+      atomicAdd(&a.hist[((long long)f * 4 + (threadIdx.x >= 16 ? 2 : 0)) * 257 + (threadIdx.x & 15)], v);
   }
 }
 
@@ -683,60 +827,55 @@ __global__ void k_ehuf_struct(const HuffCode *hc, uint32_t *ehuf) {
 }
 
 // ===========================================================================
-// k_bits: bits of every block from its tokens and the frame's code lengths;
-// chunk totals.  One thread per block.
+// k_seg_bits: bits of every segment with the frame's tables.  One wave per
+// segment, lanes over its tokens; a workgroup covers SEG_PER_WG segments of
+// one frame.
 // ===========================================================================
-__global__ __launch_bounds__(256) void k_bits(EntArgs a) {
-  __shared__ uint32_t tab[2][256];
-  __shared__ uint32_t wsum[4];
-  const Chunk c = chunk_of(a.g, blockIdx.x);
-  const uint32_t *et = a.ehuf + ((long long)c.f * 4 + (c.comp ? 2 : 0)) * 256;
-  for (int i = threadIdx.x; i < 512; i += 256) tab[i >> 8][i & 255] = et[i];
-  __syncthreads();
-  const int t = threadIdx.x;
-  uint32_t bits = 0;
-  if (t < c.n) {
-    const long long gb = (long long)c.f * a.g.nblk + c.first + t;
-    const uint32_t *tok = a.tok + gb * 64;
-    const int hd = a.hdr[gb];
-    const int n = hd & 63;
-    const int dcls = (int)(tok[0] & 255u);
-    bits = (tab[0][dcls] >> 16) + (uint32_t)dcls;
-    const uint32_t lz = tab[1][0xF0] >> 16;
-    for (int i = 1; i <= n; i++) {
-      const uint32_t tk = tok[i];
-      const uint32_t sym = tk & 255u;
-      bits += (tab[1][sym] >> 16) + (sym & 15u) + ((tk >> 8) & 3u) * lz;
-    }
-    if (hd & 128) bits += tab[1][0x00] >> 16;
-    a.bits[gb] = bits;
-  }
-  uint32_t x = bits;
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off);
-  if ((t & 63) == 0) wsum[t >> 6] = x;
-  __syncthreads();
-  if (t == 0) a.chunk_bits[blockIdx.x] = (unsigned long long)wsum[0] + wsum[1] + wsum[2] + wsum[3];
+__device__ __forceinline__ uint32_t tok_bits(uint32_t tk, const uint32_t (*tab)[256], int chroma) {
+  const int t = (chroma ? 2 : 0) + ((tk & TOK_AC) ? 1 : 0);
+  const uint32_t sym = tk & 255u;
+  return (tab[t][sym] >> 16) + (sym & 15u) + ((tk >> 8) & 3u) * (tab[t][0xF0] >> 16);
 }
 
+__global__ __launch_bounds__(256) void k_seg_bits(EntArgs a) {
+  __shared__ uint32_t tab[4][256];
+  const int per = (a.g.nseg + SEG_PER_WG - 1) / SEG_PER_WG;
+  const int f = blockIdx.x / per;
+  const int s0 = (blockIdx.x - f * per) * SEG_PER_WG;
+  for (int i = threadIdx.x; i < 1024; i += 256) tab[i >> 8][i & 255] = a.ehuf[(long long)f * 1024 + i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int s = s0 + wave; s < min(s0 + SEG_PER_WG, a.g.nseg); s += 4) {
+    const long long fs = (long long)f * a.g.nseg + s;
+    const int n = (int)a.seg_ntok[fs];
+    const uint32_t *tk = a.tok + fs * SEG_TOK;
+    const int chroma = s >= a.g.nsy;
+    uint32_t b = 0;
+    for (int i = lane; i < n; i += 64) b += tok_bits(tk[i], tab, chroma);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) b += __shfl_xor(b, off);
+    if (lane == 0) a.seg_bits[fs] = b;
+  }
+}
 
 // ===========================================================================
-// k_scan: per scan (frame, component) exclusive scan of chunk bit totals;
-// zeroes the words a chunk shares with a neighbour (they are OR-combined).
-// One wave per scan.
+// k_scan: per scan (frame, component) exclusive scan of segment bits; zeroes
+// the first/last word of every pack group (shared with neighbour groups and
+// OR-combined by k_pack).  One wave per scan.
 // ===========================================================================
 __global__ void k_scan(EntArgs a) {
   const int sid = blockIdx.x;  // frame * 3 + comp
   const int f = sid / 3, comp = sid - f * 3;
   const int lane = threadIdx.x;
-  const int q0 = f * a.g.cpf + (comp == 0 ? 0 : a.g.cy + (comp - 1) * a.g.cc);
-  const int nq = comp == 0 ? a.g.cy : a.g.cc;
+  const int sbase = comp == 0 ? 0 : a.g.nsy + (comp - 1) * a.g.nsc;
+  const int ns = comp == 0 ? a.g.nsy : a.g.nsc;
+  const long long f0 = (long long)f * a.g.nseg + sbase;
   uint32_t *raw = a.raw + (long long)f * a.g.raw_fs +
                   (comp == 0 ? 0 : a.g.raw_words[0] + (comp == 2 ? a.g.raw_words[1] : 0));
   unsigned long long carry = 0;
-  for (int base = 0; base < nq; base += 64) {
+  for (int base = 0; base < ns; base += 64) {
     const int i = base + lane;
-    const unsigned long long v = i < nq ? a.chunk_bits[q0 + i] : 0ull;
+    const unsigned long long v = i < ns ? a.seg_bits[f0 + i] : 0ull;
     unsigned long long x = v;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -744,10 +883,10 @@ __global__ void k_scan(EntArgs a) {
       if (lane >= off) x += y;
     }
     const unsigned long long excl = carry + x - v;
-    if (i < nq) {
-      a.chunk_off[q0 + i] = excl;
-      raw[excl >> 5] = 0;
-      raw[(excl + v - 1) >> 5] = 0;
+    if (i < ns) {
+      a.seg_off[f0 + i] = excl;
+      if (i % PACK_SEGS == 0) raw[excl >> 5] = 0;
+      if (i % PACK_SEGS == PACK_SEGS - 1 || i == ns - 1) raw[(excl + v - 1) >> 5] = 0;
     }
     carry += __shfl(x, 63);
   }
@@ -755,11 +894,11 @@ __global__ void k_scan(EntArgs a) {
 }
 
 // ===========================================================================
-// k_pack: bit-pack one chunk into LDS, then store it.  Thread t writes block
-// t's tokens at the block's offset (chunk offset + exclusive scan of block
-// bits); pieces are OR-ed into LDS words in big-endian bit order.  Interior
-// words are stored plainly, the two words shared with neighbouring chunks
-// atomically (k_scan zeroed them).
+// k_pack: bit-pack a group of PACK_SEGS consecutive segments of one scan in
+// LDS, then store it.  A wave takes a segment; lanes take its tokens, place
+// them at the segment offset + a wave-wide exclusive scan of token bits, and
+// OR the pieces into LDS words (big-endian bit order).  Interior words are
+// stored plainly, the group's first/last word atomically (k_scan zeroed them).
 // ===========================================================================
 __device__ __forceinline__ void put_bits(uint32_t *buf, uint32_t pos, uint32_t val, int len) {
   // len in 1..28, val < 2^len
@@ -774,67 +913,70 @@ __device__ __forceinline__ void put_bits(uint32_t *buf, uint32_t pos, uint32_t v
 }
 
 __global__ __launch_bounds__(256) void k_pack(EntArgs a) {
-  __shared__ uint32_t buf[CHUNK_WORDS];
-  __shared__ uint32_t tab[2][256];
-  __shared__ uint32_t wsum[4];
-  const Chunk c = chunk_of(a.g, blockIdx.x);
-  const uint32_t *et = a.ehuf + ((long long)c.f * 4 + (c.comp ? 2 : 0)) * 256;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int i = tid; i < 512; i += 256) tab[i >> 8][i & 255] = et[i];
-  const long long gb = (long long)c.f * a.g.nblk + c.first + tid;
-  const uint32_t mybits = tid < c.n ? a.bits[gb] : 0u;
-  uint32_t x = mybits;
+  __shared__ uint32_t buf[PACK_WORDS];
+  __shared__ uint32_t tab[4][256];
+  const Geom &G = a.g;
+  const int gy = (G.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (G.nsc + PACK_SEGS - 1) / PACK_SEGS;
+  const int gpf = gy + 2 * gc;
+  const int f = blockIdx.x / gpf;
+  int q = blockIdx.x - f * gpf, comp, sbase, ns;
+  if (q < gy) {
+    comp = 0; sbase = 0; ns = G.nsy;
+  } else {
+    q -= gy;
+    comp = 1 + (q >= gc);
+    if (q >= gc) q -= gc;
+    sbase = comp == 1 ? G.nsy : G.nsy + G.nsc;
+    ns = G.nsc;
+  }
+  const int s0 = q * PACK_SEGS, s1 = min(ns, s0 + PACK_SEGS);
+  const long long fs0 = (long long)f * G.nseg + sbase;
+  for (int i = threadIdx.x; i < 1024; i += 256) tab[i >> 8][i & 255] = a.ehuf[(long long)f * 1024 + i];
+  const unsigned long long gbase = a.seg_off[fs0 + s0];
+  const unsigned long long gend = a.seg_off[fs0 + s1 - 1] + a.seg_bits[fs0 + s1 - 1];
+  const uint32_t bit0 = (uint32_t)(gbase & 31);
+  const uint32_t nw = (uint32_t)((bit0 + (gend - gbase) + 31) >> 5);
+  for (uint32_t i = threadIdx.x; i < nw; i += 256) buf[i] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int chroma = comp != 0;
+  const int t0 = chroma ? 2 : 0;
+  const uint32_t zac = tab[t0 + 1][0xF0];
+  const int Lz = (int)(zac >> 16);
+  for (int s = s0 + wave; s < s1; s += 4) {
+    const long long fs = fs0 + s;
+    const int n = (int)a.seg_ntok[fs];
+    const uint32_t *tk = a.tok + fs * SEG_TOK;
+    uint32_t pos0 = bit0 + (uint32_t)(a.seg_off[fs] - gbase);
+    for (int i0 = 0; i0 < n; i0 += 64) {
+      const int i = i0 + lane;
+      const uint32_t t = i < n ? tk[i] : 0u;
+      const uint32_t nb = i < n ? tok_bits(t, tab, chroma) : 0u;
+      uint32_t x = nb;
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t y = __shfl_up(x, off);
-    if (lane >= off) x += y;
-  }
-  if (lane == 63) wsum[wave] = x;
-  __syncthreads();
-  uint32_t wbase = 0;
-  for (int w = 0; w < wave; w++) wbase += wsum[w];
-  const uint32_t chunk_bits = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-  const unsigned long long base = a.chunk_off[blockIdx.x];
-  const uint32_t bit0 = (uint32_t)(base & 31);
-  const uint32_t nw = (bit0 + chunk_bits + 31) >> 5;
-  for (uint32_t i = tid; i < nw; i += 256) buf[i] = 0;
-  __syncthreads();
-  if (tid < c.n) {
-    uint32_t pos = bit0 + wbase + x - mybits;
-    const uint32_t *tok = a.tok + gb * 64;
-    const int hd = a.hdr[gb];
-    const int n = hd & 63;
-    uint32_t tk = tok[0];
-    int cls = (int)(tk & 255u);
-    uint32_t e = tab[0][cls];
-    int L = (int)(e >> 16);
-    put_bits(buf, pos, ((e & 0xFFFFu) << cls) | (tk >> 16), L + cls);  // :434-446
-    pos += L + cls;
-    const uint32_t zrl = tab[1][0xF0];
-    const int Lz = (int)(zrl >> 16);
-    for (int i = 1; i <= n; i++) {
-      tk = tok[i];
-      for (uint32_t k = (tk >> 8) & 3u; k; k--) {  // :490-494 ZRL
-        put_bits(buf, pos, zrl & 0xFFFFu, Lz);
-        pos += Lz;
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
       }
-      const uint32_t sym = tk & 255u;
-      cls = (int)(sym & 15u);
-      e = tab[1][sym];
-      L = (int)(e >> 16);
-      put_bits(buf, pos, ((e & 0xFFFFu) << cls) | (tk >> 16), L + cls);  // :448-460
-      pos += L + cls;
-    }
-    if (hd & 128) {  // :479-484 EOB
-      e = tab[1][0x00];
-      put_bits(buf, pos, e & 0xFFFFu, (int)(e >> 16));
+      if (i < n) {
+        uint32_t pos = pos0 + x - nb;
+        for (uint32_t k = (t >> 8) & 3u; k; k--) {  // encoder.c:490-494 ZRL
+          put_bits(buf, pos, zac & 0xFFFFu, Lz);
+          pos += Lz;
+        }
+        const uint32_t sym = t & 255u, cls = sym & 15u;
+        const uint32_t e = tab[t0 + ((t & TOK_AC) ? 1 : 0)][sym];
+        const int L = (int)(e >> 16) + (int)cls;
+        if (L) put_bits(buf, pos, ((e & 0xFFFFu) << cls) | (t >> 16), L);  // :434-460
+      }
+      pos0 += __shfl(x, 63);
     }
   }
   __syncthreads();
-  uint32_t *raw = a.raw + (long long)c.f * a.g.raw_fs +
-                  (c.comp == 0 ? 0 : a.g.raw_words[0] + (c.comp == 2 ? a.g.raw_words[1] : 0)) +
-                  (base >> 5);
-  for (uint32_t i = tid; i < nw; i += 256) {
+  uint32_t *raw = a.raw + (long long)f * G.raw_fs +
+                  (comp == 0 ? 0 : G.raw_words[0] + (comp == 2 ? G.raw_words[1] : 0)) +
+                  (gbase >> 5);
+  for (uint32_t i = threadIdx.x; i < nw; i += 256) {
     if (i == 0 || i == nw - 1) atomicOr(&raw[i], buf[i]);
     else raw[i] = buf[i];
   }
@@ -971,9 +1113,12 @@ __global__ void k_mfma_probe(const int4 *A, const int4 *B, int4 *D) {
 static int g_k1_blocks_per_cu = -1;
 
 int k1_grid(int device, long long ntiles) {
+  // persistent: at most (resident blocks per CU) x CUs workgroups
   if (g_k1_blocks_per_cu < 0) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_mcu_dct, 256, 0) != hipSuccess || nb < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_mcu_dct<K1M_TOK_OUT>, 256, 0) !=
+            hipSuccess ||
+        nb < 1)
       nb = 1;
     g_k1_blocks_per_cu = nb;
   }
@@ -986,11 +1131,26 @@ int k1_grid(int device, long long ntiles) {
 }
 
 hipError_t launch_colour_lut(uint32_t *lut, hipStream_t s) {
-  hipLaunchKernelGGL(k_colour_lut, dim3(256), dim3(256), 0, s, lut);
+  hipLaunchKernelGGL(k_colour_lut, dim3(128), dim3(256), 0, s, lut);
   return hipGetLastError();
 }
-hipError_t launch_k1(const K1Args &a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(k_mcu_dct, dim3(grid), dim3(256), 0, s, a);
+// mode: K1M_* bits (see k_mcu_dct)
+hipError_t launch_k1(const K1Args &a, int grid, int mode, hipStream_t s) {
+  switch (mode) {
+    case K1M_COEF_OUT: hipLaunchKernelGGL((k_mcu_dct<K1M_COEF_OUT>), dim3(grid), dim3(256), 0, s, a); break;
+    case K1M_TOK_OUT: hipLaunchKernelGGL((k_mcu_dct<K1M_TOK_OUT>), dim3(grid), dim3(256), 0, s, a); break;
+    case K1M_COEF_OUT | K1M_TOK_OUT:
+      hipLaunchKernelGGL((k_mcu_dct<K1M_COEF_OUT | K1M_TOK_OUT>), dim3(grid), dim3(256), 0, s, a);
+      break;
+    case K1M_COEF_IN | K1M_TOK_OUT:
+      hipLaunchKernelGGL((k_mcu_dct<K1M_COEF_IN | K1M_TOK_OUT>), dim3(grid), dim3(256), 0, s, a);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+hipError_t launch_seg_dc(const EntArgs &a, hipStream_t s) {
+  hipLaunchKernelGGL(k_seg_dc, dim3(a.nframes * ((a.g.nseg + 255) / 256)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_dc_diff(int16_t *coef, const int16_t *dc, const Geom &g, int nframes,
@@ -998,10 +1158,6 @@ hipError_t launch_dc_diff(int16_t *coef, const int16_t *dc, const Geom &g, int n
   long long n = (long long)nframes * g.nblk;
   hipLaunchKernelGGL(k_dc_diff, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, coef, dc, g,
                      nframes);
-  return hipGetLastError();
-}
-hipError_t launch_stats(const EntArgs &a, hipStream_t s) {
-  hipLaunchKernelGGL(k_tokens, dim3(a.nframes * a.g.cpf), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_tables(const EntArgs &a, hipStream_t s) {
@@ -1013,7 +1169,8 @@ hipError_t launch_ehuf_struct(const HuffCode *hc, uint32_t *ehuf, hipStream_t s)
   return hipGetLastError();
 }
 hipError_t launch_bits(const EntArgs &a, hipStream_t s) {
-  hipLaunchKernelGGL(k_bits, dim3(a.nframes * a.g.cpf), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_seg_bits, dim3(a.nframes * ((a.g.nseg + SEG_PER_WG - 1) / SEG_PER_WG)),
+                     dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_scan(const EntArgs &a, hipStream_t s) {
@@ -1021,7 +1178,8 @@ hipError_t launch_scan(const EntArgs &a, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t launch_pack(const EntArgs &a, hipStream_t s) {
-  hipLaunchKernelGGL(k_pack, dim3(a.nframes * a.g.cpf), dim3(256), 0, s, a);
+  const int gy = (a.g.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (a.g.nsc + PACK_SEGS - 1) / PACK_SEGS;
+  hipLaunchKernelGGL(k_pack, dim3(a.nframes * (gy + 2 * gc)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_emit(const EntArgs &a, hipStream_t s) {

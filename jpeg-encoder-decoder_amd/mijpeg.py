@@ -21,7 +21,7 @@ EXPORTS = [
     "mij_set_input_stride", "mij_set_quality", "mij_last_error", "mij_strerror",
     "mij_max_jpg_bytes", "mij_encode",
     "mij_batch_create", "mij_batch_destroy", "mij_batch_upload", "mij_batch_set_input",
-    "mij_batch_encode", "mij_batch_dct", "mij_batch_sync", "mij_batch_output",
+    "mij_batch_encode", "mij_batch_keep_coefs", "mij_batch_dct", "mij_batch_sync", "mij_batch_output",
     "mij_batch_lengths", "mij_batch_coefs", "mij_batch_tables", "mij_batch_set_timing",
     "mij_batch_stage_ms", "mij_batch_stage_history", "mij_batch_replays", "mij_batch_stream",
     "mij_probe_mfma", "mij_colour_lut", "mij_build_target",
@@ -83,6 +83,7 @@ def load() -> C.CDLL:
     lib.mij_batch_upload.argtypes = [p, p, i, i]
     lib.mij_batch_set_input.argtypes = [p, p, C.c_longlong, i]
     lib.mij_batch_encode.argtypes = [p, i]
+    lib.mij_batch_keep_coefs.argtypes = [p, i]
     lib.mij_batch_dct.argtypes = [p, i]
     lib.mij_batch_sync.argtypes = [p]
     lib.mij_batch_output.argtypes = [p, i, p, sz, C.POINTER(sz)]
@@ -181,13 +182,16 @@ def encode(frame_bgr: np.ndarray, quality: int = 50, region=None) -> bytes:
 class Batch:
     STAGES = ["k1_colour_dct_quant", "stats", "tables", "bits", "scan", "pack", "emit", "total"]
 
-    def __init__(self, w: int, h: int, max_frames: int, quality: int = 50, device: int = 0):
+    def __init__(self, w: int, h: int, max_frames: int, quality: int = 50, device: int = 0,
+                 keep_coefs: bool = False):
         self.lib = load()
         self.w, self.h, self.max_frames = w, h, max_frames
         self.h_ = self.lib.mij_batch_create(device, w, h, max_frames, quality)
         if not self.h_:
             raise MijError(f"mij_batch_create failed: "
                            f"{self.lib.mij_strerror(self.lib.mij_last_error()).decode()}")
+        if keep_coefs:
+            _check(self.lib.mij_batch_keep_coefs(self.h_, 1), "keep_coefs")
 
     def close(self) -> None:
         if self.h_:
@@ -271,6 +275,6 @@ def probe_mfma(A: np.ndarray, B: np.ndarray) -> np.ndarray:
 
 
 def colour_lut() -> np.ndarray:
-    out = np.zeros(3 * 2048, np.uint32)
+    out = np.zeros(3 * 1024, np.uint32)
     _check(load().mij_colour_lut(_ptr(out)), "colour_lut")
-    return out.reshape(3, 2048)
+    return out.reshape(3, 1024)

@@ -61,11 +61,13 @@ def test_mfma_i8_operand_layout():
 def test_colour_exception_bitmaps_match_reference_set():
     lut = mijpeg.colour_lut()
     ex = np.load(os.path.join(recipes.GOLDEN, "colour_exceptions.npz"))
-    want = np.zeros((3, 65536), bool)
+    want = np.zeros((3, 32768), bool)
     for ch, key in enumerate(("Y", "Cb", "Cr")):
         t = ex[key].astype(np.int64)
         r, g, b = t[:, 0], t[:, 1], t[:, 2]
-        idx = [(r << 8) | g, (g << 8) | b, (g << 8) | r][ch]
+        # integer points need equal parities, so each table is indexed by 15 bits
+        assert (((r ^ g) & 1) == 0).all() and (ch == 0 or (((b ^ g) & 1) == 0).all())
+        idx = [(r << 7) | (g >> 1), (g << 7) | (b >> 1), (g << 7) | (r >> 1)][ch]
         want[ch, idx] = True
     got = np.unpackbits(lut.view(np.uint8).reshape(3, -1), axis=1, bitorder="little").astype(bool)
     assert (got == want).all()
@@ -84,7 +86,7 @@ def test_batch_matches_reference_golden(manifest, name):
     ent = manifest[name]
     bgr = case_input(name, ent)
     H, W = bgr.shape[:2]
-    b = mijpeg.Batch(W, H, 1, ent["quality"])
+    b = mijpeg.Batch(W, H, 1, ent["quality"], keep_coefs=True)
     b.upload(bgr)
     b.encode(1)
     jpg = b.output(0)
@@ -99,7 +101,7 @@ def test_batch_matches_reference_golden(manifest, name):
 def test_standin_1920x1280_bit_exact_gate(manifest):
     ent = manifest["standin_1920x1280"]
     bgr = case_input("standin_1920x1280", ent)
-    b = mijpeg.Batch(1920, 1280, 1)
+    b = mijpeg.Batch(1920, 1280, 1, keep_coefs=True)
     b.upload(bgr)
     b.encode(1)
     jpg = b.output(0)
