@@ -118,6 +118,9 @@ int mij_batch_encode(mij_batch *b, int nframes);     /* full path, async */
 /* encode also keeps the coefficient planes (for mij_batch_coefs); off by
  * default: the fused K1 then emits symbol tokens instead of coefficients */
 int mij_batch_keep_coefs(mij_batch *b, int on);
+/* split pipeline: K1 writes coefficient planes and a second, light pass
+ * tokenizes them (same output bytes; for performance comparison) */
+int mij_batch_set_split(mij_batch *b, int on);
 int mij_batch_dct(mij_batch *b, int nframes);        /* K1 only, async */
 int mij_batch_sync(mij_batch *b);
 int mij_batch_output(mij_batch *b, int frame, uint8_t *dst, size_t cap,
@@ -137,6 +140,11 @@ int mij_batch_stage_ms(mij_batch *b, float *ms, int n);
 /* the same for each of the last `steps` encodes (<= 64) issued while timing
  * was on, oldest first: ms[step*8 + stage]; returns the count filled */
 int mij_batch_stage_history(mij_batch *b, float *ms, int steps);
+/* symbol tokens K1 emitted for the last encode of nframes frames (4 bytes
+ * each; used for the bandwidth accounting of the fused kernel) */
+unsigned long long mij_batch_token_count(mij_batch *b, int nframes);
+/* {w, h, 8x8 blocks per frame, segments per frame, K1 tiles per frame} */
+int mij_batch_geometry(mij_batch *b, long long *out, int n);
 /* coefficients recomputed in FP64 since creation (hazard replays) */
 unsigned long long mij_batch_replays(mij_batch *b);
 /* the batch's hipStream_t, as an opaque pointer */

@@ -16,7 +16,7 @@
 
 namespace mij {
 // launch wrappers (mij_kernels.hip)
-int k1_grid(int device, long long ntiles);
+int k1_grid(int device, long long ntiles, int mode);
 hipError_t launch_colour_lut(uint32_t *lut, hipStream_t s);
 hipError_t launch_k1(const K1Args &a, int grid, int mode, hipStream_t s);
 hipError_t launch_seg_dc(const EntArgs &a, hipStream_t s);
@@ -212,6 +212,7 @@ struct mij_batch {
   int *d_err = nullptr;
   unsigned *d_replays = nullptr;
   bool keep_coefs = false;  // encode also writes coefficient planes
+  bool split = false;       // K1 writes coefficients, a second pass tokenizes
   bool timing = false;
   static constexpr int HIST = 64;
   hipEvent_t evh[HIST][8] = {};  // per-step events while timing is on
@@ -367,7 +368,7 @@ static EntArgs ent_args(mij_batch *b, int nframes) {
 
 // mode: K1 mode bits (1 coefficient planes out, 2 tokens + histograms out,
 // 4 coefficient planes in)
-static int run_k1(mij_batch *b, int nframes, int mode) {
+static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0) {
   K1Args k;
   memset(&k, 0, sizeof(k));
   k.in = b->d_in;
@@ -385,11 +386,12 @@ static int run_k1(mij_batch *b, int nframes, int mode) {
   static const int k1_flags = getenv("MIJ_K1_FLAGS") ? atoi(getenv("MIJ_K1_FLAGS")) : 0;
   k.flags = k1_flags;
   const long long ntiles = (long long)nframes * b->g.tiles_per_frame;
-  long long grid = k1_grid(b->dev, ntiles);
+  long long grid = k1_grid(b->dev, ntiles, mode);
   long long per_wg = (ntiles + grid - 1) / grid;
   if (per_wg > b->g.tiles_per_frame) per_wg = b->g.tiles_per_frame;  // <= 2 frames per WG
   grid = (ntiles + per_wg - 1) / per_wg;
   k.per_wg = (int)per_wg;
+  k.dc_diffed = dc_diffed;
   HIP_TRY(launch_k1(k, (int)grid, mode, b->stream));
   return MIJ_OK;
 }
@@ -403,10 +405,7 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   const bool t = b->timing;
   if (dc_fix) HIP_TRY(launch_seg_dc(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[2], b->stream));
-  if (!tables_given) {
-    HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * nframes, b->stream));
-    HIP_TRY(launch_tables(a, b->stream));
-  }
+  if (!tables_given) HIP_TRY(launch_tables(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[3], b->stream));
   HIP_TRY(launch_bits(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[4], b->stream));
@@ -421,8 +420,13 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
 
 static int encode_frames(mij_batch *b, int nframes) {
   HIP_TRY(hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * nframes * 4 * 257, b->stream));
+  HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * nframes, b->stream));
   if (b->timing) HIP_TRY(hipEventRecord(b->ev[0], b->stream));
-  if (run_k1(b, nframes, b->keep_coefs ? 3 : 2)) return g_err;
+  if (b->split) {
+    if (run_k1(b, nframes, 1) || run_k1(b, nframes, 6, 0)) return g_err;
+  } else if (run_k1(b, nframes, b->keep_coefs ? 3 : 2)) {
+    return g_err;
+  }
   if (b->timing) HIP_TRY(hipEventRecord(b->ev[1], b->stream));
   return run_entropy(b, nframes, true, false);
 }
@@ -443,6 +447,12 @@ extern "C" int mij_batch_encode(mij_batch *b, int nframes) {
 extern "C" int mij_batch_keep_coefs(mij_batch *b, int on) {
   if (!b) return fail(MIJ_EINVAL, "keep_coefs: null batch");
   b->keep_coefs = on != 0;
+  return MIJ_OK;
+}
+
+extern "C" int mij_batch_set_split(mij_batch *b, int on) {
+  if (!b) return fail(MIJ_EINVAL, "set_split: null batch");
+  b->split = on != 0;
   return MIJ_OK;
 }
 
@@ -499,6 +509,26 @@ extern "C" int mij_batch_stage_ms(mij_batch *b, float *ms, int n) {
   HIP_TRY(hipSetDevice(b->dev));
   HIP_TRY(hipStreamSynchronize(b->stream));
   for (int i = 0; i < n && i < 8; i++) ms[i] = elapsed(b->ev[k_stage_pairs[i][0]], b->ev[k_stage_pairs[i][1]]);
+  return MIJ_OK;
+}
+
+extern "C" unsigned long long mij_batch_token_count(mij_batch *b, int nframes) {
+  if (!b || nframes < 1 || nframes > b->cap) return 0;
+  hipSetDevice(b->dev);
+  hipStreamSynchronize(b->stream);
+  std::vector<uint32_t> v((size_t)nframes * b->g.nseg);
+  if (hipMemcpy(v.data(), b->d_seg_ntok, v.size() * sizeof(uint32_t), hipMemcpyDeviceToHost) !=
+      hipSuccess)
+    return 0;
+  unsigned long long n = 0;
+  for (uint32_t x : v) n += x;
+  return n;
+}
+
+extern "C" int mij_batch_geometry(mij_batch *b, long long *out, int n) {
+  if (!b || !out) return fail(MIJ_EINVAL, "geometry: bad args");
+  const long long v[] = {b->g.w, b->g.h, b->g.nblk, b->g.nseg, b->g.tiles_per_frame};
+  for (int i = 0; i < n && i < 5; i++) out[i] = v[i];
   return MIJ_OK;
 }
 
@@ -665,7 +695,7 @@ extern "C" void init_huffman(int16_t *Y, int16_t *Cb, int16_t *Cr, area_t dims,
   if (!b || upload_planes(b, Y, Cb, Cr)) return;
   EntArgs a = ent_args(b, 1);
   if (hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * 4 * 257, b->stream) != hipSuccess ||
-      hipMemsetAsync(b->d_err, 0, sizeof(int), b->stream) != hipSuccess || run_k1(b, 1, 6) ||
+      hipMemsetAsync(b->d_err, 0, sizeof(int), b->stream) != hipSuccess || run_k1(b, 1, 6, 1) ||
       launch_tables(a, b->stream) != hipSuccess) {
     fail(MIJ_EHIP, "init_huffman: launch failed");
     return;
@@ -707,7 +737,7 @@ extern "C" size_t write_jpg(FILE *f, uint8_t *jpg, int16_t *Y, int16_t *Cb, int1
     return 0;
   }
   if (hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * 4 * 257, b->stream) != hipSuccess ||
-      run_k1(b, 1, 6) || run_entropy(b, 1, false, true))
+      run_k1(b, 1, 6, 1) || run_entropy(b, 1, false, true))
     return 0;
   size_t n = 0;
   if (hipStreamSynchronize(b->stream) != hipSuccess) {

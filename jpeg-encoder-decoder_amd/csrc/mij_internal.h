@@ -26,9 +26,11 @@ constexpr int LUT_WORDS = 1024;      // 2^15 bits per colour-exception table
 constexpr int MAX_BLOCK_TOK = 65;                 // DC + 63 AC + EOB
 constexpr int SEG_TOK = 16 * MAX_BLOCK_TOK;       // 1040 tokens per segment slot
 constexpr int SEG_PER_WG = 64;                    // k_seg_bits segments per workgroup
-constexpr int PACK_SEGS = 16;                     // segments per k_pack workgroup
+constexpr int PACK_SEGS = 64;                     // segments per k_pack workgroup
 constexpr int MAX_BLOCK_BITS = 1729;              // 28 DC + 63 * 27 AC bits
-constexpr int PACK_WORDS = (PACK_SEGS * 16 * MAX_BLOCK_BITS + 31) / 32 + 2;
+// k_pack assembles a group in LDS windows of PACK_WORDS words; a group wider
+// than one window (only near worst-case entropy) is packed in several passes.
+constexpr int PACK_WORDS = 4096;
 
 // Layout-identical to the reference huff_code (include/structs.h:5-13).
 struct HuffCode {
@@ -78,6 +80,7 @@ struct K1Args {
   unsigned int *replays;    // count of coefficients replayed in FP64
   int flags;                // diagnostics only (MIJ_K1_FLAGS): K1F_* bits
   int per_wg;               // tiles per workgroup (<= tiles_per_frame)
+  int dc_diffed;            // coefficient input holds DC differences (drop-in)
   uint32_t *tok;            // token mode: per segment SEG_TOK tokens
   uint32_t *seg_ntok;       // token mode: tokens per segment
   uint32_t *hist;           // token mode: per frame [4][257] histograms

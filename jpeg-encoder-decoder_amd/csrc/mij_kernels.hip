@@ -26,6 +26,7 @@ namespace mij {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef unsigned u4v __attribute__((ext_vector_type(4)));
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
 __constant__ int c_zigzag[64] = {  // encoder.c:38-46
     0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
@@ -39,6 +40,27 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// DPP row_shr:n with zero fill (lanes below n in their 16-lane row read 0)
+template <int N>
+__device__ __forceinline__ uint32_t row_shr0(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x110 + N, 0xF, 0xF, true);
+}
+// inclusive prefix sum inside each 16-lane row
+__device__ __forceinline__ uint32_t row_scan16(uint32_t x) {
+  x += row_shr0<1>(x);
+  x += row_shr0<2>(x);
+  x += row_shr0<4>(x);
+  x += row_shr0<8>(x);
+  return x;
+}
+// inclusive prefix sum over the wave (row scans + row_bcast:15 / row_bcast:31)
+__device__ __forceinline__ uint32_t wave_scan64(uint32_t x) {
+  x = row_scan16(x);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+  return x;
 }
 
 __device__ __forceinline__ int mag_class(int v) {  // encoder.c:303-313
@@ -107,35 +129,6 @@ __global__ void k_colour_lut(uint32_t *lut /* [3][LUT_WORDS] */) {
 // ===========================================================================
 // K1 helpers
 // ===========================================================================
-
-// encoder.c:133-135 bit-exactly.  The fp32 forms below carry an error
-// < 2e-5 (Y) / 1e-5 (Cb, Cr), while a non-integer exact value is >= 1e-3 (Y)
-// or >= 3.2e-5 (Cb/Cr, proof in DESIGN.md) away from the next integer, so the
-// truncation is exact everywhere except at exact-integer points, where the
-// precomputed bitmaps say whether the FP64 reference lands one below.
-__device__ __forceinline__ void pixel_ycc(uint32_t B, uint32_t G, uint32_t R,
-                                          const uint32_t *__restrict__ lut,
-                                          int &y, int &cb, int &cr, bool use_lut = true) {
-  float fb = (float)B, fg = (float)G, fr = (float)R;
-  float dr = fr - fg, db = fb - fg;
-  float yf = fmaf(0.114f, db, fmaf(0.299f, dr, fg)) + 0.0005f;
-  y = (int)yf;
-  cb = (int)fmaf(-0.168736f, dr, fmaf(0.5f, db, 128.0f));
-  cr = (int)fmaf(-0.081312f, db, fmaf(0.5f, dr, 128.0f));
-  if (!use_lut) return;
-  if (__builtin_amdgcn_fractf(yf) < 0.001f) {  // exact-integer Y: R, G same parity
-    const uint32_t i = (R << 7) | (G >> 1);
-    y -= (lut[i >> 5] >> (i & 31)) & 1;
-  }
-  if (dr == 0.0f) {  // only R == G can give an integer Cb
-    const uint32_t i = (G << 7) | (B >> 1);
-    cb -= (lut[LUT_WORDS + (i >> 5)] >> (i & 31)) & ((B ^ G) & 1 ? 0u : 1u);
-  }
-  if (db == 0.0f) {  // only B == G can give an integer Cr
-    const uint32_t i = (G << 7) | (R >> 1);
-    cr -= (lut[2 * LUT_WORDS + (i >> 5)] >> (i & 31)) & ((R ^ G) & 1 ? 0u : 1u);
-  }
-}
 
 // DC of one block exactly as encoder.c:87-109: the cosines of frequency 0
 // are exactly 1.0, so both passes are exact integer sums S; what remains is
@@ -233,6 +226,60 @@ __device__ __forceinline__ void issue_tile_dma(const K1Args &a, const TilePos &p
   }
 }
 
+// Colour conversion of 4 pixels (12 bytes) of one row, encoder.c:133-135
+// bit-exactly.  fp32 forms (error < 2e-5 Y, < 1e-5 Cb/Cr) give
+// the truncation everywhere except at exact-integer values, which need equal
+// parities and R == G (Cb) or B == G (Cr); there the device-built bitmaps say
+// whether the FP64 reference lands one below.  The bitmap reads of a 4-pixel
+// run are issued together under one wave-uniform branch.
+__device__ __forceinline__ void convert4(uint32_t w0, uint32_t w1, uint32_t w2,
+                                         const uint32_t *__restrict__ lut, bool use_lut,
+                                         int (&y)[4], int (&cb)[4], int (&cr)[4]) {
+  const uint32_t Bv[4] = {w0 & 255, w0 >> 24, (w1 >> 16) & 255, (w2 >> 8) & 255};
+  const uint32_t Gv[4] = {(w0 >> 8) & 255, w1 & 255, w1 >> 24, (w2 >> 16) & 255};
+  const uint32_t Rv[4] = {(w0 >> 16) & 255, (w1 >> 8) & 255, w2 & 255, w2 >> 24};
+  bool cy = false, cc = false;
+  bool ey[4], eb[4], er[4];
+#pragma unroll
+  for (int p = 0; p < 4; p++) {
+    const float fb = (float)Bv[p], fg = (float)Gv[p], fr = (float)Rv[p];
+    const float dr = __fsub_rn(fr, fg), db = __fsub_rn(fb, fg);
+    const float yf = fmaf(0.114f, db, fmaf(0.299f, dr, fg)) + 0.0005f;
+    y[p] = (int)yf;
+    cb[p] = (int)fmaf(-0.168736f, dr, fmaf(0.5f, db, 128.0f));
+    cr[p] = (int)fmaf(-0.081312f, db, fmaf(0.5f, dr, 128.0f));
+    ey[p] = __builtin_amdgcn_fractf(yf) < 0.001f;  // exact-integer Y
+    eb[p] = dr == 0.0f;                            // only R == G can give an integer Cb
+    er[p] = db == 0.0f;                            // only B == G can give an integer Cr
+    cy |= ey[p];
+    cc |= eb[p] | er[p];
+  }
+  if (!use_lut) return;
+  if (__ballot(cc)) {
+    uint32_t wb[4], wr[4];
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+      wb[p] = lut[LUT_WORDS + ((Gv[p] << 2) | (Bv[p] >> 6))];
+      wr[p] = lut[2 * LUT_WORDS + ((Gv[p] << 2) | (Rv[p] >> 6))];
+    }
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+      // bit (G<<7 | B>>1) of the Cb table; valid when R == G and B == G (mod 2)
+      const uint32_t bb = (wb[p] >> ((Bv[p] >> 1) & 31)) & (eb[p] && !((Bv[p] ^ Gv[p]) & 1));
+      const uint32_t br = (wr[p] >> ((Rv[p] >> 1) & 31)) & (er[p] && !((Rv[p] ^ Gv[p]) & 1));
+      cb[p] -= (int)bb;
+      cr[p] -= (int)br;
+    }
+  }
+  if (__ballot(cy)) {
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+      const uint32_t i = (Rv[p] << 7) | (Gv[p] >> 1);  // integer Y needs R == G (mod 2)
+      if (ey[p]) y[p] -= (lut[i >> 5] >> (i & 31)) & 1;
+    }
+  }
+}
+
 __device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int c4, int pr,
                                              const uint32_t *__restrict__ lut, bool use_lut) {
 #pragma unroll
@@ -242,16 +289,12 @@ __device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int
 #pragma unroll
     for (int dy = 0; dy < 2; dy++) {
       const uint32_t *rw = (const uint32_t *)(raw + (2 * rp + dy) * (TILE_W * 3) + 12 * c4);
-      const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2];
-      int y0, y1, y2, y3;
-      pixel_ycc(w0 & 255, (w0 >> 8) & 255, (w0 >> 16) & 255, lut, y0, cbs[dy][0], crs[dy][0], use_lut);
-      pixel_ycc(w0 >> 24, w1 & 255, (w1 >> 8) & 255, lut, y1, cbs[dy][1], crs[dy][1], use_lut);
-      pixel_ycc((w1 >> 16) & 255, w1 >> 24, w2 & 255, lut, y2, cbs[dy][2], crs[dy][2], use_lut);
-      pixel_ycc((w2 >> 8) & 255, (w2 >> 16) & 255, w2 >> 24, lut, y3, cbs[dy][3], crs[dy][3], use_lut);
+      int yv[4];
+      convert4(rw[0], rw[1], rw[2], lut, use_lut, yv, cbs[dy], crs[dy]);
       const int yrow = 2 * rp + dy;  // 0..15
       const int by = yrow >> 3, bx = c4 >> 1;
-      const uint32_t packed = (uint32_t)y0 | ((uint32_t)y1 << 8) | ((uint32_t)y2 << 16) |
-                              ((uint32_t)y3 << 24);
+      const uint32_t packed = (uint32_t)yv[0] | ((uint32_t)yv[1] << 8) | ((uint32_t)yv[2] << 16) |
+                              ((uint32_t)yv[3] << 24);
       *(uint32_t *)(L + (by * 16 + bx) * LDS_BLK + (yrow & 7) * 8 + (c4 & 1) * 4) = packed;
     }
     // encoder.c:137-138 -- floor((a+b+c+d)/4) of the truncated values
@@ -291,30 +334,40 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
   }
   *(u4v *)&st[lane][0] = c0;
   *(u4v *)&st[lane][8] = c1;
-  uint32_t m16 = 0;
+  // nonzero mask: min(half, 1) per packed int16 pair puts coefficient 2k's
+  // flag at bit 2k and 2k+1's at bit 16+2k
+  uint32_t pm = 0;
 #pragma unroll
-  for (int k = 0; k < 16; k++) m16 |= (o[k] != 0 ? 1u : 0u) << k;
+  for (int k = 0; k < 8; k++) {
+    const uint32_t w = k < 4 ? c0[k] : c1[k - 4];
+    us2 h = __builtin_bit_cast(us2, w);
+    h = __builtin_elementwise_min(h, (us2){1, 1});
+    pm |= __builtin_bit_cast(uint32_t, h) << (2 * k);
+  }
+  uint32_t m16 = (pm & 0x5555u) | ((pm >> 15) & 0xAAAAu);
   if (g == 0) m16 &= ~1u;  // the DC is not part of the AC run structure
-  unsigned long long M = (unsigned long long)m16 << (16 * g);
-  M |= __shfl_xor(M, 16);
-  M |= __shfl_xor(M, 32);
+  // the block's 64-bit mask: rows 0|1 form the low word, rows 2|3 the high
+  uint32_t h = m16 << (16 * (g & 1));
+  const auto r16 = __builtin_amdgcn_permlane16_swap(h, h, false, false);
+  h = r16[0] | r16[1];
+  const auto r32 = __builtin_amdgcn_permlane32_swap(h, h, false, false);
+  const unsigned long long M = ((unsigned long long)r32[1] << 32) | r32[0];
   const int eob = !((M >> 63) & 1ull);
   const int n = valid ? 1 + __popcll(M) + eob : 0;
   // token offsets of the blocks inside their segment (chroma rows hold two
   // 8-block segments: Cb | Cr)
   const int pos = chroma ? (bcol & 7) : bcol;
-  int incl = n;
-#pragma unroll
-  for (int off = 1; off < 16; off <<= 1) {
-    const int y = __shfl_up(incl, off, 16);
-    if (pos >= off) incl += y;
-  }
-  const int base = incl - n;
+  uint32_t incl = (uint32_t)n;
+  incl += row_shr0<1>(incl) & (pos >= 1 ? ~0u : 0u);
+  incl += row_shr0<2>(incl) & (pos >= 2 ? ~0u : 0u);
+  incl += row_shr0<4>(incl) & (pos >= 4 ? ~0u : 0u);
+  if (!chroma) incl += row_shr0<8>(incl);
+  const int base = (int)incl - n;
   const int dc0 = o[0];
-  const int prev = __shfl_up(dc0, 1, 16);
+  const int prev = (int)row_shr0<1>((uint32_t)dc0);
   wave_lds_sync();
   if (g == 0) {
-    if (pos == (chroma ? 7 : 15)) *segcnt = (uint32_t)incl;
+    if (pos == (chroma ? 7 : 15)) *segcnt = incl;
     if (valid) {
       if (dc_diffed || pos != 0) {
         const int diff = dc_diffed ? dc0 : dc0 - prev;  // :168-177
@@ -520,7 +573,7 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
         if (TOK) {
           const long long fs = (long long)p.f * G.nseg + seg;
           const int slot = p.f - f0;
-          emit_tokens(o, lane, g, bcol, valid, comp == 1, !PIX, a.tok + fs * SEG_TOK,
+          emit_tokens(o, lane, g, bcol, valid, comp == 1, !PIX && a.dc_diffed, a.tok + fs * SEG_TOK,
                       a.seg_ntok + fs, s_hdc[TOK ? slot : 0][comp], s_hac[TOK ? slot : 0][comp],
                       s_st[wave]);
         }
@@ -844,17 +897,18 @@ __global__ __launch_bounds__(256) void k_seg_bits(EntArgs a) {
   const int s0 = (blockIdx.x - f * per) * SEG_PER_WG;
   for (int i = threadIdx.x; i < 1024; i += 256) tab[i >> 8][i & 255] = a.ehuf[(long long)f * 1024 + i];
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int s = s0 + wave; s < min(s0 + SEG_PER_WG, a.g.nseg); s += 4) {
+  // 16 lanes per segment, 16 segments in flight per workgroup
+  const int sub = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int send = min(s0 + SEG_PER_WG, a.g.nseg);
+  for (int s = s0 + grp; s < send; s += 16) {
     const long long fs = (long long)f * a.g.nseg + s;
-    const int n = (int)a.seg_ntok[fs];
+    const int n = min((int)a.seg_ntok[fs], SEG_TOK);
     const uint32_t *tk = a.tok + fs * SEG_TOK;
     const int chroma = s >= a.g.nsy;
     uint32_t b = 0;
-    for (int i = lane; i < n; i += 64) b += tok_bits(tk[i], tab, chroma);
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) b += __shfl_xor(b, off);
-    if (lane == 0) a.seg_bits[fs] = b;
+    for (int i = sub; i < n; i += 16) b += tok_bits(tk[i], tab, chroma);
+    b = row_scan16(b);
+    if (sub == 15) a.seg_bits[fs] = b;
   }
 }
 
@@ -912,9 +966,22 @@ __device__ __forceinline__ void put_bits(uint32_t *buf, uint32_t pos, uint32_t v
   }
 }
 
+// the part of a piece that falls inside the LDS window [lo_bit, hi_bit)
+__device__ __forceinline__ void put_bits_window(uint32_t *buf, uint32_t pos, uint32_t lo_bit,
+                                                uint32_t hi_bit, uint32_t val, int len) {
+  const uint32_t w = pos >> 5, wl = lo_bit >> 5, wh = hi_bit >> 5;
+  const int sh = 32 - (int)(pos & 31) - len;
+  if (sh >= 0) {
+    if (w >= wl && w < wh) atomicOr(&buf[w - wl], val << sh);
+  } else {
+    if (w >= wl && w < wh) atomicOr(&buf[w - wl], val >> (-sh));
+    if (w + 1 >= wl && w + 1 < wh) atomicOr(&buf[w + 1 - wl], val << (32 + sh));
+  }
+}
+
 __global__ __launch_bounds__(256) void k_pack(EntArgs a) {
   __shared__ uint32_t buf[PACK_WORDS];
-  __shared__ uint32_t tab[4][256];
+  __shared__ uint32_t tab[2][256];  // this component's DC and AC codes
   const Geom &G = a.g;
   const int gy = (G.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (G.nsc + PACK_SEGS - 1) / PACK_SEGS;
   const int gpf = gy + 2 * gc;
@@ -929,59 +996,69 @@ __global__ __launch_bounds__(256) void k_pack(EntArgs a) {
     sbase = comp == 1 ? G.nsy : G.nsy + G.nsc;
     ns = G.nsc;
   }
+  const int chroma = comp != 0;
   const int s0 = q * PACK_SEGS, s1 = min(ns, s0 + PACK_SEGS);
   const long long fs0 = (long long)f * G.nseg + sbase;
-  for (int i = threadIdx.x; i < 1024; i += 256) tab[i >> 8][i & 255] = a.ehuf[(long long)f * 1024 + i];
+  for (int i = threadIdx.x; i < 512; i += 256)
+    tab[i >> 8][i & 255] = a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + i];
   const unsigned long long gbase = a.seg_off[fs0 + s0];
   const unsigned long long gend = a.seg_off[fs0 + s1 - 1] + a.seg_bits[fs0 + s1 - 1];
   const uint32_t bit0 = (uint32_t)(gbase & 31);
-  const uint32_t nw = (uint32_t)((bit0 + (gend - gbase) + 31) >> 5);
-  for (uint32_t i = threadIdx.x; i < nw; i += 256) buf[i] = 0;
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int chroma = comp != 0;
-  const int t0 = chroma ? 2 : 0;
-  const uint32_t zac = tab[t0 + 1][0xF0];
-  const int Lz = (int)(zac >> 16);
-  for (int s = s0 + wave; s < s1; s += 4) {
-    const long long fs = fs0 + s;
-    const int n = (int)a.seg_ntok[fs];
-    const uint32_t *tk = a.tok + fs * SEG_TOK;
-    uint32_t pos0 = bit0 + (uint32_t)(a.seg_off[fs] - gbase);
-    for (int i0 = 0; i0 < n; i0 += 64) {
-      const int i = i0 + lane;
-      const uint32_t t = i < n ? tk[i] : 0u;
-      const uint32_t nb = i < n ? tok_bits(t, tab, chroma) : 0u;
-      uint32_t x = nb;
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off);
-        if (lane >= off) x += y;
-      }
-      if (i < n) {
-        uint32_t pos = pos0 + x - nb;
-        for (uint32_t k = (t >> 8) & 3u; k; k--) {  // encoder.c:490-494 ZRL
-          put_bits(buf, pos, zac & 0xFFFFu, Lz);
-          pos += Lz;
-        }
-        const uint32_t sym = t & 255u, cls = sym & 15u;
-        const uint32_t e = tab[t0 + ((t & TOK_AC) ? 1 : 0)][sym];
-        const int L = (int)(e >> 16) + (int)cls;
-        if (L) put_bits(buf, pos, ((e & 0xFFFFu) << cls) | (t >> 16), L);  // :434-460
-      }
-      pos0 += __shfl(x, 63);
-    }
+  uint32_t nw = (uint32_t)((bit0 + (gend - gbase) + 31) >> 5);  // words of the group
+  if ((gbase >> 5) + nw + 1 > (unsigned long long)G.raw_words[comp]) {  // cannot happen for valid
+    if (threadIdx.x == 0) a.err[f] = 2;                                 // tokens; never write OOB
+    nw = 0;
   }
-  __syncthreads();
   uint32_t *raw = a.raw + (long long)f * G.raw_fs +
                   (comp == 0 ? 0 : G.raw_words[0] + (comp == 2 ? G.raw_words[1] : 0)) +
                   (gbase >> 5);
-  for (uint32_t i = threadIdx.x; i < nw; i += 256) {
-    if (i == 0 || i == nw - 1) atomicOr(&raw[i], buf[i]);
-    else raw[i] = buf[i];
+  // 16 lanes (one DPP row) per segment, 16 segments in flight per workgroup
+  const int sub = threadIdx.x & 15, row = threadIdx.x >> 4;
+  __syncthreads();
+  const uint32_t zac = tab[1][0xF0];
+  const int Lz = (int)(zac >> 16);
+  // window [w0, w0 + PACK_WORDS) of the group's words per pass
+  for (uint32_t w0 = 0; w0 < nw; w0 += PACK_WORDS) {
+    const uint32_t wn = min((uint32_t)PACK_WORDS, nw - w0);
+    const uint32_t lo_bit = w0 * 32, hi_bit = (w0 + wn) * 32;
+    for (uint32_t i = threadIdx.x; i < wn; i += 256) buf[i] = 0;
+    __syncthreads();
+    for (int s = s0 + row; s < s1; s += 16) {
+      const long long fs = fs0 + s;
+      const uint32_t sb = bit0 + (uint32_t)(a.seg_off[fs] - gbase);
+      if (sb >= hi_bit || sb + a.seg_bits[fs] <= lo_bit) continue;  // row-uniform
+      const int n = min((int)a.seg_ntok[fs], SEG_TOK);
+      const uint32_t *tk = a.tok + fs * SEG_TOK;
+      uint32_t pos0 = sb;
+      for (int i0 = 0; i0 < n; i0 += 16) {
+        const int i = i0 + sub;
+        const uint32_t t = i < n ? tk[i] : 0u;
+        const uint32_t sym = t & 255u, cls = sym & 15u;
+        const uint32_t e = i < n ? tab[(t & TOK_AC) ? 1 : 0][sym] : 0u;
+        const uint32_t nz = (t >> 8) & 3u;
+        const uint32_t L = (e >> 16) + cls;
+        const uint32_t nb = i < n ? L + nz * (uint32_t)Lz : 0u;
+        const uint32_t x = row_scan16(nb);
+        uint32_t pos = pos0 + x - nb;
+        if (nb && pos < hi_bit && pos + nb > lo_bit) {
+          for (uint32_t k = nz; k; k--) {  // encoder.c:490-494 ZRL
+            put_bits_window(buf, pos, lo_bit, hi_bit, zac & 0xFFFFu, Lz);
+            pos += Lz;
+          }
+          if (L) put_bits_window(buf, pos, lo_bit, hi_bit, ((e & 0xFFFFu) << cls) | (t >> 16), (int)L);
+        }
+        pos0 += __shfl(x, 15, 16);
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < wn; i += 256) {
+      const uint32_t wi = w0 + i;
+      if (wi == 0 || wi == nw - 1) atomicOr(&raw[wi], buf[i]);
+      else raw[wi] = buf[i];
+    }
+    __syncthreads();
   }
 }
-
 
 // ===========================================================================
 // k_emit: one workgroup per frame assembles the JFIF stream (encoder.c
@@ -994,9 +1071,16 @@ __global__ __launch_bounds__(256) void k_emit(EntArgs a) {
   __shared__ uint32_t s_ff[256];
   __shared__ unsigned long long s_pos;
   const int f = blockIdx.x, tid = threadIdx.x;
-  if (a.err[f]) {
-    if (tid == 0) a.out_len[f] = 0;
-    return;
+  {
+    unsigned long long need = 1024;  // headers, markers, pads
+    for (int c = 0; c < 3; c++) need += 2 * (a.scan_bits[f * 3 + c] >> 3) + 2;
+    if (a.err[f] || need > (unsigned long long)a.g.out_cap ||
+        a.scan_bits[f * 3 + 0] > 32ull * a.g.raw_words[0] ||
+        a.scan_bits[f * 3 + 1] > 32ull * a.g.raw_words[1] ||
+        a.scan_bits[f * 3 + 2] > 32ull * a.g.raw_words[2]) {
+      if (tid == 0) a.out_len[f] = 0;
+      return;
+    }
   }
   uint8_t *out = a.out + (long long)f * a.g.out_cap;
   const HuffCode *hc = a.hc + (long long)f * 4;
@@ -1110,23 +1194,33 @@ __global__ void k_mfma_probe(const int4 *A, const int4 *B, int4 *D) {
 // ===========================================================================
 // host-side launch wrappers (kernels are launched only through these)
 // ===========================================================================
-static int g_k1_blocks_per_cu = -1;
-
-int k1_grid(int device, long long ntiles) {
-  // persistent: at most (resident blocks per CU) x CUs workgroups
-  if (g_k1_blocks_per_cu < 0) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_mcu_dct<K1M_TOK_OUT>, 256, 0) !=
-            hipSuccess ||
+template <int MODE>
+static int k1_blocks_per_cu() {
+  static int nb = -1;
+  if (nb < 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_mcu_dct<MODE>, 256, 0) != hipSuccess ||
         nb < 1)
       nb = 1;
-    g_k1_blocks_per_cu = nb;
   }
-  hipDeviceProp_t prop;
-  int cus = 256;
-  if (hipGetDeviceProperties(&prop, device) == hipSuccess) cus = prop.multiProcessorCount;
+  return nb;
+}
+
+// persistent grid for a K1 variant: at most (resident blocks per CU) x CUs
+int k1_grid(int device, long long ntiles, int mode) {
+  int per_cu = 1;
+  switch (mode) {
+    case K1M_COEF_OUT: per_cu = k1_blocks_per_cu<K1M_COEF_OUT>(); break;
+    case K1M_TOK_OUT: per_cu = k1_blocks_per_cu<K1M_TOK_OUT>(); break;
+    case K1M_COEF_OUT | K1M_TOK_OUT: per_cu = k1_blocks_per_cu<K1M_COEF_OUT | K1M_TOK_OUT>(); break;
+    default: per_cu = k1_blocks_per_cu<K1M_COEF_IN | K1M_TOK_OUT>(); break;
+  }
+  static int cus = -1;
+  if (cus < 0) {
+    hipDeviceProp_t prop;
+    cus = hipGetDeviceProperties(&prop, device) == hipSuccess ? prop.multiProcessorCount : 256;
+  }
   long long want = (ntiles + K1_WAVES - 1) / K1_WAVES;
-  long long cap = (long long)cus * g_k1_blocks_per_cu;
+  long long cap = (long long)cus * per_cu;
   return (int)(want < cap ? want : cap);
 }
 

@@ -21,9 +21,9 @@ EXPORTS = [
     "mij_set_input_stride", "mij_set_quality", "mij_last_error", "mij_strerror",
     "mij_max_jpg_bytes", "mij_encode",
     "mij_batch_create", "mij_batch_destroy", "mij_batch_upload", "mij_batch_set_input",
-    "mij_batch_encode", "mij_batch_keep_coefs", "mij_batch_dct", "mij_batch_sync", "mij_batch_output",
+    "mij_batch_encode", "mij_batch_keep_coefs", "mij_batch_set_split", "mij_batch_dct", "mij_batch_sync", "mij_batch_output",
     "mij_batch_lengths", "mij_batch_coefs", "mij_batch_tables", "mij_batch_set_timing",
-    "mij_batch_stage_ms", "mij_batch_stage_history", "mij_batch_replays", "mij_batch_stream",
+    "mij_batch_stage_ms", "mij_batch_stage_history", "mij_batch_token_count", "mij_batch_geometry", "mij_batch_replays", "mij_batch_stream",
     "mij_probe_mfma", "mij_colour_lut", "mij_build_target",
 ]
 
@@ -84,6 +84,7 @@ def load() -> C.CDLL:
     lib.mij_batch_set_input.argtypes = [p, p, C.c_longlong, i]
     lib.mij_batch_encode.argtypes = [p, i]
     lib.mij_batch_keep_coefs.argtypes = [p, i]
+    lib.mij_batch_set_split.argtypes = [p, i]
     lib.mij_batch_dct.argtypes = [p, i]
     lib.mij_batch_sync.argtypes = [p]
     lib.mij_batch_output.argtypes = [p, i, p, sz, C.POINTER(sz)]
@@ -93,6 +94,9 @@ def load() -> C.CDLL:
     lib.mij_batch_set_timing.argtypes = [p, i]
     lib.mij_batch_stage_ms.argtypes = [p, p, i]
     lib.mij_batch_stage_history.argtypes = [p, p, i]
+    lib.mij_batch_token_count.restype = C.c_ulonglong
+    lib.mij_batch_token_count.argtypes = [p, i]
+    lib.mij_batch_geometry.argtypes = [p, p, i]
     lib.mij_batch_replays.restype = C.c_ulonglong
     lib.mij_batch_replays.argtypes = [p]
     lib.mij_batch_stream.restype = p
@@ -204,6 +208,9 @@ class Batch:
         except Exception:
             pass
 
+    def set_split(self, on: bool) -> None:
+        _check(self.lib.mij_batch_set_split(self.h_, int(on)), "set_split")
+
     def upload(self, frames_bgr: np.ndarray, first: int = 0) -> None:
         frames_bgr = np.ascontiguousarray(frames_bgr, np.uint8)
         n = frames_bgr.shape[0] if frames_bgr.ndim == 4 else 1
@@ -261,6 +268,14 @@ class Batch:
         if n < 0:
             _check(self.lib.mij_last_error(), "stage_history")
         return [dict(zip(self.STAGES, [float(v) for v in row])) for row in ms[:n]]
+
+    def token_count(self, n: int) -> int:
+        return int(self.lib.mij_batch_token_count(self.h_, n))
+
+    def geometry(self) -> dict:
+        g = np.zeros(5, np.int64)
+        _check(self.lib.mij_batch_geometry(self.h_, _ptr(g), 5), "geometry")
+        return dict(zip(["w", "h", "nblk", "nseg", "tiles_per_frame"], [int(v) for v in g]))
 
     def replays(self) -> int:
         return int(self.lib.mij_batch_replays(self.h_))

@@ -252,3 +252,15 @@ def test_c_host_tool_three_call_and_fused():
             out = os.path.join(d, "o.jpg")
             subprocess.check_call([tool, src, out, "50"] + extra, stdout=subprocess.DEVNULL)
             assert open(out, "rb").read() == gold
+
+
+def test_split_pipeline_same_bytes(manifest):
+    """K1 -> coefficient planes -> separate tokenize pass gives the same JFIF."""
+    frames = np.stack([recipes.config3_frame(0, 544, 960), recipes.noise(544, 960, 3)])
+    b = mijpeg.Batch(960, 544, 2)
+    b.set_split(True)
+    b.upload(frames)
+    b.encode(2)
+    for i in range(2):
+        assert b.output(i) == O.cref_encode(frames[i])
+    b.close()
