@@ -29,10 +29,10 @@ for p in (os.path.join(REPO, "jpeg-encoder-decoder_amd"), os.path.join(REPO, "te
     sys.path.insert(0, p)
 
 import mijpeg  # noqa: E402
+import sharding  # noqa: E402
 import recipes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
-K1_COEF_BYTES_PER_PX = 6.0  # coefficient mode: 3 B BGR read + 1.5 int16 coefficients written
 
 
 def parse():
@@ -51,8 +51,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bound on the CPU-baseline sample (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--split", action="store_true",
-                    help="K1 writes coefficients + separate tokenize pass (comparison)")
+    ap.add_argument("--fused", action="store_true",
+                    help="fused pipeline: K1 emits symbol tokens directly (default: split, "
+                         "K1 writes coefficients and a second pass tokenizes)")
     ap.add_argument("--verify", type=int, default=2,
                     help="frames re-checked against the oracle after timing")
     return ap.parse_args()
@@ -125,8 +126,7 @@ def main():
     W, H, F = args.width, args.height, args.frames
     frames = make_frames(args, rank)
     batch = mijpeg.Batch(W, H, F, args.quality, device=local)
-    if args.split:
-        batch.set_split(True)
+    batch.set_split(not args.fused)
     for i in range(F):
         batch.upload(frames[i % len(frames)], first=i)
     run = batch.encode if args.mode == "encode" else batch.dct
@@ -148,16 +148,14 @@ def main():
     batch.sync()
     el = time.perf_counter() - t0
     barrier()
-    if dist is not None:
-        t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    # max time over ranks, pixels over all ranks (sharding.py; no data-path collective)
+    el, px_all = sharding.reduce_timing(el, W * H * F * args.steps, dist, f"cuda:{local}")
 
     hist = batch.stage_history(args.steps)
-    k1_ms = float(np.mean([h["k1_colour_dct_quant"] for h in hist]))
     stage_avg = {k: round(float(np.mean([h[k] for h in hist])), 4) for k in mijpeg.Batch.STAGES}
+    k1_ms, tok_ms = stage_avg["k1_colour_dct_quant"], stage_avg["tokenize"]
     if args.mode == "dct":
-        stage_avg = {"k1_colour_dct_quant": stage_avg["k1_colour_dct_quant"]}
+        stage_avg = {"k1_colour_dct_quant": k1_ms}
 
     # correctness spot check after timing (not timed): frames vs the oracle
     verified = 0
@@ -169,17 +167,27 @@ def main():
             verified += 1
 
     px_step = W * H * F
-    value = world * px_step * args.steps / el / 1e6
+    value = px_all / el / 1e6
     geo = batch.geometry()
-    if args.mode == "encode":
-        # fused K1 (token mode): reads BGR, writes the per-segment symbol
-        # tokens (4 B each), one raw DC (2 B) per block and one count per segment
-        k1_bytes = px_step * 3 + batch.token_count(F) * 4 + F * (geo["nblk"] * 2 + geo["nseg"] * 4)
-        k1_kernel = "k_mcu_dct<TOK_OUT> (K1: colour+DCT+quant+zigzag+symbol tokens)"
+    # algorithmic HBM bytes per launch (DESIGN.md "Roofline accounting"):
+    # BGR in 3 B/px; coefficient planes 2 B x 64 per block (= 3 B/px at 4:2:0);
+    # one raw DC (2 B) per block; tokens 4 B each + one count (4 B) per segment
+    coef_bytes = F * geo["nblk"] * 64 * 2
+    dc_bytes = F * geo["nblk"] * 2
+    tok_bytes = batch.token_count(F) * 4 + F * geo["nseg"] * 4 if args.mode == "encode" else 0
+    kernels = {}
+    if args.mode == "encode" and args.fused:
+        kernels["k_mcu_dct<TOK_OUT>"] = (px_step * 3 + tok_bytes + dc_bytes, k1_ms,
+                                         "K1 fused: colour+DCT+quant+zigzag+symbol tokens")
     else:
-        k1_bytes = K1_COEF_BYTES_PER_PX * px_step + F * geo["nblk"] * 2
-        k1_kernel = "k_mcu_dct<COEF_OUT> (K1: colour+DCT+quant+zigzag -> int16 planes)"
-    k1_gbs = k1_bytes / (k1_ms * 1e-3) / 1e9
+        kernels["k_mcu_dct<COEF_OUT>"] = (px_step * 3 + coef_bytes + dc_bytes, k1_ms,
+                                          "K1: colour+DCT+quant+zigzag -> int16 planes")
+        if args.mode == "encode":
+            kernels["k_mcu_dct<COEF_IN|TOK_OUT>"] = (coef_bytes + tok_bytes, tok_ms,
+                                                     "tokenize: planes -> symbol tokens + histograms")
+    dom = max(kernels, key=lambda k: kernels[k][1])
+    k1_bytes, dom_ms, dom_desc = kernels[dom]
+    k1_gbs = k1_bytes / (dom_ms * 1e-3) / 1e9
     res = {
         "metric": "Mpixels/s encoded (device-resident BGR888 -> JFIF bytes)",
         "value": round(value, 1),
@@ -197,12 +205,16 @@ def main():
         "config": {"workload": f"config 3: {F} x {W}x{H} BGR888 frames per GPU, 4:2:0, "
                                f"Q={args.quality}, one independent JFIF per frame",
                    "frames_per_gpu": F, "width": W, "height": H, "quality": args.quality,
-                   "mode": args.mode, "parallelism": f"frame-parallel x{world}"},
-        "roofline": {"bound": "hbm", "kernel": k1_kernel,
+                   "mode": args.mode, "pipeline": "fused" if args.fused else "split",
+                   "parallelism": f"frame-parallel x{world}"},
+        "roofline": {"bound": "hbm", "kernel": f"{dom} ({dom_desc})",
                      "achieved": round(k1_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(k1_gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                     "k1_ms_per_launch": round(k1_ms, 4),
+                     "ms_per_launch": round(dom_ms, 4),
                      "algorithmic_bytes_per_launch": int(k1_bytes)},
+        "kernels": {k: {"ms": round(v[1], 4), "algorithmic_GB": round(v[0] / 1e9, 3),
+                        "GB_per_s": round(v[0] / (v[1] * 1e-3) / 1e9, 1)}
+                    for k, v in kernels.items()},
         "stages_ms": stage_avg,
         "verified_frames": verified,
         "fp64_replays_per_frame": round(batch.replays() / (F * (args.warmup + args.steps)), 2),

@@ -115,12 +115,13 @@ int mij_batch_upload(mij_batch *b, const uint8_t *bgr, int first, int nframes);
 int mij_batch_set_input(mij_batch *b, const void *d_bgr, long long frame_stride,
                         int pitch);
 int mij_batch_encode(mij_batch *b, int nframes);     /* full path, async */
-/* encode also keeps the coefficient planes (for mij_batch_coefs); off by
- * default: the fused K1 then emits symbol tokens instead of coefficients */
-int mij_batch_keep_coefs(mij_batch *b, int on);
-/* split pipeline: K1 writes coefficient planes and a second, light pass
- * tokenizes them (same output bytes; for performance comparison) */
+/* pipeline: split (default) -- K1 writes zigzag coefficient planes and a
+ * second pass tokenizes them; fused (set_split(b, 0)) -- K1 emits the symbol
+ * tokens directly.  Same output bytes either way. */
 int mij_batch_set_split(mij_batch *b, int on);
+/* fused pipeline only: also keep the coefficient planes (for
+ * mij_batch_coefs); the split pipeline always has them */
+int mij_batch_keep_coefs(mij_batch *b, int on);
 int mij_batch_dct(mij_batch *b, int nframes);        /* K1 only, async */
 int mij_batch_sync(mij_batch *b);
 int mij_batch_output(mij_batch *b, int frame, uint8_t *dst, size_t cap,
@@ -132,9 +133,11 @@ int mij_batch_coefs(mij_batch *b, int frame, int16_t *Y, int16_t *Cb,
                     int16_t *Cr, int diffed);
 int mij_batch_tables(mij_batch *b, int frame, huff_code out[4]);
 /* timing: when enabled, HIP events bracket each stage of the next encode;
- * mij_batch_stage_ms returns up to n stage durations (ms) of the last one:
- * [0]=K1 colour+DCT+quant, [1]=stats, [2]=tables, [3]=bits, [4]=scan,
- * [5]=pack, [6]=emit, [7]=whole encode */
+ * mij_batch_stage_ms returns up to n (<= MIJ_NSTAGES) stage durations (ms) of
+ * the last one: [0]=K1 colour+DCT+quant (+tokens when fused), [1]=tokenize
+ * (split pipeline), [2]=stats (segment DC fixup), [3]=tables, [4]=bits,
+ * [5]=scan, [6]=pack, [7]=emit, [8]=whole encode */
+#define MIJ_NSTAGES 9
 int mij_batch_set_timing(mij_batch *b, int on);
 int mij_batch_stage_ms(mij_batch *b, float *ms, int n);
 /* the same for each of the last `steps` encodes (<= 64) issued while timing

@@ -212,10 +212,10 @@ struct mij_batch {
   int *d_err = nullptr;
   unsigned *d_replays = nullptr;
   bool keep_coefs = false;  // encode also writes coefficient planes
-  bool split = false;       // K1 writes coefficients, a second pass tokenizes
+  bool split = true;        // K1 writes coefficients, a second pass tokenizes
   bool timing = false;
   static constexpr int HIST = 64;
-  hipEvent_t evh[HIST][8] = {};  // per-step events while timing is on
+  hipEvent_t evh[HIST][MIJ_NSTAGES] = {};  // per-step events while timing is on
   hipEvent_t *ev = evh[0];       // current step's events
   long long steps = 0;
   int last_frames = 0;
@@ -404,17 +404,17 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   EntArgs a = ent_args(b, nframes);
   const bool t = b->timing;
   if (dc_fix) HIP_TRY(launch_seg_dc(a, b->stream));
-  if (t) HIP_TRY(hipEventRecord(b->ev[2], b->stream));
-  if (!tables_given) HIP_TRY(launch_tables(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[3], b->stream));
-  HIP_TRY(launch_bits(a, b->stream));
+  if (!tables_given) HIP_TRY(launch_tables(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[4], b->stream));
-  HIP_TRY(launch_scan(a, b->stream));
+  HIP_TRY(launch_bits(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[5], b->stream));
-  HIP_TRY(launch_pack(a, b->stream));
+  HIP_TRY(launch_scan(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[6], b->stream));
-  HIP_TRY(launch_emit(a, b->stream));
+  HIP_TRY(launch_pack(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[7], b->stream));
+  HIP_TRY(launch_emit(a, b->stream));
+  if (t) HIP_TRY(hipEventRecord(b->ev[8], b->stream));
   return MIJ_OK;
 }
 
@@ -423,11 +423,14 @@ static int encode_frames(mij_batch *b, int nframes) {
   HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * nframes, b->stream));
   if (b->timing) HIP_TRY(hipEventRecord(b->ev[0], b->stream));
   if (b->split) {
-    if (run_k1(b, nframes, 1) || run_k1(b, nframes, 6, 0)) return g_err;
-  } else if (run_k1(b, nframes, b->keep_coefs ? 3 : 2)) {
-    return g_err;
+    if (run_k1(b, nframes, 1)) return g_err;
+    if (b->timing) HIP_TRY(hipEventRecord(b->ev[1], b->stream));
+    if (run_k1(b, nframes, 6, 0)) return g_err;
+  } else {
+    if (run_k1(b, nframes, b->keep_coefs ? 3 : 2)) return g_err;
+    if (b->timing) HIP_TRY(hipEventRecord(b->ev[1], b->stream));
   }
-  if (b->timing) HIP_TRY(hipEventRecord(b->ev[1], b->stream));
+  if (b->timing) HIP_TRY(hipEventRecord(b->ev[2], b->stream));
   return run_entropy(b, nframes, true, false);
 }
 
@@ -462,7 +465,8 @@ extern "C" int mij_batch_dct(mij_batch *b, int nframes) {
   next_slot(b);
   if (b->timing) HIP_TRY(hipEventRecord(b->ev[0], b->stream));
   if (run_k1(b, nframes, 1)) return g_err;
-  if (b->timing) HIP_TRY(hipEventRecord(b->ev[1], b->stream));
+  if (b->timing)
+    for (int k = 1; k < MIJ_NSTAGES; k++) HIP_TRY(hipEventRecord(b->ev[k], b->stream));
   return MIJ_OK;
 }
 
@@ -487,8 +491,9 @@ static float elapsed(hipEvent_t a, hipEvent_t z) {
   return v;
 }
 
-static const int k_stage_pairs[8][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4},
-                                        {4, 5}, {5, 6}, {6, 7}, {0, 7}};
+// stage i spans events (i, i+1); the last one is the whole encode
+static const int k_stage_pairs[MIJ_NSTAGES][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5},
+                                                  {5, 6}, {6, 7}, {7, 8}, {0, 8}};
 
 extern "C" int mij_batch_stage_history(mij_batch *b, float *ms, int steps) {
   if (!b || !ms || steps < 1) return fail(MIJ_EINVAL, "stage_history: bad args");
@@ -499,7 +504,7 @@ extern "C" int mij_batch_stage_history(mij_batch *b, float *ms, int steps) {
   for (int i = 0; i < n; i++) {
     const long long step = b->steps - n + i;
     hipEvent_t *e = b->evh[step % mij_batch::HIST];
-    for (int k = 0; k < 8; k++) ms[i * 8 + k] = elapsed(e[k_stage_pairs[k][0]], e[k_stage_pairs[k][1]]);
+    for (int k = 0; k < MIJ_NSTAGES; k++) ms[i * MIJ_NSTAGES + k] = elapsed(e[k_stage_pairs[k][0]], e[k_stage_pairs[k][1]]);
   }
   return n;
 }
@@ -508,7 +513,7 @@ extern "C" int mij_batch_stage_ms(mij_batch *b, float *ms, int n) {
   if (!b || !ms) return fail(MIJ_EINVAL, "stage_ms: bad args");
   HIP_TRY(hipSetDevice(b->dev));
   HIP_TRY(hipStreamSynchronize(b->stream));
-  for (int i = 0; i < n && i < 8; i++) ms[i] = elapsed(b->ev[k_stage_pairs[i][0]], b->ev[k_stage_pairs[i][1]]);
+  for (int i = 0; i < n && i < MIJ_NSTAGES; i++) ms[i] = elapsed(b->ev[k_stage_pairs[i][0]], b->ev[k_stage_pairs[i][1]]);
   return MIJ_OK;
 }
 

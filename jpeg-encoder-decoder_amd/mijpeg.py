@@ -184,7 +184,8 @@ def encode(frame_bgr: np.ndarray, quality: int = 50, region=None) -> bytes:
 # ---- device-resident batch ---------------------------------------------------
 
 class Batch:
-    STAGES = ["k1_colour_dct_quant", "stats", "tables", "bits", "scan", "pack", "emit", "total"]
+    STAGES = ["k1_colour_dct_quant", "tokenize", "stats", "tables", "bits", "scan", "pack", "emit",
+              "total"]
 
     def __init__(self, w: int, h: int, max_frames: int, quality: int = 50, device: int = 0,
                  keep_coefs: bool = False):
@@ -258,12 +259,12 @@ class Batch:
         _check(self.lib.mij_batch_set_timing(self.h_, int(on)), "set_timing")
 
     def stage_ms(self) -> dict:
-        ms = np.zeros(8, np.float32)
-        _check(self.lib.mij_batch_stage_ms(self.h_, _ptr(ms), 8), "stage_ms")
+        ms = np.zeros(len(self.STAGES), np.float32)
+        _check(self.lib.mij_batch_stage_ms(self.h_, _ptr(ms), len(ms)), "stage_ms")
         return dict(zip(self.STAGES, [float(v) for v in ms]))
 
     def stage_history(self, steps: int) -> list:
-        ms = np.zeros((steps, 8), np.float32)
+        ms = np.zeros((steps, len(self.STAGES)), np.float32)
         n = self.lib.mij_batch_stage_history(self.h_, _ptr(ms), steps)
         if n < 0:
             _check(self.lib.mij_last_error(), "stage_history")

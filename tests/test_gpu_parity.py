@@ -254,13 +254,28 @@ def test_c_host_tool_three_call_and_fused():
             assert open(out, "rb").read() == gold
 
 
-def test_split_pipeline_same_bytes(manifest):
-    """K1 -> coefficient planes -> separate tokenize pass gives the same JFIF."""
+@pytest.mark.parametrize("split", [True, False])
+def test_split_and_fused_pipelines_same_bytes(split):
+    """split (K1 -> coefficient planes -> tokenize pass) and fused (K1 emits
+    tokens) give the reference's JFIF."""
     frames = np.stack([recipes.config3_frame(0, 544, 960), recipes.noise(544, 960, 3)])
     b = mijpeg.Batch(960, 544, 2)
-    b.set_split(True)
+    b.set_split(split)
     b.upload(frames)
     b.encode(2)
     for i in range(2):
         assert b.output(i) == O.cref_encode(frames[i])
+    b.close()
+
+
+def test_fused_pipeline_keep_coefs_golden(manifest):
+    ent = manifest["sample_640x640"]
+    bgr = case_input("sample_640x640", ent)
+    b = mijpeg.Batch(640, 640, 1, keep_coefs=True)
+    b.set_split(False)
+    b.upload(bgr)
+    b.encode(1)
+    assert sha(b.output(0)) == ent["jpg_sha256"]
+    Y, Cb, Cr = b.coefs(0, diffed=True)
+    assert [sha(Y), sha(Cb), sha(Cr)] == ent["coef_sha256"]
     b.close()
