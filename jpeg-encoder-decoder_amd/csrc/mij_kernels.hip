@@ -140,27 +140,40 @@ __device__ __forceinline__ int dc_exact(int S, int q) {
   return t < -2048 ? -2048 : (t > 2047 ? 2047 : t);
 }
 
+// DC fast path: the reference's FP64 DC (dc_exact) equals trunc(S / 8q) with
+// the sign of S, except possibly when |S| is a multiple of 8q (then its FP64
+// roundings decide between K and K-1).  k = trunc(|S|*fl(1/8q) + 2e-4) is
+// floor(|S|/8q) exactly: the fp32 error is < 1.2e-4 and a non-integer |S|/8q
+// is >= 1/2040 from an integer.  `tie` flags the |S| = K*8q (K > 0) case.
+__device__ __forceinline__ int dc_fast(int S, int q8, float inv8q, bool &tie) {
+  const int s = S >> 31;
+  const int a = (S ^ s) - s;
+  const int k = (int)fmaf((float)a, inv8q, 2e-4f);
+  tie = a != 0 && k * q8 == a;
+  return (k ^ s) - s;
+}
+
 // One AC coefficient replayed exactly as encoder.c:87-109 computes it
 // (column pass summed from 0 in y order, row pass in x order, FP64, no FMA).
-// C = the 64 cosines (LDS), blk = the block's 64 staged pixels (LDS).
+// C = the 64 cosines (LDS), blk = the block's 64 staged pixels (LDS).  The
+// eight column sums are independent chains, evaluated side by side.
 __device__ __forceinline__ int ac_exact(const uint8_t *blk, int z, int q, const double *C) {
   const int rz = c_zigzag[z];
   const int v = rz >> 3, u = rz & 7;
-  double cv[8];
+  double inner[8];
 #pragma unroll
-  for (int y = 0; y < 8; y++) cv[y] = C[y * 8 + v];
-  uint64_t rows[8];
+  for (int x = 0; x < 8; x++) inner[x] = 0.0;
+#pragma unroll 2
+  for (int y = 0; y < 8; y++) {
+    const double cv = C[y * 8 + v];
+    const uint64_t row = *(const uint64_t *)(blk + y * 8);
 #pragma unroll
-  for (int y = 0; y < 8; y++) rows[y] = *(const uint64_t *)(blk + y * 8);
-  double freq = 0.0;
-#pragma unroll 1
-  for (int x = 0; x < 8; x++) {  // rare path: keep register pressure low
-    double inner = 0.0;
-#pragma unroll
-    for (int y = 0; y < 8; y++)
-      inner = __dadd_rn(inner, __dmul_rn((double)((int)((rows[y] >> (8 * x)) & 255) - 128), cv[y]));
-    freq = __dadd_rn(freq, __dmul_rn(inner, C[x * 8 + u]));
+    for (int x = 0; x < 8; x++)
+      inner[x] = __dadd_rn(inner[x], __dmul_rn((double)((int)((row >> (8 * x)) & 255) - 128), cv));
   }
+  double freq = 0.0;
+#pragma unroll
+  for (int x = 0; x < 8; x++) freq = __dadd_rn(freq, __dmul_rn(inner[x], C[x * 8 + u]));
   if (u == 0) freq = __dmul_rn(freq, SQRT1_2);
   if (v == 0) freq = __dmul_rn(freq, SQRT1_2);
   freq = __dmul_rn(freq, 0.25);
@@ -216,15 +229,28 @@ __device__ __forceinline__ void issue_tile_dma(const K1Args &a, const TilePos &p
   const uint8_t *src = a.in + (long long)p.f * a.in_fs + (long long)(p.ty * TILE_H) * a.pitch +
                        p.tx * TILE_W * 3;
   const int vb = p.valid_px * 3;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t *)raw);
 #pragma unroll
   for (int k = 0; k < TILE_RAW / 1024; k++) {
     const int pos = 1024 * k + 16 * lane;
     const int row = pos / (TILE_W * 3), col = pos - row * (TILE_W * 3);
-    if (col < vb)
-      __builtin_amdgcn_global_load_lds((global_void_t *)(src + (long long)row * a.pitch + col),
-                                       (lds_void_t *)(raw + 1024 * k), 16, 0, 0);
+    if (col < vb) {
+      // issued as asm so the compiler does not tie the next LDS read of `raw`
+      // to vmcnt(0) -- that wait would also drain the previous tile's
+      // coefficient stores; K1 waits for the DMA itself (dma_wait) before
+      // its first store, when the DMA has long landed
+      const uint8_t *g = src + (long long)row * a.pitch + col;
+      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off"
+                   :
+                   : "v"(g), "s"(lds0 + 1024 * k)
+                   : "memory", "m0");
+    }
   }
 }
+
+// all of this wave's outstanding vector-memory operations (the tile DMA above
+// included) have completed; VMEM operations retire in issue order
+__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Colour conversion of 4 pixels (12 bytes) of one row, encoder.c:133-135
 // bit-exactly.  fp32 forms (error < 2e-5 Y, < 1e-5 Cb/Cr) give
@@ -232,19 +258,38 @@ __device__ __forceinline__ void issue_tile_dma(const K1Args &a, const TilePos &p
 // parities and R == G (Cb) or B == G (Cr); there the device-built bitmaps say
 // whether the FP64 reference lands one below.  The bitmap reads of a 4-pixel
 // run are issued together under one wave-uniform branch.
+// byte N of w as float (v_cvt_f32_ubyteN); asm keeps the compiler from
+// rewriting fsub(cvt(a), cvt(b)) into cvt(sub(a, b)), which costs two slow
+// conversions instead of one
+template <int N>
+__device__ __forceinline__ float ubyte_f32(uint32_t w) {
+  float r;
+  if constexpr (N == 0) asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(r) : "v"(w));
+  else if constexpr (N == 1) asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(r) : "v"(w));
+  else if constexpr (N == 2) asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(r) : "v"(w));
+  else asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(r) : "v"(w));
+  return r;
+}
+
+// Colour conversion of 4 pixels (12 bytes) of one row, encoder.c:133-135
+// bit-exactly.  fp32 forms (error < 2e-5 Y, < 1.1e-5 Cb/Cr)
+// give the truncation everywhere except at exact-integer values, which need
+// equal parities and R == G (Cb) or B == G (Cr); there the device-built
+// bitmaps say whether the FP64 reference lands one below.  The bitmap reads
+// of a 4-pixel run are issued together under one wave-uniform branch.
 __device__ __forceinline__ void convert4(uint32_t w0, uint32_t w1, uint32_t w2,
                                          const uint32_t *__restrict__ lut, bool use_lut,
                                          int (&y)[4], int (&cb)[4], int (&cr)[4]) {
-  const uint32_t Bv[4] = {w0 & 255, w0 >> 24, (w1 >> 16) & 255, (w2 >> 8) & 255};
-  const uint32_t Gv[4] = {(w0 >> 8) & 255, w1 & 255, w1 >> 24, (w2 >> 16) & 255};
-  const uint32_t Rv[4] = {(w0 >> 16) & 255, (w1 >> 8) & 255, w2 & 255, w2 >> 24};
+  // BGR of pixel p: w0 = B0 G0 R0 B1, w1 = G1 R1 B2 G2, w2 = R2 B3 G3 R3
+  const float fb[4] = {ubyte_f32<0>(w0), ubyte_f32<3>(w0), ubyte_f32<2>(w1), ubyte_f32<1>(w2)};
+  const float fg[4] = {ubyte_f32<1>(w0), ubyte_f32<0>(w1), ubyte_f32<3>(w1), ubyte_f32<2>(w2)};
+  const float fr[4] = {ubyte_f32<2>(w0), ubyte_f32<1>(w1), ubyte_f32<0>(w2), ubyte_f32<3>(w2)};
   bool cy = false, cc = false;
   bool ey[4], eb[4], er[4];
 #pragma unroll
   for (int p = 0; p < 4; p++) {
-    const float fb = (float)Bv[p], fg = (float)Gv[p], fr = (float)Rv[p];
-    const float dr = __fsub_rn(fr, fg), db = __fsub_rn(fb, fg);
-    const float yf = fmaf(0.114f, db, fmaf(0.299f, dr, fg)) + 0.0005f;
+    const float dr = fr[p] - fg[p], db = fb[p] - fg[p];
+    const float yf = fmaf(0.114f, db, fmaf(0.299f, dr, fg[p])) + 0.0005f;
     y[p] = (int)yf;
     cb[p] = (int)fmaf(-0.168736f, dr, fmaf(0.5f, db, 128.0f));
     cr[p] = (int)fmaf(-0.081312f, db, fmaf(0.5f, dr, 128.0f));
@@ -255,27 +300,32 @@ __device__ __forceinline__ void convert4(uint32_t w0, uint32_t w1, uint32_t w2,
     cc |= eb[p] | er[p];
   }
   if (!use_lut) return;
-  if (__ballot(cc)) {
-    uint32_t wb[4], wr[4];
+  if (__ballot(cc | cy)) {
+    const uint32_t Bv[4] = {w0 & 255, w0 >> 24, (w1 >> 16) & 255, (w2 >> 8) & 255};
+    const uint32_t Gv[4] = {(w0 >> 8) & 255, w1 & 255, w1 >> 24, (w2 >> 16) & 255};
+    const uint32_t Rv[4] = {(w0 >> 16) & 255, (w1 >> 8) & 255, w2 & 255, w2 >> 24};
+    if (__ballot(cc)) {
+      uint32_t wb[4], wr[4];
 #pragma unroll
-    for (int p = 0; p < 4; p++) {
-      wb[p] = lut[LUT_WORDS + ((Gv[p] << 2) | (Bv[p] >> 6))];
-      wr[p] = lut[2 * LUT_WORDS + ((Gv[p] << 2) | (Rv[p] >> 6))];
+      for (int p = 0; p < 4; p++) {
+        wb[p] = lut[LUT_WORDS + ((Gv[p] << 2) | (Bv[p] >> 6))];
+        wr[p] = lut[2 * LUT_WORDS + ((Gv[p] << 2) | (Rv[p] >> 6))];
+      }
+#pragma unroll
+      for (int p = 0; p < 4; p++) {
+        // bit (G<<7 | B>>1) of the Cb table; valid when R == G and B == G (mod 2)
+        const uint32_t bb = (wb[p] >> ((Bv[p] >> 1) & 31)) & (eb[p] && !((Bv[p] ^ Gv[p]) & 1));
+        const uint32_t br = (wr[p] >> ((Rv[p] >> 1) & 31)) & (er[p] && !((Rv[p] ^ Gv[p]) & 1));
+        cb[p] -= (int)bb;
+        cr[p] -= (int)br;
+      }
     }
+    if (__ballot(cy)) {
 #pragma unroll
-    for (int p = 0; p < 4; p++) {
-      // bit (G<<7 | B>>1) of the Cb table; valid when R == G and B == G (mod 2)
-      const uint32_t bb = (wb[p] >> ((Bv[p] >> 1) & 31)) & (eb[p] && !((Bv[p] ^ Gv[p]) & 1));
-      const uint32_t br = (wr[p] >> ((Rv[p] >> 1) & 31)) & (er[p] && !((Rv[p] ^ Gv[p]) & 1));
-      cb[p] -= (int)bb;
-      cr[p] -= (int)br;
-    }
-  }
-  if (__ballot(cy)) {
-#pragma unroll
-    for (int p = 0; p < 4; p++) {
-      const uint32_t i = (Rv[p] << 7) | (Gv[p] >> 1);  // integer Y needs R == G (mod 2)
-      if (ey[p]) y[p] -= (lut[i >> 5] >> (i & 31)) & 1;
+      for (int p = 0; p < 4; p++) {
+        const uint32_t i = (Rv[p] << 7) | (Gv[p] >> 1);  // integer Y needs R == G (mod 2)
+        if (ey[p]) y[p] -= (lut[i >> 5] >> (i & 31)) & 1;
+      }
     }
   }
 }
@@ -413,8 +463,7 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
   __shared__ __attribute__((aligned(16))) uint8_t s_tile[PIX ? K1_WAVES : 1][LDS_WAVE];
   __shared__ __attribute__((aligned(16))) int4 s_A[PIX ? 12 * 64 : 1];
   __shared__ __attribute__((aligned(16))) float s_fac[2][64];
-  __shared__ __attribute__((aligned(16))) float s_tau[2][64];
-  __shared__ __attribute__((aligned(16))) float s_rel[2][64];
+  __shared__ float s_inv8q[2];
   __shared__ uint32_t s_lut[PIX ? 3 * LUT_WORDS : 1];
   __shared__ double s_cos[64];
   __shared__ int s_qint[2][64];
@@ -430,18 +479,18 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
     if (threadIdx.x < 64) (&s_hdc[0][0][0])[threadIdx.x] = 0;
   }
   if (threadIdx.x < 128) s_qint[threadIdx.x >> 6][threadIdx.x & 63] = T->qint[threadIdx.x >> 6][threadIdx.x & 63];
+  if (threadIdx.x < 2) s_inv8q[threadIdx.x] = 1.0f / (float)(8 * T->qint[threadIdx.x][0]);
   if (PIX) {
     for (int i = threadIdx.x; i < 12 * 64; i += 256) s_A[i] = T->mfma_a[i];
     for (int i = threadIdx.x; i < 3 * LUT_WORDS; i += 256) s_lut[i] = (&T->lut[0][0])[i];
   }
   for (int i = threadIdx.x; i < 128; i += 256) {
     s_fac[i >> 6][i & 63] = T->qfac[i >> 6][i & 63];
-    s_tau[i >> 6][i & 63] = T->qtau[i >> 6][i & 63];
-    s_rel[i >> 6][i & 63] = T->qrel[i >> 6][i & 63];
   }
   __syncthreads();
 
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR: tile math on SALU
   uint8_t *L = s_tile[PIX ? wave : 0];
   const int g = lane >> 4, bcol = lane & 15;
   const int c4 = lane & 31, pr = lane >> 5;
@@ -460,7 +509,10 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
     for (; t < tend; t += K1_WAVES) {
       TilePos pn = p;
       if (PIX) {
-        // ---- 1. colour convert + subsample + stage (waits for this tile's DMA)
+        // ---- 1. colour convert + subsample + stage.  This tile's DMA was
+        // waited for before the previous tile's stores (dma_wait), except for
+        // the first tile and when the DCT phase is skipped (diagnostics).
+        if (t == t0 + wave || (a.flags & K1F_NO_DCT)) dma_wait();
         if (!(a.flags & K1F_NO_COLOUR)) colour_stage(raw, L, c4, pr, s_lut, !(a.flags & K1F_NO_LUT));
         wave_lds_sync();
         // ---- stream the wave's next tile into the freed raw buffer -----------
@@ -472,9 +524,48 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
         pn = tile_pos(G, t + K1_WAVES);
       }
 
-      // ---- 2-4. DCT on MFMA, quantize, emit ----------------------------------
-#pragma unroll 1
-      for (int nt = 0; nt < ((a.flags & K1F_NO_DCT) ? 0 : 3); nt++) {
+      // ---- 2. DCT on MFMA for the tile's three N-tiles ------------------------
+      // N = ((D2.X << 7) + D1.X << 7) + D0.X, accumulated in place: each
+      // digit's MFMA takes the shifted partial sum as its C input.  The A
+      // fragments are read once per tile and the 12 chains (3 N-tiles x 4
+      // M-tiles) are issued digit by digit so no MFMA waits on its
+      // predecessor's result.
+      const bool do_dct = !(a.flags & K1F_NO_DCT);
+      v4i acc[3][4];
+      float lc[3];  // per block: error bound of N in N units (before the fp32 term)
+      if (PIX && do_dct) {
+        v4i Bf[3];
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++) {
+          Bf[nt] = *(const v4i *)(L + (nt * 16 + bcol) * LDS_BLK + 16 * g);
+          // L1 = sum |pixel - 128| of the block bounds the integer DCT's
+          // rounding error: |N - 2^19 sum K X| <= sum |W - 2^19 K| |X| <= L1 / 2
+          uint32_t l1 = 0;
+#pragma unroll
+          for (int k = 0; k < 4; k++) l1 = __builtin_amdgcn_sad_u8((uint32_t)Bf[nt][k], 0x80808080u, l1);
+          const auto r16 = __builtin_amdgcn_permlane16_swap(l1, l1, false, false);
+          l1 = r16[0] + r16[1];
+          const auto r32 = __builtin_amdgcn_permlane32_swap(l1, l1, false, false);
+          lc[nt] = fmaf((float)(r32[0] + r32[1]), 0.625f, 80.0f);  // 1.25 * (L1/2 + 64)
+          Bf[nt] ^= (int)0x80808080;  // pixel - 128 as int8
+        }
+#pragma unroll
+        for (int d = 0; d < 3; d++)
+#pragma unroll
+          for (int m = 0; m < 4; m++) {
+            const int4 F = s_A[(3 * m + d) * 64 + lane];
+            const v4i Fv = {F.x, F.y, F.z, F.w};
+#pragma unroll
+            for (int nt = 0; nt < 3; nt++) {
+              const v4i c = d == 0 ? v4i{0, 0, 0, 0} : acc[nt][m] << 7;
+              acc[nt][m] = (a.flags & K1F_NO_MFMA) ? c + Fv + Bf[nt]
+                                                   : __builtin_amdgcn_mfma_i32_16x16x64_i8(Fv, Bf[nt], c, 0, 0, 0);
+            }
+          }
+      }
+
+      // ---- 3-4. quantize, replay, store, emit -----------------------------------
+      auto finish = [&](const int nt, int (&o)[16]) {
         const int comp = nt == 2 ? 1 : 0;
         bool valid;
         int blk;  // block index inside the frame's coefficient space
@@ -490,60 +581,7 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
           blk = G.nY + (bcol >= 8 ? G.nC : 0) + p.ty * mw + mx;
           seg = G.nsy + (bcol >= 8 ? G.nsc : 0) + p.ty * G.tiles_x + p.tx;
         }
-        int o[16];
-        if (PIX) {
-          const uint8_t *Pb = L + (nt * 16 + bcol) * LDS_BLK;
-          v4i Bf = *(const v4i *)(Pb + 16 * g);
-          Bf ^= (int)0x80808080;  // pixel - 128 as int8
-          // N = ((D2.X << 7) + D1.X << 7) + D0.X, accumulated in place: each
-          // digit's MFMA takes the shifted partial sum as its C input
-          v4i acc[4];
-#pragma unroll
-          for (int m = 0; m < 4; m++) {
-            const int4 F2 = s_A[(3 * m + 0) * 64 + lane];
-            const int4 F1 = s_A[(3 * m + 1) * 64 + lane];
-            const int4 F0 = s_A[(3 * m + 2) * 64 + lane];
-            const v4i zero = {0, 0, 0, 0};
-            v4i tt = __builtin_amdgcn_mfma_i32_16x16x64_i8(v4i{F2.x, F2.y, F2.z, F2.w}, Bf, zero, 0, 0, 0);
-            tt = __builtin_amdgcn_mfma_i32_16x16x64_i8(v4i{F1.x, F1.y, F1.z, F1.w}, Bf, tt << 7, 0, 0, 0);
-            acc[m] = __builtin_amdgcn_mfma_i32_16x16x64_i8(v4i{F0.x, F0.y, F0.z, F0.w}, Bf, tt << 7, 0, 0, 0);
-          }
-          uint32_t hz = 0;  // coefficients whose +-tau interval straddles a boundary
-#pragma unroll
-          for (int m = 0; m < 4; m++) {
-            const float4 fac = *(const float4 *)&s_fac[comp][16 * g + 4 * m];
-            const float4 tau = *(const float4 *)&s_tau[comp][16 * g + 4 * m];
-            const float4 rel = *(const float4 *)&s_rel[comp][16 * g + 4 * m];
-            const float fa[4] = {fac.x, fac.y, fac.z, fac.w};
-            const float ta[4] = {tau.x, tau.y, tau.z, tau.w};
-            const float ra[4] = {rel.x, rel.y, rel.z, rel.w};
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-              const int k = 4 * m + r;
-              const float nf = (float)acc[m][r];
-              const float tv = fmaf(fabsf(nf), ra[r], ta[r]);  // tau for this value
-              const int lo = (int)fmaf(nf, fa[r], -tv);
-              const int hi = (int)fmaf(nf, fa[r], tv);
-              o[k] = lo;
-              hz |= (uint32_t)(hi - lo) << k;  // hi - lo is 0 or 1 (2*tau < 1)
-            }
-          }
-          if (g == 0) o[0] = dc_exact(acc[0][0], q_dc[comp]);  // z = 0: fac = tau = 0
-          if (__ballot(hz != 0) && !(a.flags & K1F_NO_REPLAY)) {
-            int16_t *rep = s_st[wave][lane];
-            uint32_t mm = hz;
-            while (mm) {
-              const int k = __ffs(mm) - 1;
-              mm &= mm - 1u;
-              const int z = 16 * g + k;
-              rep[k] = (int16_t)ac_exact(Pb, z, s_qint[comp][z], s_cos);
-            }
-#pragma unroll
-            for (int k = 0; k < 16; k++)
-              if ((hz >> k) & 1u) o[k] = rep[k];
-            if (hz) atomicAdd(a.replays, (unsigned)__popc(hz));
-          }
-        } else {  // coefficients from memory (drop-in write_jpg / init_huffman)
+        if (!PIX) {  // coefficients from memory (drop-in write_jpg / init_huffman)
           u4v c0 = {0, 0, 0, 0}, c1 = {0, 0, 0, 0};
           if (valid) {
             const int16_t *src = a.coef + (long long)p.f * G.coef_fs + (long long)blk * 64 + 16 * g;
@@ -576,6 +614,76 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
           emit_tokens(o, lane, g, bcol, valid, comp == 1, !PIX && a.dc_diffed, a.tok + fs * SEG_TOK,
                       a.seg_ntok + fs, s_hdc[TOK ? slot : 0][comp], s_hac[TOK ? slot : 0][comp],
                       s_st[wave]);
+        }
+      };
+      if (PIX && do_dct) {
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++) {
+          const int comp = nt == 2 ? 1 : 0;
+          int o[16];
+          uint32_t hz = 0;  // nonzero iff some coefficient's +-tau interval straddles a boundary
+          if (a.flags & K1F_NO_QUANT) {
+#pragma unroll
+            for (int k = 0; k < 16; k++) o[k] = acc[nt][k >> 2][k & 3];
+          } else
+#pragma unroll
+          for (int m = 0; m < 4; m++) {
+            const float4 fac = *(const float4 *)&s_fac[comp][16 * g + 4 * m];
+            const float fa[4] = {fac.x, fac.y, fac.z, fac.w};
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+              const float nf = (float)acc[nt][m][r];
+              // tau = fac * (lc + 3e-7 |N|) + 1e-6
+              const float tv = fmaf(fmaf(fabsf(nf), 3.0e-7f, lc[nt]), fa[r], 1.0e-6f);
+              const int lo = (int)fmaf(nf, fa[r], -tv);
+              const int hi = (int)fmaf(nf, fa[r], tv);
+              o[4 * m + r] = lo;
+              hz |= (uint32_t)(hi ^ lo);
+            }
+          }
+          {  // z = 0: exact from the pixel sum (fac = 0 above)
+            bool tie;
+            const int dcv = dc_fast(acc[nt][0][0], 8 * q_dc[comp], s_inv8q[comp], tie);
+            if (g == 0) o[0] = dcv;
+            if (__ballot(tie && g == 0))
+              if (g == 0 && tie) o[0] = dc_exact(acc[nt][0][0], q_dc[comp]);
+          }
+          if (__ballot(hz != 0) && !(a.flags & K1F_NO_REPLAY)) {
+            // rare path: find the straddling coefficients (same arithmetic) and
+            // recompute them in FP64 exactly as encoder.c:87-109
+            const uint8_t *Pb = L + (nt * 16 + bcol) * LDS_BLK;
+            uint32_t mm = 0;
+#pragma unroll
+            for (int m = 0; m < 4; m++)
+#pragma unroll
+              for (int r = 0; r < 4; r++) {
+                const int k = 4 * m + r;
+                const float nf = (float)acc[nt][m][r];
+                const float fa = s_fac[comp][16 * g + k];
+                const float tv = fmaf(fmaf(fabsf(nf), 3.0e-7f, lc[nt]), fa, 1.0e-6f);
+                mm |= (uint32_t)((int)fmaf(nf, fa, -tv) != (int)fmaf(nf, fa, tv)) << k;
+              }
+            const uint32_t hm = mm;
+            int16_t *rep = s_st[wave][lane];
+            while (mm) {
+              const int k = __ffs(mm) - 1;
+              mm &= mm - 1u;
+              const int z = 16 * g + k;
+              rep[k] = (int16_t)ac_exact(Pb, z, s_qint[comp][z], s_cos);
+            }
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+              if ((hm >> k) & 1u) o[k] = rep[k];
+            if (hm) atomicAdd(a.replays, (unsigned)__popc(hm));
+          }
+          if (nt == 0) dma_wait();  // next tile's DMA has landed; no store is outstanding
+          finish(nt, o);
+        }
+      } else if (!PIX) {
+#pragma unroll 1
+        for (int nt = 0; nt < 3; nt++) {
+          int o[16];
+          finish(nt, o);
         }
       }
       if (PIX) wave_lds_sync();

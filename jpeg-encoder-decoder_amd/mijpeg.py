@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmijpeg.so")
+# MIJ_LIB: alternative build of the same library (A/B timing runs, scripts/ab.sh)
+LIB_PATH = os.environ.get("MIJ_LIB") or os.path.join(HERE, "libmijpeg.so")
 
 EXPORTS = [
     # drop-in (reference include/encoder.h:10-12)

@@ -1,24 +1,28 @@
 #!/bin/bash
-# scripts/pmc_k1.sh -- SQ counters on K1 (separate passes; no tracing domains)
+# scripts/pmc_k1.sh -- SQ/SQC counter passes on K1 (dct mode), one pass per group.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 out=gpurun_out/pmc_k1; mkdir -p $out
-rocprofv3 -L > $out/counters_list.txt 2>&1 || true
 i=0
-for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
-           "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" \
-           "SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"; do
+while read -r grp; do
+  [ -z "$grp" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d $out/p$i -o run -- \
-     python3 bench.py --mode dct --steps 2 --warmup 1 --no-cpu-baseline --verify 0 > $out/p$i.log 2>&1 || { echo "pass $i failed"; tail -20 $out/p$i.log; }
-done
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex mcu --output-format csv -d $out/p$i -o run -- \
+      python3 bench.py --mode ${MODE:-dct} --steps 2 --warmup 1 --no-cpu-baseline --verify 0 > $out/p$i.log 2>&1 || { echo "pass $i failed"; tail -3 $out/p$i.log; exit 1; }
+done <<'G'
+SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY
+SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU
+SQ_IFETCH SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_THREAD_CYCLES_VALU SQ_INSTS_BRANCH
+SQC_ICACHE_MISSES SQC_ICACHE_REQ SQC_ICACHE_HITS SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_LDS_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL SQ_INST_LEVEL_LDS
+G
 python3 - <<'PY'
 import csv, glob, collections
 acc = collections.defaultdict(list)
 for f in glob.glob('gpurun_out/pmc_k1/p*/run_counter_collection.csv'):
     for r in csv.DictReader(open(f)):
-        if 'k_mcu_dct' in r['Kernel_Name']:
+        if 'mcu' in r['Kernel_Name']:
             acc[r['Counter_Name']].append(float(r['Counter_Value']))
-for k, v in sorted(acc.items()):
-    print(f"{k:28s} {sum(v)/len(v):16.1f}  (n={len(v)})")
+for k in sorted(acc):
+    v = acc[k]
+    print(f"{k:28s} {sum(v)/len(v):14.4g}")
 PY
