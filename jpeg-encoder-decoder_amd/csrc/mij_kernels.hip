@@ -332,15 +332,25 @@ __device__ __forceinline__ void convert4(uint32_t w0, uint32_t w1, uint32_t w2,
 
 __device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int c4, int pr,
                                              const uint32_t *__restrict__ lut, bool use_lut) {
+  // all 8 row pieces of this lane up front: the exception branches below
+  // split the code into many blocks the scheduler cannot hoist loads across
+  uint32_t w[4][2][3];
+#pragma unroll
+  for (int it = 0; it < 4; it++)
+#pragma unroll
+    for (int dy = 0; dy < 2; dy++) {
+      const uint32_t *rw = (const uint32_t *)(raw + (4 * it + 2 * pr + dy) * (TILE_W * 3) + 12 * c4);
+#pragma unroll
+      for (int k = 0; k < 3; k++) w[it][dy][k] = rw[k];
+    }
 #pragma unroll
   for (int it = 0; it < 4; it++) {
     const int rp = 2 * it + pr;  // row pair 0..7 == chroma row
     int cbs[2][4], crs[2][4];
 #pragma unroll
     for (int dy = 0; dy < 2; dy++) {
-      const uint32_t *rw = (const uint32_t *)(raw + (2 * rp + dy) * (TILE_W * 3) + 12 * c4);
       int yv[4];
-      convert4(rw[0], rw[1], rw[2], lut, use_lut, yv, cbs[dy], crs[dy]);
+      convert4(w[it][dy][0], w[it][dy][1], w[it][dy][2], lut, use_lut, yv, cbs[dy], crs[dy]);
       const int yrow = 2 * rp + dy;  // 0..15
       const int by = yrow >> 3, bx = c4 >> 1;
       const uint32_t packed = (uint32_t)yv[0] | ((uint32_t)yv[1] << 8) | ((uint32_t)yv[2] << 16) |
@@ -425,11 +435,12 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
         segtok[base] = (uint32_t)cls | (mag_bits(diff, cls) << 16);
         atomicAdd(&hDC[cls], 1u);
       }
-      if (eob) {
-        segtok[base + n - 1] = TOK_AC;
-        atomicAdd(&hAC[0x00], 1u);
-      }
+      if (eob) segtok[base + n - 1] = TOK_AC;
     }
+  }
+  {  // one histogram update for all of the wave's EOBs
+    const unsigned long long eobs = __ballot(g == 0 && valid && eob);
+    if (lane == 0 && eobs) atomicAdd(&hAC[0x00], (unsigned)__popcll(eobs));
   }
   if (valid) {  // lane (g, b) takes the zigzag positions z == g (mod 4)
     unsigned long long mm = M & (0x1111111111111111ull << g);
@@ -469,14 +480,17 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
   __shared__ int s_qint[2][64];
   __shared__ __attribute__((aligned(16))) int16_t s_st[K1_WAVES][64][16];  // replays / tokens
   // per-frame histograms of this workgroup: [frame slot][luma, chroma][symbol]
-  __shared__ uint32_t s_hac[TOK ? 2 : 1][2][256];
-  __shared__ uint32_t s_hdc[TOK ? 2 : 1][2][16];
+  // per-frame histograms of this workgroup: [frame slot][luma, chroma][copy][symbol];
+  // the tokenize pass keeps HREP copies (by block) to spread same-symbol atomics
+  constexpr int HREP = PIX ? 1 : 4;
+  __shared__ uint32_t s_hac[TOK ? 2 : 1][2][HREP][256];
+  __shared__ uint32_t s_hdc[TOK ? 2 : 1][2][HREP][16];
 
   const Tables *__restrict__ T = a.tab;
   if (threadIdx.x < 64) s_cos[threadIdx.x] = T->cosd[threadIdx.x];
   if (TOK) {
-    for (int i = threadIdx.x; i < 2 * 2 * 256; i += 256) (&s_hac[0][0][0])[i] = 0;
-    if (threadIdx.x < 64) (&s_hdc[0][0][0])[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < 2 * 2 * HREP * 256; i += 256) (&s_hac[0][0][0][0])[i] = 0;
+    for (int i = threadIdx.x; i < 2 * 2 * HREP * 16; i += 256) (&s_hdc[0][0][0][0])[i] = 0;
   }
   if (threadIdx.x < 128) s_qint[threadIdx.x >> 6][threadIdx.x & 63] = T->qint[threadIdx.x >> 6][threadIdx.x & 63];
   if (threadIdx.x < 2) s_inv8q[threadIdx.x] = 1.0f / (float)(8 * T->qint[threadIdx.x][0]);
@@ -564,6 +578,31 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
           }
       }
 
+      // coefficient input: all three N-tiles' loads in flight at once
+      u4v pre[PIX ? 1 : 3][2];
+      if (!PIX) {
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++) {
+          bool valid;
+          long long blk;
+          if (nt < 2) {
+            const int bx = p.tx * 16 + bcol;
+            valid = bx < bw;
+            blk = (long long)(2 * p.ty + nt) * bw + bx;
+          } else {
+            const int mx = p.tx * 8 + (bcol & 7);
+            valid = mx < mw;
+            blk = G.nY + (bcol >= 8 ? G.nC : 0) + (long long)p.ty * mw + mx;
+          }
+          pre[PIX ? 0 : nt][0] = pre[PIX ? 0 : nt][1] = u4v{0, 0, 0, 0};
+          if (valid) {
+            const int16_t *src = a.coef + (long long)p.f * G.coef_fs + blk * 64 + 16 * g;
+            pre[PIX ? 0 : nt][0] = *(const u4v *)src;
+            pre[PIX ? 0 : nt][1] = *(const u4v *)(src + 8);
+          }
+        }
+      }
+
       // ---- 3-4. quantize, replay, store, emit -----------------------------------
       auto finish = [&](const int nt, int (&o)[16]) {
         const int comp = nt == 2 ? 1 : 0;
@@ -582,12 +621,7 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
           seg = G.nsy + (bcol >= 8 ? G.nsc : 0) + p.ty * G.tiles_x + p.tx;
         }
         if (!PIX) {  // coefficients from memory (drop-in write_jpg / init_huffman)
-          u4v c0 = {0, 0, 0, 0}, c1 = {0, 0, 0, 0};
-          if (valid) {
-            const int16_t *src = a.coef + (long long)p.f * G.coef_fs + (long long)blk * 64 + 16 * g;
-            c0 = *(const u4v *)src;
-            c1 = *(const u4v *)(src + 8);
-          }
+          const u4v c0 = pre[PIX ? 0 : nt][0], c1 = pre[PIX ? 0 : nt][1];
 #pragma unroll
           for (int k = 0; k < 4; k++) {
             o[2 * k] = (int16_t)(c0[k] & 0xFFFFu);
@@ -612,7 +646,8 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
           const long long fs = (long long)p.f * G.nseg + seg;
           const int slot = p.f - f0;
           emit_tokens(o, lane, g, bcol, valid, comp == 1, !PIX && a.dc_diffed, a.tok + fs * SEG_TOK,
-                      a.seg_ntok + fs, s_hdc[TOK ? slot : 0][comp], s_hac[TOK ? slot : 0][comp],
+                      a.seg_ntok + fs, s_hdc[TOK ? slot : 0][comp][bcol & (HREP - 1)],
+                      s_hac[TOK ? slot : 0][comp][bcol & (HREP - 1)],
                       s_st[wave]);
         }
       };
@@ -680,7 +715,7 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
           finish(nt, o);
         }
       } else if (!PIX) {
-#pragma unroll 1
+#pragma unroll
         for (int nt = 0; nt < 3; nt++) {
           int o[16];
           finish(nt, o);
@@ -694,13 +729,17 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
     __syncthreads();
     for (int i = threadIdx.x; i < 2 * 2 * 256; i += 256) {
       const int slot = i >> 9, tb = (i >> 8) & 1, sym = i & 255;
-      const uint32_t v = s_hac[slot][tb][sym];
+      uint32_t v = 0;
+#pragma unroll
+      for (int c = 0; c < HREP; c++) v += s_hac[slot][tb][c][sym];
       if (v && f0 + slot < a.nframes)
         atomicAdd(&a.hist[((long long)(f0 + slot) * 4 + (tb ? 3 : 1)) * 257 + sym], v);
     }
     if (threadIdx.x < 64) {
       const int slot = threadIdx.x >> 5, tb = (threadIdx.x >> 4) & 1, sym = threadIdx.x & 15;
-      const uint32_t v = s_hdc[slot][tb][sym];
+      uint32_t v = 0;
+#pragma unroll
+      for (int c = 0; c < HREP; c++) v += s_hdc[slot][tb][c][sym];
       if (v && f0 + slot < a.nframes)
         atomicAdd(&a.hist[((long long)(f0 + slot) * 4 + (tb ? 2 : 0)) * 257 + sym], v);
     }
@@ -1014,7 +1053,18 @@ __global__ __launch_bounds__(256) void k_seg_bits(EntArgs a) {
     const uint32_t *tk = a.tok + fs * SEG_TOK;
     const int chroma = s >= a.g.nsy;
     uint32_t b = 0;
-    for (int i = sub; i < n; i += 16) b += tok_bits(tk[i], tab, chroma);
+    // four loads in flight per lane before any is used (latency-bound loop)
+    for (int i0 = 0; i0 < n; i0 += 64) {
+      uint32_t t[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int i = i0 + 16 * u + sub;
+        t[u] = i < n ? tk[i] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+        if (i0 + 16 * u + sub < n) b += tok_bits(t[u], tab, chroma);
+    }
     b = row_scan16(b);
     if (sub == 15) a.seg_bits[fs] = b;
   }
@@ -1138,9 +1188,16 @@ __global__ __launch_bounds__(256) void k_pack(EntArgs a) {
       const int n = min((int)a.seg_ntok[fs], SEG_TOK);
       const uint32_t *tk = a.tok + fs * SEG_TOK;
       uint32_t pos0 = sb;
+      uint32_t tq[4];  // tokens of the next 64, loaded ahead (latency-bound loop)
+#pragma unroll
+      for (int u = 0; u < 4; u++) tq[u] = 16 * u + sub < n ? tk[16 * u + sub] : 0u;
       for (int i0 = 0; i0 < n; i0 += 16) {
         const int i = i0 + sub;
-        const uint32_t t = i < n ? tk[i] : 0u;
+        const uint32_t t = tq[0];
+        tq[0] = tq[1];
+        tq[1] = tq[2];
+        tq[2] = tq[3];
+        tq[3] = i + 64 < n ? tk[i + 64] : 0u;
         const uint32_t sym = t & 255u, cls = sym & 15u;
         const uint32_t e = i < n ? tab[(t & TOK_AC) ? 1 : 0][sym] : 0u;
         const uint32_t nz = (t >> 8) & 3u;

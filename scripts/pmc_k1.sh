@@ -7,7 +7,7 @@ i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex mcu --output-format csv -d $out/p$i -o run -- \
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "${KRE:-mcu}" --output-format csv -d $out/p$i -o run -- \
       python3 bench.py --mode ${MODE:-dct} --steps 2 --warmup 1 --no-cpu-baseline --verify 0 > $out/p$i.log 2>&1 || { echo "pass $i failed"; tail -3 $out/p$i.log; exit 1; }
 done <<'G'
 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY
@@ -17,12 +17,13 @@ SQC_ICACHE_MISSES SQC_ICACHE_REQ SQC_ICACHE_HITS SQ_LDS_ADDR_CONFLICT SQ_LDS_UNA
 G
 python3 - <<'PY'
 import csv, glob, collections
-acc = collections.defaultdict(list)
+acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob('gpurun_out/pmc_k1/p*/run_counter_collection.csv'):
     for r in csv.DictReader(open(f)):
-        if 'mcu' in r['Kernel_Name']:
-            acc[r['Counter_Name']].append(float(r['Counter_Value']))
-for k in sorted(acc):
-    v = acc[k]
-    print(f"{k:28s} {sum(v)/len(v):14.4g}")
+        acc[r['Kernel_Name'][:40]][r['Counter_Name']].append(float(r['Counter_Value']))
+names = sorted({c for d in acc.values() for c in d})
+ks = sorted(acc)
+print(f"{'counter':28s}" + "".join(f"{k[:18]:>20s}" for k in ks))
+for c in names:
+    print(f"{c:28s}" + "".join(f"{(sum(acc[k][c])/len(acc[k][c]) if acc[k][c] else float('nan')):20.4g}" for k in ks))
 PY
