@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bound on the CPU-baseline sample (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1),
+                    help="processes for the frame-parallel CPU baseline (the GPU box's CPU "
+                         "share is 16 cores per GPU); 1 disables it")
     ap.add_argument("--fused", action="store_true",
                     help="fused pipeline: K1 emits symbol tokens directly (default: split, "
                          "K1 writes coefficients and a second pass tokenizes)")
@@ -87,6 +90,31 @@ def make_frames(args, rank):
     return out
 
 
+# rocprofv3 symbol of each K1 variant (for the PMC traffic lookup)
+K1_SYMBOL = {"k_mcu_dct<COEF_OUT>": "k_mcu_dct<1>", "k_mcu_dct<TOK_OUT>": "k_mcu_dct<2>",
+             "k_mcu_dct<COEF_IN|TOK_OUT>": "k_mcu_dct<6>"}
+
+
+def pmc_traffic(kernel, config):
+    """HBM bytes per launch of `kernel` measured by rocprofv3 PMC passes
+    (FETCH_SIZE x2 + WRITE_SIZE, scripts/profile.sh + scripts/traffic.py) on
+    the same workload, from the newest profiles/rNN/traffic.json whose
+    recorded configuration matches; None if there is none."""
+    import glob
+    keys = ("width", "height", "frames_per_gpu", "quality", "mode", "pipeline")
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "traffic.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if any(d.get("config", {}).get(k) != config.get(k) for k in keys):
+            continue
+        for name, v in d.get("kernels", {}).items():
+            if K1_SYMBOL.get(kernel, kernel) in name:
+                return v["hbm_bytes"], os.path.relpath(path, REPO)
+    return None, None
+
+
 def cpu_baseline(frames, seconds):
     """The reference encoder.c itself (oracle/_ref, compiled from the
     reference sources) when present, else the C restatement; 1 thread."""
@@ -118,6 +146,42 @@ def cpu_baseline(frames, seconds):
             "sample": f"{n} frames of {w}x{h} (config-3 recipe), {el:.1f} s, 1 thread, "
                       f"{'reference main/encoder.c via oracle/_ref' if use_ref else 'oracle/cpu_ref.c'}"
                       f", output to memory, on {cpu}"}
+
+
+def _cpu_worker(job):
+    """One process of the frame-parallel CPU baseline: the reference keeps
+    its bit-writer state in globals (encoder.c:383-384), so frames are spread
+    over processes, not threads.  Returns (pixels, seconds)."""
+    seed, h, w, seconds = job
+    import oracle as O
+    use_ref = O.ref_available()
+    frame = recipes.config3_frame(seed) if (w, h) == (3840, 2160) else recipes.config3_frame(seed, h, w)
+    enc = (lambda f: O.ref_stages(f)[4]) if use_ref else (lambda f: O.cref_encode(f))
+    n, t0 = 0, time.perf_counter()
+    while True:
+        enc(frame)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and n >= 1:
+            return n * h * w, el
+
+
+def cpu_baseline_parallel(h, w, seconds, workers):
+    """Frame-parallel reference encoder over `workers` host cores (BASELINE.md
+    CPU-baseline plan (ii)): aggregate pixels / wall time."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        parts = pool.map(_cpu_worker, [(i, h, w, seconds) for i in range(workers)])
+    wall = time.perf_counter() - t0
+    px = sum(p for p, _ in parts)
+    busy = max(e for _, e in parts)
+    import oracle as O
+    return {"value": round(px / busy / 1e6, 3), "unit": "Mpixels/s", "cores": workers,
+            "kind": "reference" if O.ref_available() else "port",
+            "sample": f"{workers} processes x >= {seconds:.0f} s each, one {w}x{h} config-3 frame "
+                      f"per process, aggregate over the slowest process ({wall:.1f} s wall incl. start-up)"}
 
 
 def main():
@@ -219,10 +283,17 @@ def main():
         "verified_frames": verified,
         "fp64_replays_per_frame": round(batch.replays() / (F * (args.warmup + args.steps)), 2),
     }
+    traffic, src = pmc_traffic(dom, res["config"])
+    if traffic is not None:
+        res["roofline"]["traffic"] = traffic
+        res["roofline"]["traffic_source"] = f"{src} (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE, same workload)"
     if os.environ.get("MIJ_K1_FLAGS"):
         res["diagnostic_k1_flags"] = int(os.environ["MIJ_K1_FLAGS"])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(frames[:4], args.cpu_seconds)
+        if args.cpu_workers > 1:
+            res["cpu_baseline_parallel"] = cpu_baseline_parallel(H, W, args.cpu_seconds,
+                                                                 args.cpu_workers)
     if rank == 0:
         print(json.dumps(res), flush=True)
     batch.close()
