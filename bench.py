@@ -57,6 +57,10 @@ def parse():
     ap.add_argument("--fused", action="store_true",
                     help="fused pipeline: K1 emits symbol tokens directly (default: split, "
                          "K1 writes coefficients and a second pass tokenizes)")
+    ap.add_argument("--workload", choices=["config3", "config4"], default="config3",
+                    help="config4: a stream of 7680x4320 frames, each split into MCU-row bands "
+                         "over the ranks with the RCCL exchange steps (strong scaling)")
+    ap.add_argument("--frames4", type=int, default=8, help="config4 frames per step")
     ap.add_argument("--verify", type=int, default=2,
                     help="frames re-checked against the oracle after timing")
     return ap.parse_args()
@@ -69,10 +73,82 @@ def dist_setup(args):
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
+        # nccl (= RCCL) between GPUs; MIJ_DIST_BACKEND=gloo rehearses several
+        # ranks on one GPU (collectives then go through host memory)
+        backend = os.environ.get("MIJ_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend, init_method="env://")
         return world, rank, local, dist, torch
     return 1, 0, 0, None, None
+
+
+def dist_device(dist, local):
+    return f"cuda:{local}" if dist is not None and dist.get_backend() == "nccl" else "cpu"
+
+
+def run_config4(args, world, rank, local, dist):
+    """SURVEY §8(e) config 4: each step encodes --frames4 frames of 7680x4320;
+    every frame is split into world MCU-row bands, one per rank, joined by the
+    exchanges of sharding.encode_banded (last DCs, histograms, bit counts,
+    packed words to rank 0 -- RCCL when the backend is nccl)."""
+    W, H, n = 7680, 4320, args.frames4
+    gpu = 0 if dist is not None and dist.get_backend() != "nccl" else local
+    r0, rows = sharding.band_rows(H, world, rank)
+    band = mijpeg.Batch(W, rows, n, args.quality, device=gpu)
+    distinct = min(n, args.distinct)
+    frames = [recipes.config4_frame(f) for f in range(distinct)]
+    for f in range(n):
+        band.upload(np.ascontiguousarray(frames[f % distinct][r0:r0 + rows]), first=f)
+    full = mijpeg.Batch(W, H, n, args.quality, device=gpu) if rank == 0 else None
+    xch = sharding.TorchExchange(dist, dist_device(dist, local)) if dist is not None \
+        else sharding.LocalExchange()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        sharding.encode_banded(band, n, xch, full)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sharding.encode_banded(band, n, xch, full)
+    if full is not None:
+        full.sync()
+    el = time.perf_counter() - t0
+    barrier()
+    el, _ = sharding.reduce_timing(el, 0, dist, dist_device(dist, local))
+    verified = 0
+    if rank == 0 and args.verify:
+        import oracle as O
+        for f in range(min(args.verify, n)):
+            if full.output(f) != O.cref_encode(frames[f % distinct], args.quality):
+                raise SystemExit(f"bench config4: frame {f} differs from the oracle")
+            verified += 1
+    px = W * H * n * args.steps
+    res = {
+        "metric": "Mpixels/s encoded (device-resident BGR888 -> JFIF bytes)",
+        "value": round(px / el / 1e6, 1), "unit": "Mpixels/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "int8",
+        "data": f"synthetic: SURVEY §8(d) config-4 recipe, {distinct} distinct frames",
+        "config": {"workload": f"config 4: {n} frames of {W}x{H} per step, each split into {world} "
+                               f"MCU-row bands (one per rank) with DC/histogram/bit-offset "
+                               f"exchanges and a packed-word gather to rank 0",
+                   "frames_per_step": n, "width": W, "height": H, "quality": args.quality,
+                   "parallelism": f"band-parallel x{world}",
+                   "backend": dist.get_backend() if dist is not None else "none"},
+        "verified_frames": verified,
+    }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    band.close()
+    if full is not None:
+        full.close()
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 def make_frames(args, rank):
@@ -187,9 +263,12 @@ def cpu_baseline_parallel(h, w, seconds, workers):
 def main():
     args = parse()
     world, rank, local, dist, torch = dist_setup(args)
+    if args.workload == "config4":
+        return run_config4(args, world, rank, local, dist)
     W, H, F = args.width, args.height, args.frames
     frames = make_frames(args, rank)
-    batch = mijpeg.Batch(W, H, F, args.quality, device=local)
+    gpu = 0 if dist is not None and dist.get_backend() != "nccl" else local
+    batch = mijpeg.Batch(W, H, F, args.quality, device=gpu)
     batch.set_split(not args.fused)
     for i in range(F):
         batch.upload(frames[i % len(frames)], first=i)
@@ -213,7 +292,7 @@ def main():
     el = time.perf_counter() - t0
     barrier()
     # max time over ranks, pixels over all ranks (sharding.py; no data-path collective)
-    el, px_all = sharding.reduce_timing(el, W * H * F * args.steps, dist, f"cuda:{local}")
+    el, px_all = sharding.reduce_timing(el, W * H * F * args.steps, dist, dist_device(dist, local))
 
     hist = batch.stage_history(args.steps)
     stage_avg = {k: round(float(np.mean([h[k] for h in hist])), 4) for k in mijpeg.Batch.STAGES}

@@ -153,6 +153,35 @@ unsigned long long mij_batch_replays(mij_batch *b);
 /* the batch's hipStream_t, as an opaque pointer */
 void *mij_batch_stream(mij_batch *b);
 
+/* ---- one large frame over several ranks -------
+ * Rank r encodes band r -- an MCU-row range [row0, row0 + rows) with rows a
+ * multiple of 16 -- of each of n frames as frames 0..n-1 of its own batch
+ * (created for width x rows, input pointing at the band's first row).  The
+ * caller moves four small things between ranks (sharding.py does it with
+ * torch.distributed / RCCL):
+ *   1. mij_band_analyze    -> last raw DC per component      [n*3]  all-gather
+ *   2. mij_band_histograms(previous band's last DCs, 0 for band 0)
+ *                          -> the band's symbol counts       [n*4*257] all-reduce(sum)
+ *   3. mij_band_tables(summed counts) -> bits per scan       [n*3]  all-gather, exclusive scan
+ *   4. mij_band_pack(global bit offset of the band in each scan)
+ *      mij_band_words(frame, comp) -> packed big-endian words; word 0 is
+ *      global word offset/32 of that scan (bits before the offset are 0)  gather
+ * One rank assembles on a batch of the whole frame: mij_assemble_begin
+ * (summed counts -> tables), mij_assemble_words per band and component (OR:
+ * neighbouring bands share at most one word), mij_assemble_end(total bits per
+ * scan) -> 0xFF stuffing, pads, headers; then mij_batch_output. */
+int mij_band_analyze(mij_batch *b, int n, int16_t *last_dc);
+int mij_band_histograms(mij_batch *b, int n, const int16_t *prev_dc, uint32_t *hist);
+int mij_band_tables(mij_batch *b, int n, const uint32_t *hist, unsigned long long *bits);
+int mij_band_pack(mij_batch *b, int n, const unsigned long long *bit_offset,
+                  unsigned long long *nwords);
+int mij_band_words(mij_batch *b, int frame, int comp, void *dst, size_t cap_words,
+                   int dst_on_device);
+int mij_assemble_begin(mij_batch *b, int n, const uint32_t *hist);
+int mij_assemble_words(mij_batch *b, int frame, int comp, unsigned long long first_word,
+                       const void *src, size_t nwords, int src_on_device);
+int mij_assemble_end(mij_batch *b, int n, const unsigned long long *total_bits);
+
 /* ---- diagnostics used by the test-suite -----------------------------------*/
 /* 16x16x64 i8 MFMA layout probe: A, B are 64 lanes x 16 int8, D 64 x 4 int32 */
 int mij_probe_mfma(const int8_t *A, const int8_t *B, int32_t *D);

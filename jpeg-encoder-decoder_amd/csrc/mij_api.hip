@@ -28,6 +28,7 @@ hipError_t launch_bits(const EntArgs &a, hipStream_t s);
 hipError_t launch_scan(const EntArgs &a, hipStream_t s);
 hipError_t launch_pack(const EntArgs &a, hipStream_t s);
 hipError_t launch_emit(const EntArgs &a, hipStream_t s);
+hipError_t launch_or_words(uint32_t *dst, const uint32_t *src, long long n, hipStream_t s);
 hipError_t launch_mfma_probe(const int4 *A, const int4 *B, int4 *D, hipStream_t s);
 }  // namespace mij
 
@@ -211,6 +212,12 @@ struct mij_batch {
   uint8_t *d_out = nullptr;
   int *d_err = nullptr;
   unsigned *d_replays = nullptr;
+  // bands of one large frame (mij_band_*, mij_assemble_*): per frame [4]
+  int16_t *d_dcpred = nullptr;
+  uint32_t *d_bitbase = nullptr;
+  uint32_t *d_stage = nullptr;      // H2D staging for mij_assemble_words
+  size_t stage_words = 0;
+  std::vector<unsigned long long> band_words;  // per frame x 3: packed words after mij_band_pack
   bool keep_coefs = false;  // encode also writes coefficient planes
   bool split = true;        // K1 writes coefficients, a second pass tokenizes
   bool timing = false;
@@ -232,7 +239,8 @@ static void batch_free(mij_batch *b) {
   if (b->stream) hipStreamSynchronize(b->stream);
   void *ptrs[] = {b->d_tab, b->own_in ? b->d_in : nullptr, b->d_coef, b->d_dc, b->d_hist,
                   b->d_ehuf, b->d_raw, b->d_tok, b->d_seg_ntok, b->d_seg_bits, b->d_seg_off,
-                  b->d_scan_bits, b->d_out_len, b->d_hc, b->d_out, b->d_err, b->d_replays};
+                  b->d_scan_bits, b->d_out_len, b->d_hc, b->d_out, b->d_err, b->d_replays,
+                  b->d_dcpred, b->d_bitbase, b->d_stage};
   for (void *p : ptrs)
     if (p) hipFree(p);
   for (auto &row : b->evh)
@@ -291,6 +299,11 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
   HIP_TRY(dalloc(&b->d_err, F));
   HIP_TRY(dalloc(&b->d_replays, 1));
   HIP_TRY(hipMemsetAsync(b->d_replays, 0, sizeof(unsigned), b->stream));
+  HIP_TRY(dalloc(&b->d_dcpred, F * 4));
+  HIP_TRY(dalloc(&b->d_bitbase, F * 4));
+  HIP_TRY(hipMemsetAsync(b->d_dcpred, 0, sizeof(int16_t) * F * 4, b->stream));
+  HIP_TRY(hipMemsetAsync(b->d_bitbase, 0, sizeof(uint32_t) * F * 4, b->stream));
+  b->band_words.assign((size_t)F * 3, 0);
   for (auto &row : b->evh)
     for (auto &e : row) HIP_TRY(hipEventCreate(&e));
   HIP_TRY(hipStreamSynchronize(b->stream));
@@ -363,6 +376,8 @@ static EntArgs ent_args(mij_batch *b, int nframes) {
   a.out = b->d_out;
   a.out_len = b->d_out_len;
   a.err = b->d_err;
+  a.dc_pred = b->d_dcpred;
+  a.bit_base = b->d_bitbase;
   return a;
 }
 
@@ -775,6 +790,167 @@ extern "C" int mij_encode(const uint8_t *bgr, int stride_px, area_t dims, int qu
   if (n > cap) return fail(MIJ_ENOSPC, "mij_encode: need %zu bytes", n);
   if (mij_batch_output(b, 0, out, cap, &n)) return g_err;
   if (out_len) *out_len = n;
+  return MIJ_OK;
+}
+
+// ---------------------------------------------------------------------------
+// one large frame over several ranks
+//
+// Rank r encodes band r (an MCU-row range) of each frame as the frames of its
+// own batch (width x band rows); the caller moves four small things between
+// ranks (RCCL in sharding.py).  DC differencing, the Huffman statistics and
+// the bit positions are the only couplings between bands (encoder.c:168-177,
+// :360-381, :462-502): each band's first DC is predicted from the previous
+// band's last DC, the tables are built from the summed histograms, and each
+// band's share of a scan starts at the sum of the earlier bands' bits.
+// ---------------------------------------------------------------------------
+static int band_check(mij_batch *b, int n, const char *what) {
+  if (!b || n < 1 || n > b->cap) return fail(MIJ_EINVAL, "%s: bad frame count", what);
+  HIP_TRY(hipSetDevice(b->dev));
+  return MIJ_OK;
+}
+
+extern "C" int mij_band_analyze(mij_batch *b, int n, int16_t *last_dc) {
+  if (band_check(b, n, "band_analyze")) return g_err;
+  if (!last_dc) return fail(MIJ_EINVAL, "band_analyze: null last_dc");
+  HIP_TRY(hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * n * 4 * 257, b->stream));
+  HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * n, b->stream));
+  if (run_k1(b, n, 1) || run_k1(b, n, 6, 0)) return g_err;
+  const Geom &g = b->g;
+  const long long last[3] = {g.nY - 1, g.nY + g.nC - 1, g.nY + 2LL * g.nC - 1};
+  for (int f = 0; f < n; f++)
+    for (int c = 0; c < 3; c++)
+      HIP_TRY(hipMemcpyAsync(last_dc + f * 3 + c, b->d_dc + (long long)f * g.nblk + last[c],
+                             sizeof(int16_t), hipMemcpyDeviceToHost, b->stream));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  return MIJ_OK;
+}
+
+extern "C" int mij_band_histograms(mij_batch *b, int n, const int16_t *prev_dc, uint32_t *hist) {
+  if (band_check(b, n, "band_histograms")) return g_err;
+  if (!prev_dc || !hist) return fail(MIJ_EINVAL, "band_histograms: null argument");
+  std::vector<int16_t> pred((size_t)n * 4, 0);
+  for (int f = 0; f < n; f++)
+    for (int c = 0; c < 3; c++) pred[f * 4 + c] = prev_dc[f * 3 + c];
+  HIP_TRY(hipMemcpyAsync(b->d_dcpred, pred.data(), sizeof(int16_t) * n * 4, hipMemcpyHostToDevice,
+                         b->stream));
+  EntArgs a = ent_args(b, n);
+  HIP_TRY(launch_seg_dc(a, b->stream));
+  HIP_TRY(hipMemcpyAsync(hist, b->d_hist, sizeof(uint32_t) * n * 4 * 257, hipMemcpyDeviceToHost,
+                         b->stream));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  return MIJ_OK;
+}
+
+static int upload_hist_tables(mij_batch *b, int n, const uint32_t *hist) {
+  HIP_TRY(hipMemcpyAsync(b->d_hist, hist, sizeof(uint32_t) * n * 4 * 257, hipMemcpyHostToDevice,
+                         b->stream));
+  HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * n, b->stream));
+  EntArgs a = ent_args(b, n);
+  HIP_TRY(launch_tables(a, b->stream));
+  return MIJ_OK;
+}
+
+extern "C" int mij_band_tables(mij_batch *b, int n, const uint32_t *hist, unsigned long long *bits) {
+  if (band_check(b, n, "band_tables")) return g_err;
+  if (!hist || !bits) return fail(MIJ_EINVAL, "band_tables: null argument");
+  if (upload_hist_tables(b, n, hist)) return g_err;
+  HIP_TRY(hipMemsetAsync(b->d_bitbase, 0, sizeof(uint32_t) * n * 4, b->stream));
+  EntArgs a = ent_args(b, n);
+  HIP_TRY(launch_bits(a, b->stream));
+  HIP_TRY(launch_scan(a, b->stream));
+  HIP_TRY(hipMemcpyAsync(bits, b->d_scan_bits, sizeof(uint64_t) * n * 3, hipMemcpyDeviceToHost,
+                         b->stream));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  int err = 0;
+  for (int f = 0; f < n; f++) {
+    HIP_TRY(hipMemcpy(&err, b->d_err + f, sizeof(int), hipMemcpyDeviceToHost));
+    if (err) return fail(MIJ_ETABLE, "band frame %d: Huffman table construction failed", f);
+  }
+  return MIJ_OK;
+}
+
+extern "C" int mij_band_pack(mij_batch *b, int n, const unsigned long long *bit_offset,
+                             unsigned long long *nwords) {
+  if (band_check(b, n, "band_pack")) return g_err;
+  if (!bit_offset) return fail(MIJ_EINVAL, "band_pack: null bit_offset");
+  std::vector<uint32_t> base((size_t)n * 4, 0);
+  for (int f = 0; f < n; f++)
+    for (int c = 0; c < 3; c++) base[f * 4 + c] = (uint32_t)(bit_offset[f * 3 + c] & 31);
+  HIP_TRY(hipMemcpyAsync(b->d_bitbase, base.data(), sizeof(uint32_t) * n * 4, hipMemcpyHostToDevice,
+                         b->stream));
+  EntArgs a = ent_args(b, n);
+  HIP_TRY(launch_scan(a, b->stream));
+  HIP_TRY(launch_pack(a, b->stream));
+  std::vector<unsigned long long> tot((size_t)n * 3);
+  HIP_TRY(hipMemcpyAsync(tot.data(), b->d_scan_bits, sizeof(uint64_t) * n * 3,
+                         hipMemcpyDeviceToHost, b->stream));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  for (int i = 0; i < n * 3; i++) {
+    b->band_words[i] = (tot[i] + 31) >> 5;  // scan bits include the in-word start offset
+    if (nwords) nwords[i] = b->band_words[i];
+  }
+  return MIJ_OK;
+}
+
+static uint32_t *scan_words(mij_batch *b, int frame, int comp) {
+  const Geom &g = b->g;
+  return b->d_raw + (long long)frame * g.raw_fs +
+         (comp == 0 ? 0 : g.raw_words[0] + (comp == 2 ? g.raw_words[1] : 0));
+}
+
+extern "C" int mij_band_words(mij_batch *b, int frame, int comp, void *dst, size_t cap_words,
+                              int dst_on_device) {
+  if (!b || frame < 0 || frame >= b->cap || comp < 0 || comp > 2 || !dst)
+    return fail(MIJ_EINVAL, "band_words: bad arguments");
+  HIP_TRY(hipSetDevice(b->dev));
+  const unsigned long long nw = b->band_words[frame * 3 + comp];
+  if (cap_words < nw) return fail(MIJ_ENOSPC, "band_words: need %llu words", nw);
+  HIP_TRY(hipMemcpyAsync(dst, scan_words(b, frame, comp), nw * 4,
+                         dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, b->stream));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  return MIJ_OK;
+}
+
+extern "C" int mij_assemble_begin(mij_batch *b, int n, const uint32_t *hist) {
+  if (band_check(b, n, "assemble_begin")) return g_err;
+  if (!hist) return fail(MIJ_EINVAL, "assemble_begin: null hist");
+  HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * n * b->g.raw_fs, b->stream));
+  return upload_hist_tables(b, n, hist);
+}
+
+extern "C" int mij_assemble_words(mij_batch *b, int frame, int comp, unsigned long long first_word,
+                                  const void *src, size_t nwords, int src_on_device) {
+  if (!b || frame < 0 || frame >= b->cap || comp < 0 || comp > 2 || (!src && nwords))
+    return fail(MIJ_EINVAL, "assemble_words: bad arguments");
+  if (first_word + nwords > (unsigned long long)b->g.raw_words[comp])
+    return fail(MIJ_ENOSPC, "assemble_words: words beyond the scan buffer");
+  HIP_TRY(hipSetDevice(b->dev));
+  const uint32_t *s32 = (const uint32_t *)src;
+  if (!src_on_device && nwords) {
+    if (b->stage_words < nwords) {
+      if (b->d_stage) HIP_TRY(hipFree(b->d_stage));
+      b->d_stage = nullptr;
+      HIP_TRY(dalloc(&b->d_stage, nwords));
+      b->stage_words = nwords;
+    }
+    HIP_TRY(hipMemcpyAsync(b->d_stage, src, nwords * 4, hipMemcpyHostToDevice, b->stream));
+    s32 = b->d_stage;
+  }
+  // neighbouring bands share at most their boundary word: OR-combine
+  HIP_TRY(launch_or_words(scan_words(b, frame, comp) + first_word, s32, (long long)nwords, b->stream));
+  if (!src_on_device) HIP_TRY(hipStreamSynchronize(b->stream));
+  return MIJ_OK;
+}
+
+extern "C" int mij_assemble_end(mij_batch *b, int n, const unsigned long long *total_bits) {
+  if (band_check(b, n, "assemble_end")) return g_err;
+  if (!total_bits) return fail(MIJ_EINVAL, "assemble_end: null total_bits");
+  HIP_TRY(hipMemcpyAsync(b->d_scan_bits, total_bits, sizeof(uint64_t) * n * 3,
+                         hipMemcpyHostToDevice, b->stream));
+  EntArgs a = ent_args(b, n);
+  HIP_TRY(launch_emit(a, b->stream));
+  b->last_frames = n;
   return MIJ_OK;
 }
 

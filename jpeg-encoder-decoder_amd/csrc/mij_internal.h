@@ -107,6 +107,9 @@ struct EntArgs {
   uint8_t *out;             // per frame out_cap bytes
   uint64_t *out_len;        // per frame
   int *err;                 // per frame error flag
+  // one large frame split into bands (mij_band_*): per frame [4]
+  const int16_t *dc_pred;   // DC predictor of each component's first block (null: 0)
+  const uint32_t *bit_base; // bit offset of each scan inside its first word (null: 0)
 };
 
 }  // namespace mij

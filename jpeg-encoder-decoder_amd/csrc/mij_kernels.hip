@@ -801,7 +801,11 @@ __global__ __launch_bounds__(256) void k_seg_dc(EntArgs a) {
     int comp, first, cstart, local;
     seg_info(a.g, s, comp, first, cstart, local);
     const long long fb = (long long)f * a.g.nblk;
-    const int diff = (int)a.dc[fb + first] - (first == cstart ? 0 : (int)a.dc[fb + first - 1]);
+    // a component's first block is predicted from 0 (encoder.c:168-177), or
+    // from the previous band's last DC when the frame is split into bands
+    const int pred = first == cstart ? (a.dc_pred ? (int)a.dc_pred[f * 4 + comp] : 0)
+                                     : (int)a.dc[fb + first - 1];
+    const int diff = (int)a.dc[fb + first] - pred;
     const int cls = mag_class(diff);
     a.tok[((long long)f * a.g.nseg + s) * SEG_TOK] = (uint32_t)cls | (mag_bits(diff, cls) << 16);
     atomicAdd(&h[comp ? 1 : 0][cls], 1u);
@@ -1084,7 +1088,7 @@ __global__ void k_scan(EntArgs a) {
   const long long f0 = (long long)f * a.g.nseg + sbase;
   uint32_t *raw = a.raw + (long long)f * a.g.raw_fs +
                   (comp == 0 ? 0 : a.g.raw_words[0] + (comp == 2 ? a.g.raw_words[1] : 0));
-  unsigned long long carry = 0;
+  unsigned long long carry = a.bit_base ? a.bit_base[f * 4 + comp] : 0u;  // band: start bit in word 0
   for (int base = 0; base < ns; base += 64) {
     const int i = base + lane;
     const unsigned long long v = i < ns ? a.seg_bits[f0 + i] : 0ull;
@@ -1346,6 +1350,12 @@ __global__ __launch_bounds__(256) void k_emit(EntArgs a) {
   }
 }
 
+// ---- band assembly: OR a band's packed words into the frame's scan buffer ----
+__global__ void k_or_words(uint32_t *dst, const uint32_t *src, long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] |= src[i];
+}
+
 // ---- tiny self-test used by the test-suite: exact i8 MFMA layout check ----
 __global__ void k_mfma_probe(const int4 *A, const int4 *B, int4 *D) {
   const int lane = threadIdx.x;
@@ -1436,6 +1446,12 @@ hipError_t launch_scan(const EntArgs &a, hipStream_t s) {
   hipLaunchKernelGGL(k_scan, dim3(a.nframes * 3), dim3(64), 0, s, a);
   return hipGetLastError();
 }
+hipError_t launch_or_words(uint32_t *dst, const uint32_t *src, long long n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_or_words, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dst, src, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_pack(const EntArgs &a, hipStream_t s) {
   const int gy = (a.g.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (a.g.nsc + PACK_SEGS - 1) / PACK_SEGS;
   hipLaunchKernelGGL(k_pack, dim3(a.nframes * (gy + 2 * gc)), dim3(256), 0, s, a);

@@ -25,6 +25,8 @@ EXPORTS = [
     "mij_batch_encode", "mij_batch_keep_coefs", "mij_batch_set_split", "mij_batch_dct", "mij_batch_sync", "mij_batch_output",
     "mij_batch_lengths", "mij_batch_coefs", "mij_batch_tables", "mij_batch_set_timing",
     "mij_batch_stage_ms", "mij_batch_stage_history", "mij_batch_token_count", "mij_batch_geometry", "mij_batch_replays", "mij_batch_stream",
+    "mij_band_analyze", "mij_band_histograms", "mij_band_tables", "mij_band_pack", "mij_band_words",
+    "mij_assemble_begin", "mij_assemble_words", "mij_assemble_end",
     "mij_probe_mfma", "mij_colour_lut", "mij_build_target",
 ]
 
@@ -102,6 +104,15 @@ def load() -> C.CDLL:
     lib.mij_batch_replays.argtypes = [p]
     lib.mij_batch_stream.restype = p
     lib.mij_batch_stream.argtypes = [p]
+    u64 = C.c_ulonglong
+    lib.mij_band_analyze.argtypes = [p, i, p]
+    lib.mij_band_histograms.argtypes = [p, i, p, p]
+    lib.mij_band_tables.argtypes = [p, i, p, p]
+    lib.mij_band_pack.argtypes = [p, i, p, p]
+    lib.mij_band_words.argtypes = [p, i, i, p, C.c_size_t, i]
+    lib.mij_assemble_begin.argtypes = [p, i, p]
+    lib.mij_assemble_words.argtypes = [p, i, i, u64, p, C.c_size_t, i]
+    lib.mij_assemble_end.argtypes = [p, i, p]
     lib.mij_probe_mfma.argtypes = [p, p, p]
     lib.mij_colour_lut.argtypes = [p]
     lib.mij_build_target.restype = C.c_char_p
@@ -281,6 +292,58 @@ class Batch:
 
     def replays(self) -> int:
         return int(self.lib.mij_batch_replays(self.h_))
+
+    # ---- one large frame over several ranks (include/mijpeg.h, sharding.py) ----
+    def band_analyze(self, n: int) -> np.ndarray:
+        last = np.zeros((n, 3), np.int16)
+        _check(self.lib.mij_band_analyze(self.h_, n, _ptr(last)), "band_analyze")
+        return last
+
+    def band_histograms(self, n: int, prev_dc: np.ndarray) -> np.ndarray:
+        prev = np.ascontiguousarray(prev_dc, np.int16).reshape(n, 3)
+        hist = np.zeros((n, 4, 257), np.uint32)
+        _check(self.lib.mij_band_histograms(self.h_, n, _ptr(prev), _ptr(hist)), "band_histograms")
+        return hist
+
+    def band_tables(self, n: int, hist: np.ndarray) -> np.ndarray:
+        h = np.ascontiguousarray(hist, np.uint32).reshape(n, 4, 257)
+        bits = np.zeros((n, 3), np.uint64)
+        _check(self.lib.mij_band_tables(self.h_, n, _ptr(h), _ptr(bits)), "band_tables")
+        return bits
+
+    def band_pack(self, n: int, bit_offset: np.ndarray) -> np.ndarray:
+        off = np.ascontiguousarray(bit_offset, np.uint64).reshape(n, 3)
+        nw = np.zeros((n, 3), np.uint64)
+        _check(self.lib.mij_band_pack(self.h_, n, _ptr(off), _ptr(nw)), "band_pack")
+        return nw
+
+    def band_words(self, frame: int, comp: int, nwords: int, dst_dev_ptr: int = 0):
+        """Packed words of one band scan: into host memory (returned array), or
+        into device memory at dst_dev_ptr (returns None)."""
+        if dst_dev_ptr:
+            _check(self.lib.mij_band_words(self.h_, frame, comp, dst_dev_ptr, nwords, 1), "band_words")
+            return None
+        out = np.zeros(max(nwords, 1), np.uint32)
+        _check(self.lib.mij_band_words(self.h_, frame, comp, _ptr(out), nwords, 0), "band_words")
+        return out[:nwords]
+
+    def assemble_begin(self, n: int, hist: np.ndarray) -> None:
+        h = np.ascontiguousarray(hist, np.uint32).reshape(n, 4, 257)
+        _check(self.lib.mij_assemble_begin(self.h_, n, _ptr(h)), "assemble_begin")
+
+    def assemble_words(self, frame: int, comp: int, first_word: int, words=None,
+                       src_dev_ptr: int = 0, nwords: int = 0) -> None:
+        if src_dev_ptr:
+            _check(self.lib.mij_assemble_words(self.h_, frame, comp, first_word, src_dev_ptr,
+                                               nwords, 1), "assemble_words")
+        else:
+            w = np.ascontiguousarray(words, np.uint32)
+            _check(self.lib.mij_assemble_words(self.h_, frame, comp, first_word, _ptr(w), w.size, 0),
+                   "assemble_words")
+
+    def assemble_end(self, n: int, total_bits: np.ndarray) -> None:
+        t = np.ascontiguousarray(total_bits, np.uint64).reshape(n, 3)
+        _check(self.lib.mij_assemble_end(self.h_, n, _ptr(t)), "assemble_end")
 
 
 def probe_mfma(A: np.ndarray, B: np.ndarray) -> np.ndarray:

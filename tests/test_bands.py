@@ -1,0 +1,124 @@
+"""One large frame split into MCU-row bands:
+each band is encoded by the library as its own frame, the bands exchange
+their last DCs, histograms, bit counts and packed words, and one side
+assembles the JFIF.  The result must be the reference's bytes for the whole
+frame.  GPU tests drive the bands in one process (the exchanges done in
+Python) and over two processes with torch.distributed (gloo, both ranks on
+GPU 0)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import sharding
+
+pytestmark = pytest.mark.gpu
+
+
+def encode_banded_local(frames: np.ndarray, world: int, quality: int = 50):
+    """All bands of n frames in one process; mirrors sharding.encode_banded."""
+    import mijpeg
+    n, H, W = frames.shape[:3]
+    bands = []
+    for r in range(world):
+        r0, rows = sharding.band_rows(H, world, r)
+        b = mijpeg.Batch(W, rows, n, quality)
+        b.upload(np.ascontiguousarray(frames[:, r0:r0 + rows]))
+        bands.append(b)
+    lasts = [b.band_analyze(n) for b in bands]
+    hists = [b.band_histograms(n, np.zeros((n, 3), np.int16) if r == 0 else lasts[r - 1])
+             for r, b in enumerate(bands)]
+    ghist = np.sum(np.stack(hists).astype(np.int64), axis=0).astype(np.uint32)
+    bits = np.stack([b.band_tables(n, ghist) for b in bands]).astype(np.uint64)
+    offs = np.concatenate([np.zeros((1, n, 3), np.uint64), np.cumsum(bits, axis=0)[:-1]])
+    full = mijpeg.Batch(W, H, n, quality)
+    full.assemble_begin(n, ghist)
+    for r, b in enumerate(bands):
+        nw = b.band_pack(n, offs[r])
+        for f in range(n):
+            for c in range(3):
+                words = b.band_words(f, c, int(nw[f, c]))
+                full.assemble_words(f, c, int(offs[r][f, c]) >> 5, words)
+    full.assemble_end(n, bits.sum(axis=0))
+    out = [full.output(f) for f in range(n)]
+    for b in bands:
+        b.close()
+    full.close()
+    return out
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5])
+def test_bands_match_reference(world):
+    import oracle as O
+    import recipes
+    frames = np.stack([recipes.config3_frame(0, 320, 480), recipes.noise(320, 480, 7)])
+    got = encode_banded_local(frames, world)
+    for f in range(2):
+        assert got[f] == O.cref_encode(frames[f]), f"world {world} frame {f}"
+
+
+def test_bands_one_mcu_row_each_and_quality():
+    import oracle as O
+    import recipes
+    frame = recipes.config3_frame(3, 64, 640)[None]  # 4 MCU rows -> 4 one-row bands
+    assert encode_banded_local(frame, 4, 75)[0] == O.cref_encode(frame[0], 75)
+
+
+def test_bands_config4_shape_two_bands():
+    """A 7680x4320 frame (config-4 shape) in two bands == the one-frame encode."""
+    import mijpeg
+    import recipes
+    frame = recipes.config4_frame(0)[None]
+    got = encode_banded_local(frame, 2)[0]
+    b = mijpeg.Batch(7680, 4320, 1)
+    b.upload(frame)
+    b.encode(1)
+    assert got == b.output(0)
+    b.close()
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    import mijpeg
+    import recipes
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        frames = np.stack([recipes.config3_frame(1, 320, 480), recipes.noise(320, 480, 9)])
+        H, W = frames.shape[1:3]
+        r0, rows = sharding.band_rows(H, world, rank)
+        band = mijpeg.Batch(W, rows, 2)
+        band.upload(np.ascontiguousarray(frames[:, r0:r0 + rows]))
+        full = mijpeg.Batch(W, H, 2) if rank == 0 else None
+        sharding.encode_banded(band, 2, sharding.TorchExchange(dist, "cpu"), full)
+        if rank == 0:
+            q.put([full.output(f) for f in range(2)])
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_process_banded_encode_gloo():
+    import multiprocessing as mp
+    import oracle as O
+    import recipes
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    frames = [recipes.config3_frame(1, 320, 480), recipes.noise(320, 480, 9)]
+    assert outs == [O.cref_encode(f) for f in frames]
