@@ -150,12 +150,9 @@ static void fill_tables(int quality, Tables *t) {
       t->dqt[c][z] = qz;
       // z = 0 (DC) is computed exactly from the pixel sum: no fast path
       const double fac = 1.0 / (2097152.0 * qz);
+      // the error bound tau = fac * (0.72 L1 + 80) + 1e-6 is formed per block
+      // in K1 from the block's L1 = sum |pixel - 128|
       t->qfac[c][z] = z ? (float)fac : 0.0f;
-      // |N - 2^19*sum(K'X)| <= 0.5*sum|X| <= 4096 (+64 for float(N)), 25%
-      // margin, +1e-6 for the FP64 reference; fp32 roundings of t = N*fac and
-      // of t -+ tau stay below 1.8e-7*|t|, covered by 3e-7*|t|
-      t->qtau[c][z] = z ? (float)(1.25 * 4160.0 * fac + 1.0e-6) : 0.0f;
-      t->qrel[c][z] = z ? (float)(3.0e-7 * fac) : 0.0f;
     }
   // A fragments of v_mfma_i32_16x16x64_i8: lane l holds row (l & 15) and the
   // 16 k-values 16*(l>>4) .. +15.  Row r of M-tile m is zigzag coefficient

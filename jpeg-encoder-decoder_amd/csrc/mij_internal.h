@@ -60,8 +60,6 @@ struct Geom {
 struct Tables {
   int4 mfma_a[12 * 64];   // A fragments: 4 M-tiles x 3 digits x 64 lanes
   float qfac[2][64];      // zigzag order: 1 / (2^21 * q)
-  float qtau[2][64];      // zigzag order: proven error bound, constant part (t units)
-  float qrel[2][64];      // zigzag order: error bound per unit |N| (fp32 rounding)
   int qint[2][64];        // zigzag order: integer quantizer
   int dqt[2][64];         // zigzag order: DQT bytes
   double cosd[64];        // encoder.c:8-16 constants

@@ -487,6 +487,13 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
   __shared__ uint32_t s_hdc[TOK ? 2 : 1][2][HREP][16];
 
   const Tables *__restrict__ T = a.tab;
+  // diagnostic switches exist only in the MIJ_K1_DIAG build (make diag): in
+  // the product kernel they fold away at compile time
+#ifdef MIJ_K1_DIAG
+  const int kflags = a.flags;
+#else
+  constexpr int kflags = 0;
+#endif
   if (threadIdx.x < 64) s_cos[threadIdx.x] = T->cosd[threadIdx.x];
   if (TOK) {
     for (int i = threadIdx.x; i < 2 * 2 * HREP * 256; i += 256) (&s_hac[0][0][0][0])[i] = 0;
@@ -526,8 +533,8 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
         // ---- 1. colour convert + subsample + stage.  This tile's DMA was
         // waited for before the previous tile's stores (dma_wait), except for
         // the first tile and when the DCT phase is skipped (diagnostics).
-        if (t == t0 + wave || (a.flags & K1F_NO_DCT)) dma_wait();
-        if (!(a.flags & K1F_NO_COLOUR)) colour_stage(raw, L, c4, pr, s_lut, !(a.flags & K1F_NO_LUT));
+        if (t == t0 + wave || (kflags & K1F_NO_DCT)) dma_wait();
+        if (!(kflags & K1F_NO_COLOUR)) colour_stage(raw, L, c4, pr, s_lut, !(kflags & K1F_NO_LUT));
         wave_lds_sync();
         // ---- stream the wave's next tile into the freed raw buffer -----------
         if (t + K1_WAVES < tend) {
@@ -544,9 +551,9 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
       // fragments are read once per tile and the 12 chains (3 N-tiles x 4
       // M-tiles) are issued digit by digit so no MFMA waits on its
       // predecessor's result.
-      const bool do_dct = !(a.flags & K1F_NO_DCT);
+      const bool do_dct = !(kflags & K1F_NO_DCT);
       v4i acc[3][4];
-      float lc[3];  // per block: error bound of N in N units (before the fp32 term)
+      float lc[3];  // per block: error bound of N in N units
       if (PIX && do_dct) {
         v4i Bf[3];
 #pragma unroll
@@ -560,7 +567,9 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
           const auto r16 = __builtin_amdgcn_permlane16_swap(l1, l1, false, false);
           l1 = r16[0] + r16[1];
           const auto r32 = __builtin_amdgcn_permlane32_swap(l1, l1, false, false);
-          lc[nt] = fmaf((float)(r32[0] + r32[1]), 0.625f, 80.0f);  // 1.25 * (L1/2 + 64)
+          // 1.25 * (L1/2 + 64) for the integer DCT and float(N), + 0.095 L1 for
+          // the fp32 roundings of t -+ tau (<= 1.8e-7 |N| with |N| <= 2^19 L1)
+          lc[nt] = fmaf((float)(r32[0] + r32[1]), 0.72f, 80.0f);
           Bf[nt] ^= (int)0x80808080;  // pixel - 128 as int8
         }
 #pragma unroll
@@ -572,7 +581,7 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
 #pragma unroll
             for (int nt = 0; nt < 3; nt++) {
               const v4i c = d == 0 ? v4i{0, 0, 0, 0} : acc[nt][m] << 7;
-              acc[nt][m] = (a.flags & K1F_NO_MFMA) ? c + Fv + Bf[nt]
+              acc[nt][m] = (kflags & K1F_NO_MFMA) ? c + Fv + Bf[nt]
                                                    : __builtin_amdgcn_mfma_i32_16x16x64_i8(Fv, Bf[nt], c, 0, 0, 0);
             }
           }
@@ -630,7 +639,7 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
             o[9 + 2 * k] = (int16_t)(c1[k] >> 16);
           }
         }
-        if ((MODE & K1M_COEF_OUT) && valid && !(a.flags & K1F_NO_STORE)) {
+        if ((MODE & K1M_COEF_OUT) && valid && !(kflags & K1F_NO_STORE)) {
           int16_t *dst = a.coef + (long long)p.f * G.coef_fs + (long long)blk * 64 + 16 * g;
           u4v s0, s1;
 #pragma unroll
@@ -657,7 +666,7 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
           const int comp = nt == 2 ? 1 : 0;
           int o[16];
           uint32_t hz = 0;  // nonzero iff some coefficient's +-tau interval straddles a boundary
-          if (a.flags & K1F_NO_QUANT) {
+          if (kflags & K1F_NO_QUANT) {
 #pragma unroll
             for (int k = 0; k < 16; k++) o[k] = acc[nt][k >> 2][k & 3];
           } else
@@ -668,8 +677,8 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
 #pragma unroll
             for (int r = 0; r < 4; r++) {
               const float nf = (float)acc[nt][m][r];
-              // tau = fac * (lc + 3e-7 |N|) + 1e-6
-              const float tv = fmaf(fmaf(fabsf(nf), 3.0e-7f, lc[nt]), fa[r], 1.0e-6f);
+              // tau = fac * lc + 1e-6
+              const float tv = fmaf(fa[r], lc[nt], 1.0e-6f);
               const int lo = (int)fmaf(nf, fa[r], -tv);
               const int hi = (int)fmaf(nf, fa[r], tv);
               o[4 * m + r] = lo;
@@ -683,7 +692,7 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
             if (__ballot(tie && g == 0))
               if (g == 0 && tie) o[0] = dc_exact(acc[nt][0][0], q_dc[comp]);
           }
-          if (__ballot(hz != 0) && !(a.flags & K1F_NO_REPLAY)) {
+          if (__ballot(hz != 0) && !(kflags & K1F_NO_REPLAY)) {
             // rare path: find the straddling coefficients (same arithmetic) and
             // recompute them in FP64 exactly as encoder.c:87-109
             const uint8_t *Pb = L + (nt * 16 + bcol) * LDS_BLK;
@@ -695,7 +704,7 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
                 const int k = 4 * m + r;
                 const float nf = (float)acc[nt][m][r];
                 const float fa = s_fac[comp][16 * g + k];
-                const float tv = fmaf(fmaf(fabsf(nf), 3.0e-7f, lc[nt]), fa, 1.0e-6f);
+                const float tv = fmaf(fa, lc[nt], 1.0e-6f);
                 mm |= (uint32_t)((int)fmaf(nf, fa, -tv) != (int)fmaf(nf, fa, tv)) << k;
               }
             const uint32_t hm = mm;
