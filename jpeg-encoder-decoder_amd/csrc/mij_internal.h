@@ -15,7 +15,6 @@ constexpr int TILE_W = 128;
 constexpr int TILE_H = 16;
 constexpr int LDS_BLK = 80;          // bytes per staged 8x8 block (64 + pad)
 constexpr int LDS_WAVE = 48 * LDS_BLK;  // 32 Y + 16 chroma blocks per wave
-constexpr int K1_WAVES = 4;
 constexpr int LUT_WORDS = 1024;      // 2^15 bits per colour-exception table
 
 // ---- entropy stage: segments ---------------------------------------------

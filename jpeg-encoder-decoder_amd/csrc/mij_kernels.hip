@@ -466,20 +466,28 @@ constexpr int K1M_COEF_OUT = 1;  // write zigzag coefficient planes
 constexpr int K1M_TOK_OUT = 2;   // write per-segment token streams + histograms
 constexpr int K1M_COEF_IN = 4;   // read coefficient planes (DC differences) instead of pixels
 
+// Waves per workgroup: the coefficient-only variant runs one 12-wave
+// workgroup per CU (3 waves per SIMD: 120 KB of per-wave tile buffers + the
+// shared tables fit the 160 KB LDS, <= 168 VGPRs); the token variants carry
+// per-wave token staging and run 4-wave workgroups, two per CU.
 template <int MODE>
-__global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
+constexpr int k1_waves() { return MODE == K1M_COEF_OUT ? 12 : 4; }
+
+template <int MODE>
+__global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2) void k_mcu_dct(K1Args a) {
   constexpr bool PIX = !(MODE & K1M_COEF_IN);
   constexpr bool TOK = MODE & K1M_TOK_OUT;
-  __shared__ __attribute__((aligned(16))) uint8_t s_raw[PIX ? K1_WAVES : 1][TILE_RAW];
-  __shared__ __attribute__((aligned(16))) uint8_t s_tile[PIX ? K1_WAVES : 1][LDS_WAVE];
+  constexpr int NW = k1_waves<MODE>();
+  constexpr int NT = 64 * NW;  // threads per workgroup
+  __shared__ __attribute__((aligned(16))) uint8_t s_raw[PIX ? NW : 1][TILE_RAW];
+  __shared__ __attribute__((aligned(16))) uint8_t s_tile[PIX ? NW : 1][LDS_WAVE];
   __shared__ __attribute__((aligned(16))) int4 s_A[PIX ? 12 * 64 : 1];
   __shared__ __attribute__((aligned(16))) float s_fac[2][64];
   __shared__ float s_inv8q[2];
   __shared__ uint32_t s_lut[PIX ? 3 * LUT_WORDS : 1];
   __shared__ double s_cos[64];
   __shared__ int s_qint[2][64];
-  __shared__ __attribute__((aligned(16))) int16_t s_st[K1_WAVES][64][16];  // replays / tokens
-  // per-frame histograms of this workgroup: [frame slot][luma, chroma][symbol]
+  __shared__ __attribute__((aligned(16))) int16_t s_st[TOK ? NW : 1][64][16];  // token staging
   // per-frame histograms of this workgroup: [frame slot][luma, chroma][copy][symbol];
   // the tokenize pass keeps HREP copies (by block) to spread same-symbol atomics
   constexpr int HREP = PIX ? 1 : 4;
@@ -496,16 +504,16 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
 #endif
   if (threadIdx.x < 64) s_cos[threadIdx.x] = T->cosd[threadIdx.x];
   if (TOK) {
-    for (int i = threadIdx.x; i < 2 * 2 * HREP * 256; i += 256) (&s_hac[0][0][0][0])[i] = 0;
-    for (int i = threadIdx.x; i < 2 * 2 * HREP * 16; i += 256) (&s_hdc[0][0][0][0])[i] = 0;
+    for (int i = threadIdx.x; i < 2 * 2 * HREP * 256; i += NT) (&s_hac[0][0][0][0])[i] = 0;
+    for (int i = threadIdx.x; i < 2 * 2 * HREP * 16; i += NT) (&s_hdc[0][0][0][0])[i] = 0;
   }
   if (threadIdx.x < 128) s_qint[threadIdx.x >> 6][threadIdx.x & 63] = T->qint[threadIdx.x >> 6][threadIdx.x & 63];
   if (threadIdx.x < 2) s_inv8q[threadIdx.x] = 1.0f / (float)(8 * T->qint[threadIdx.x][0]);
   if (PIX) {
-    for (int i = threadIdx.x; i < 12 * 64; i += 256) s_A[i] = T->mfma_a[i];
-    for (int i = threadIdx.x; i < 3 * LUT_WORDS; i += 256) s_lut[i] = (&T->lut[0][0])[i];
+    for (int i = threadIdx.x; i < 12 * 64; i += NT) s_A[i] = T->mfma_a[i];
+    for (int i = threadIdx.x; i < 3 * LUT_WORDS; i += NT) s_lut[i] = (&T->lut[0][0])[i];
   }
-  for (int i = threadIdx.x; i < 128; i += 256) {
+  for (int i = threadIdx.x; i < 128; i += NT) {
     s_fac[i >> 6][i & 63] = T->qfac[i >> 6][i & 63];
   }
   __syncthreads();
@@ -527,7 +535,7 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
     uint8_t *raw = s_raw[PIX ? wave : 0];
     TilePos p = tile_pos(G, t);
     if (PIX) issue_tile_dma(a, p, lane, raw);
-    for (; t < tend; t += K1_WAVES) {
+    for (; t < tend; t += NW) {
       TilePos pn = p;
       if (PIX) {
         // ---- 1. colour convert + subsample + stage.  This tile's DMA was
@@ -537,55 +545,46 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
         if (!(kflags & K1F_NO_COLOUR)) colour_stage(raw, L, c4, pr, s_lut, !(kflags & K1F_NO_LUT));
         wave_lds_sync();
         // ---- stream the wave's next tile into the freed raw buffer -----------
-        if (t + K1_WAVES < tend) {
-          pn = tile_pos(G, t + K1_WAVES);
+        if (t + NW < tend) {
+          pn = tile_pos(G, t + NW);
           issue_tile_dma(a, pn, lane, raw);
         }
-      } else if (t + K1_WAVES < tend) {
-        pn = tile_pos(G, t + K1_WAVES);
+      } else if (t + NW < tend) {
+        pn = tile_pos(G, t + NW);
       }
 
-      // ---- 2. DCT on MFMA for the tile's three N-tiles ------------------------
+      // ---- 2. DCT on MFMA, one 16-block N-tile at a time ----------------------
       // N = ((D2.X << 7) + D1.X << 7) + D0.X, accumulated in place: each
-      // digit's MFMA takes the shifted partial sum as its C input.  The A
-      // fragments are read once per tile and the 12 chains (3 N-tiles x 4
-      // M-tiles) are issued digit by digit so no MFMA waits on its
-      // predecessor's result.
+      // digit's MFMA takes the shifted partial sum as its C input.  The four
+      // M-tile chains of an N-tile are issued digit by digit, so no MFMA waits
+      // on its predecessor's result; the N-tile's quantisation and stores
+      // follow before the next N-tile's MFMAs (16 accumulator VGPRs live).
       const bool do_dct = !(kflags & K1F_NO_DCT);
-      v4i acc[3][4];
-      float lc[3];  // per block: error bound of N in N units
-      if (PIX && do_dct) {
-        v4i Bf[3];
+      auto dct_ntile = [&](const int nt, v4i (&acc)[4], float &lc) {
+        v4i Bf = *(const v4i *)(L + (nt * 16 + bcol) * LDS_BLK + 16 * g);
+        // L1 = sum |pixel - 128| of the block bounds the integer DCT's
+        // rounding error: |N - 2^19 sum K X| <= sum |W - 2^19 K| |X| <= L1 / 2
+        uint32_t l1 = 0;
 #pragma unroll
-        for (int nt = 0; nt < 3; nt++) {
-          Bf[nt] = *(const v4i *)(L + (nt * 16 + bcol) * LDS_BLK + 16 * g);
-          // L1 = sum |pixel - 128| of the block bounds the integer DCT's
-          // rounding error: |N - 2^19 sum K X| <= sum |W - 2^19 K| |X| <= L1 / 2
-          uint32_t l1 = 0;
-#pragma unroll
-          for (int k = 0; k < 4; k++) l1 = __builtin_amdgcn_sad_u8((uint32_t)Bf[nt][k], 0x80808080u, l1);
-          const auto r16 = __builtin_amdgcn_permlane16_swap(l1, l1, false, false);
-          l1 = r16[0] + r16[1];
-          const auto r32 = __builtin_amdgcn_permlane32_swap(l1, l1, false, false);
-          // 1.25 * (L1/2 + 64) for the integer DCT and float(N), + 0.095 L1 for
-          // the fp32 roundings of t -+ tau (<= 1.8e-7 |N| with |N| <= 2^19 L1)
-          lc[nt] = fmaf((float)(r32[0] + r32[1]), 0.72f, 80.0f);
-          Bf[nt] ^= (int)0x80808080;  // pixel - 128 as int8
-        }
+        for (int k = 0; k < 4; k++) l1 = __builtin_amdgcn_sad_u8((uint32_t)Bf[k], 0x80808080u, l1);
+        const auto r16 = __builtin_amdgcn_permlane16_swap(l1, l1, false, false);
+        l1 = r16[0] + r16[1];
+        const auto r32 = __builtin_amdgcn_permlane32_swap(l1, l1, false, false);
+        // 1.25 * (L1/2 + 64) for the integer DCT and float(N), + 0.095 L1 for
+        // the fp32 roundings of t -+ tau (<= 1.8e-7 |N| with |N| <= 2^19 L1)
+        lc = fmaf((float)(r32[0] + r32[1]), 0.72f, 80.0f);
+        Bf ^= (int)0x80808080;  // pixel - 128 as int8
 #pragma unroll
         for (int d = 0; d < 3; d++)
 #pragma unroll
           for (int m = 0; m < 4; m++) {
             const int4 F = s_A[(3 * m + d) * 64 + lane];
             const v4i Fv = {F.x, F.y, F.z, F.w};
-#pragma unroll
-            for (int nt = 0; nt < 3; nt++) {
-              const v4i c = d == 0 ? v4i{0, 0, 0, 0} : acc[nt][m] << 7;
-              acc[nt][m] = (kflags & K1F_NO_MFMA) ? c + Fv + Bf[nt]
-                                                   : __builtin_amdgcn_mfma_i32_16x16x64_i8(Fv, Bf[nt], c, 0, 0, 0);
-            }
+            const v4i c = d == 0 ? v4i{0, 0, 0, 0} : acc[m] << 7;
+            acc[m] = (kflags & K1F_NO_MFMA) ? c + Fv + Bf
+                                            : __builtin_amdgcn_mfma_i32_16x16x64_i8(Fv, Bf, c, 0, 0, 0);
           }
-      }
+      };
 
       // coefficient input: all three N-tiles' loads in flight at once
       u4v pre[PIX ? 1 : 3][2];
@@ -657,18 +656,21 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
           emit_tokens(o, lane, g, bcol, valid, comp == 1, !PIX && a.dc_diffed, a.tok + fs * SEG_TOK,
                       a.seg_ntok + fs, s_hdc[TOK ? slot : 0][comp][bcol & (HREP - 1)],
                       s_hac[TOK ? slot : 0][comp][bcol & (HREP - 1)],
-                      s_st[wave]);
+                      s_st[TOK ? wave : 0]);
         }
       };
       if (PIX && do_dct) {
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
           const int comp = nt == 2 ? 1 : 0;
+          v4i acc[4];
+          float lc;  // per block: error bound of N in N units
+          dct_ntile(nt, acc, lc);
           int o[16];
           uint32_t hz = 0;  // nonzero iff some coefficient's +-tau interval straddles a boundary
           if (kflags & K1F_NO_QUANT) {
 #pragma unroll
-            for (int k = 0; k < 16; k++) o[k] = acc[nt][k >> 2][k & 3];
+            for (int k = 0; k < 16; k++) o[k] = acc[k >> 2][k & 3];
           } else
 #pragma unroll
           for (int m = 0; m < 4; m++) {
@@ -676,9 +678,9 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
             const float fa[4] = {fac.x, fac.y, fac.z, fac.w};
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-              const float nf = (float)acc[nt][m][r];
+              const float nf = (float)acc[m][r];
               // tau = fac * lc + 1e-6
-              const float tv = fmaf(fa[r], lc[nt], 1.0e-6f);
+              const float tv = fmaf(fa[r], lc, 1.0e-6f);
               const int lo = (int)fmaf(nf, fa[r], -tv);
               const int hi = (int)fmaf(nf, fa[r], tv);
               o[4 * m + r] = lo;
@@ -687,10 +689,10 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
           }
           {  // z = 0: exact from the pixel sum (fac = 0 above)
             bool tie;
-            const int dcv = dc_fast(acc[nt][0][0], 8 * q_dc[comp], s_inv8q[comp], tie);
+            const int dcv = dc_fast(acc[0][0], 8 * q_dc[comp], s_inv8q[comp], tie);
             if (g == 0) o[0] = dcv;
             if (__ballot(tie && g == 0))
-              if (g == 0 && tie) o[0] = dc_exact(acc[nt][0][0], q_dc[comp]);
+              if (g == 0 && tie) o[0] = dc_exact(acc[0][0], q_dc[comp]);
           }
           if (__ballot(hz != 0) && !(kflags & K1F_NO_REPLAY)) {
             // rare path: find the straddling coefficients (same arithmetic) and
@@ -702,22 +704,20 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
 #pragma unroll
               for (int r = 0; r < 4; r++) {
                 const int k = 4 * m + r;
-                const float nf = (float)acc[nt][m][r];
+                const float nf = (float)acc[m][r];
                 const float fa = s_fac[comp][16 * g + k];
-                const float tv = fmaf(fa, lc[nt], 1.0e-6f);
+                const float tv = fmaf(fa, lc, 1.0e-6f);
                 mm |= (uint32_t)((int)fmaf(nf, fa, -tv) != (int)fmaf(nf, fa, tv)) << k;
               }
             const uint32_t hm = mm;
-            int16_t *rep = s_st[wave][lane];
             while (mm) {
               const int k = __ffs(mm) - 1;
               mm &= mm - 1u;
               const int z = 16 * g + k;
-              rep[k] = (int16_t)ac_exact(Pb, z, s_qint[comp][z], s_cos);
-            }
+              const int v = ac_exact(Pb, z, s_qint[comp][z], s_cos);
 #pragma unroll
-            for (int k = 0; k < 16; k++)
-              if ((hm >> k) & 1u) o[k] = rep[k];
+              for (int j = 0; j < 16; j++) o[j] = j == k ? v : o[j];
+            }
             if (hm) atomicAdd(a.replays, (unsigned)__popc(hm));
           }
           if (nt == 0) dma_wait();  // next tile's DMA has landed; no store is outstanding
@@ -736,7 +736,7 @@ __global__ __launch_bounds__(256, 2) void k_mcu_dct(K1Args a) {
   }
   if (TOK) {  // per-frame histograms of this workgroup
     __syncthreads();
-    for (int i = threadIdx.x; i < 2 * 2 * 256; i += 256) {
+    for (int i = threadIdx.x; i < 2 * 2 * 256; i += NT) {
       const int slot = i >> 9, tb = (i >> 8) & 1, sym = i & 255;
       uint32_t v = 0;
 #pragma unroll
@@ -1382,7 +1382,7 @@ template <int MODE>
 static int k1_blocks_per_cu() {
   static int nb = -1;
   if (nb < 0) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_mcu_dct<MODE>, 256, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_mcu_dct<MODE>, 64 * k1_waves<MODE>(), 0) != hipSuccess ||
         nb < 1)
       nb = 1;
   }
@@ -1391,9 +1391,12 @@ static int k1_blocks_per_cu() {
 
 // persistent grid for a K1 variant: at most (resident blocks per CU) x CUs
 int k1_grid(int device, long long ntiles, int mode) {
-  int per_cu = 1;
+  int per_cu = 1, nw = 4;
   switch (mode) {
-    case K1M_COEF_OUT: per_cu = k1_blocks_per_cu<K1M_COEF_OUT>(); break;
+    case K1M_COEF_OUT:
+      per_cu = k1_blocks_per_cu<K1M_COEF_OUT>();
+      nw = k1_waves<K1M_COEF_OUT>();
+      break;
     case K1M_TOK_OUT: per_cu = k1_blocks_per_cu<K1M_TOK_OUT>(); break;
     case K1M_COEF_OUT | K1M_TOK_OUT: per_cu = k1_blocks_per_cu<K1M_COEF_OUT | K1M_TOK_OUT>(); break;
     default: per_cu = k1_blocks_per_cu<K1M_COEF_IN | K1M_TOK_OUT>(); break;
@@ -1403,7 +1406,7 @@ int k1_grid(int device, long long ntiles, int mode) {
     hipDeviceProp_t prop;
     cus = hipGetDeviceProperties(&prop, device) == hipSuccess ? prop.multiProcessorCount : 256;
   }
-  long long want = (ntiles + K1_WAVES - 1) / K1_WAVES;
+  long long want = (ntiles + nw - 1) / nw;
   long long cap = (long long)cus * per_cu;
   return (int)(want < cap ? want : cap);
 }
@@ -1415,7 +1418,9 @@ hipError_t launch_colour_lut(uint32_t *lut, hipStream_t s) {
 // mode: K1M_* bits (see k_mcu_dct)
 hipError_t launch_k1(const K1Args &a, int grid, int mode, hipStream_t s) {
   switch (mode) {
-    case K1M_COEF_OUT: hipLaunchKernelGGL((k_mcu_dct<K1M_COEF_OUT>), dim3(grid), dim3(256), 0, s, a); break;
+    case K1M_COEF_OUT:
+      hipLaunchKernelGGL((k_mcu_dct<K1M_COEF_OUT>), dim3(grid), dim3(64 * k1_waves<K1M_COEF_OUT>()), 0, s, a);
+      break;
     case K1M_TOK_OUT: hipLaunchKernelGGL((k_mcu_dct<K1M_TOK_OUT>), dim3(grid), dim3(256), 0, s, a); break;
     case K1M_COEF_OUT | K1M_TOK_OUT:
       hipLaunchKernelGGL((k_mcu_dct<K1M_COEF_OUT | K1M_TOK_OUT>), dim3(grid), dim3(256), 0, s, a);

@@ -2,7 +2,7 @@
 # scripts/pmc_k1.sh -- SQ/SQC counter passes on K1 (dct mode), one pass per group.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-out=gpurun_out/pmc_k1; mkdir -p $out
+out=gpurun_out/pmc_k1${TAG:-}; mkdir -p $out
 i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
@@ -15,10 +15,10 @@ SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_AC
 SQ_IFETCH SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_THREAD_CYCLES_VALU SQ_INSTS_BRANCH
 SQC_ICACHE_MISSES SQC_ICACHE_REQ SQC_ICACHE_HITS SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_LDS_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL SQ_INST_LEVEL_LDS
 G
-python3 - <<'PY'
-import csv, glob, collections
+OUT=$out python3 - <<'PY'
+import csv, glob, collections, os
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in glob.glob('gpurun_out/pmc_k1/p*/run_counter_collection.csv'):
+for f in glob.glob(os.environ['OUT'] + '/p*/run_counter_collection.csv'):
     for r in csv.DictReader(open(f)):
         acc[r['Kernel_Name'][:40]][r['Counter_Name']].append(float(r['Counter_Value']))
 names = sorted({c for d in acc.values() for c in d})
