@@ -19,6 +19,7 @@ namespace mij {
 int k1_grid(int device, long long ntiles, int mode);
 hipError_t launch_colour_lut(uint32_t *lut, hipStream_t s);
 hipError_t launch_k1(const K1Args &a, int grid, int mode, hipStream_t s);
+hipError_t launch_fix_blocks(const K1Args &a, hipStream_t s);
 hipError_t launch_seg_dc(const EntArgs &a, hipStream_t s);
 hipError_t launch_dc_diff(int16_t *coef, const int16_t *dc, const Geom &g, int nframes,
                           hipStream_t s);
@@ -154,6 +155,20 @@ static void fill_tables(int quality, Tables *t) {
       // in K1 from the block's L1 = sum |pixel - 128|
       t->qfac[c][z] = z ? (float)fac : 0.0f;
     }
+  // DC ties (K1 dc_tie): at |S| = 8qK the reference computes
+  // (int)(((S * M_SQRT1_2) * M_SQRT1_2) / 4 / q) (encoder.c:87-109 with the
+  // frequency-0 cosines exactly 1.0), which is K or K - 1
+  for (int c = 0; c < 2; c++) {
+    const int q0 = q[c][0];
+    for (int K = 1; K < 32 * DCTIE_WORDS && 8 * q0 * K <= 8192; K++) {
+      volatile double f = (double)(8 * q0 * K);  // volatile: keep the reference's rounding steps
+      f = f * M_SQRT1_2;
+      f = f * M_SQRT1_2;
+      f = f / 4;
+      const int r = (int)(f / q0);
+      if (r != K) t->dctie[c][K >> 5] |= 1u << (K & 31);
+    }
+  }
   // A fragments of v_mfma_i32_16x16x64_i8: lane l holds row (l & 15) and the
   // 16 k-values 16*(l>>4) .. +15.  Row r of M-tile m is zigzag coefficient
   // z = 16*(r>>2) + 4m + (r&3); k = pixel index y*8+x of the block.
@@ -209,6 +224,8 @@ struct mij_batch {
   uint8_t *d_out = nullptr;
   int *d_err = nullptr;
   unsigned *d_replays = nullptr;
+  uint32_t *d_fix = nullptr;      // K1 fix list (frame * nblk + block), worst case every block
+  unsigned *d_fix_count = nullptr;
   // bands of one large frame (mij_band_*, mij_assemble_*): per frame [4]
   int16_t *d_dcpred = nullptr;
   uint32_t *d_bitbase = nullptr;
@@ -237,7 +254,7 @@ static void batch_free(mij_batch *b) {
   void *ptrs[] = {b->d_tab, b->own_in ? b->d_in : nullptr, b->d_coef, b->d_dc, b->d_hist,
                   b->d_ehuf, b->d_raw, b->d_tok, b->d_seg_ntok, b->d_seg_bits, b->d_seg_off,
                   b->d_scan_bits, b->d_out_len, b->d_hc, b->d_out, b->d_err, b->d_replays,
-                  b->d_dcpred, b->d_bitbase, b->d_stage};
+                  b->d_dcpred, b->d_bitbase, b->d_stage, b->d_fix, b->d_fix_count};
   for (void *p : ptrs)
     if (p) hipFree(p);
   for (auto &row : b->evh)
@@ -295,6 +312,8 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
   HIP_TRY(dalloc(&b->d_out, F * g.out_cap));
   HIP_TRY(dalloc(&b->d_err, F));
   HIP_TRY(dalloc(&b->d_replays, 1));
+  HIP_TRY(dalloc(&b->d_fix, F * g.nblk));
+  HIP_TRY(dalloc(&b->d_fix_count, 1));
   HIP_TRY(hipMemsetAsync(b->d_replays, 0, sizeof(unsigned), b->stream));
   HIP_TRY(dalloc(&b->d_dcpred, F * 4));
   HIP_TRY(dalloc(&b->d_bitbase, F * 4));
@@ -395,6 +414,8 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0) {
   k.tok = b->d_tok;
   k.seg_ntok = b->d_seg_ntok;
   k.hist = b->d_hist;
+  k.fix_list = b->d_fix;
+  k.fix_count = b->d_fix_count;
   static const int k1_flags = getenv("MIJ_K1_FLAGS") ? atoi(getenv("MIJ_K1_FLAGS")) : 0;
   k.flags = k1_flags;
   const long long ntiles = (long long)nframes * b->g.tiles_per_frame;
@@ -404,7 +425,11 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0) {
   grid = (ntiles + per_wg - 1) / per_wg;
   k.per_wg = (int)per_wg;
   k.dc_diffed = dc_diffed;
+  // the coefficient variant lists hazard blocks; k_fix_blocks recomputes
+  // them in FP64 right after it, on the same stream
+  if (mode == 1) HIP_TRY(hipMemsetAsync(b->d_fix_count, 0, sizeof(unsigned), b->stream));
   HIP_TRY(launch_k1(k, (int)grid, mode, b->stream));
+  if (mode == 1) HIP_TRY(launch_fix_blocks(k, b->stream));
   return MIJ_OK;
 }
 

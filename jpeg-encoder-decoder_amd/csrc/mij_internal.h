@@ -16,6 +16,7 @@ constexpr int TILE_H = 16;
 constexpr int LDS_BLK = 80;          // bytes per staged 8x8 block (64 + pad)
 constexpr int LDS_WAVE = 48 * LDS_BLK;  // 32 Y + 16 chroma blocks per wave
 constexpr int LUT_WORDS = 1024;      // 2^15 bits per colour-exception table
+constexpr int DCTIE_WORDS = 33;      // DC tie bits for K = 0..1055 (|S| <= 8192 -> K <= 1024)
 
 // ---- entropy stage: segments ---------------------------------------------
 // A segment is the run of blocks one K1 N-tile covers in a component's scan
@@ -63,6 +64,7 @@ struct Tables {
   int dqt[2][64];         // zigzag order: DQT bytes
   double cosd[64];        // encoder.c:8-16 constants
   uint32_t lut[3][1024];  // colour-exception bitmaps (Y by R,G/2; Cb by G,B/2; Cr by G,R/2)
+  uint32_t dctie[2][DCTIE_WORDS];  // bit K: the reference's DC at |S| = 8qK is K - 1
 };
 
 struct K1Args {
@@ -81,6 +83,8 @@ struct K1Args {
   uint32_t *tok;            // token mode: per segment SEG_TOK tokens
   uint32_t *seg_ntok;       // token mode: tokens per segment
   uint32_t *hist;           // token mode: per frame [4][257] histograms
+  uint32_t *fix_list;       // coefficient mode: blocks (frame * nblk + blk) for k_fix_blocks
+  unsigned int *fix_count;  // coefficient mode: length of fix_list
 };
 // K1 diagnostic switches (timing attribution; outputs are wrong when set)
 constexpr int K1F_NO_LUT = 1, K1F_NO_REPLAY = 2, K1F_NO_COLOUR = 4, K1F_NO_DCT = 8,

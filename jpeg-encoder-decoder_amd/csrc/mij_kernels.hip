@@ -153,6 +153,17 @@ __device__ __forceinline__ int dc_fast(int S, int q8, float inv8q, bool &tie) {
   return (k ^ s) - s;
 }
 
+// DC at a tie |S| = K * 8q: the FP64 chain of dc_exact lands on K or K - 1
+// depending only on K and q; Tables::dctie holds "K - 1" bits per K, built on
+// the host with the reference's double operations (mij_api.hip fill_tables).
+// d = the fast-path value (+-K).
+__device__ __forceinline__ int dc_tie(int d, const uint32_t *bits) {
+  const int s = d >> 31;
+  int k = (d ^ s) - s;
+  k -= (int)((bits[k >> 5] >> (k & 31)) & 1u);
+  return (k ^ s) - s;
+}
+
 // One AC coefficient replayed exactly as encoder.c:87-109 computes it
 // (column pass summed from 0 in y order, row pass in x order, FP64, no FMA).
 // C = the 64 cosines (LDS), blk = the block's 64 staged pixels (LDS).  The
@@ -222,42 +233,45 @@ typedef __attribute__((address_space(1))) void global_void_t;
 constexpr int TILE_RAW = TILE_W * 3 * TILE_H;  // 6144 B of BGR888 per tile
 
 // Streams a tile's 16 rows x 384 B into LDS with global_load_lds_dwordx4 (no
-// VGPRs): instruction k moves LDS bytes [1024k, 1024k+1024), lane i the 16 B
-// at tile offset 1024k + 16i (a 384-B row holds exactly 24 such pieces).
-__device__ __forceinline__ void issue_tile_dma(const K1Args &a, const TilePos &p, int lane,
-                                               uint8_t *raw) {
+// VGPRs for the data): instruction k moves rows 2k and 2k+1 = LDS bytes
+// [768k, 768k + 768); lane i < 48 moves the 16 B at row 2k + i / 24, column
+// 16 * (i % 24).  The lane offset is the same for every k (the 2k rows go
+// into the SGPR base), so a full tile costs no VALU and one VGPR.
+constexpr int DMA_K = TILE_H / 2;
+__device__ __forceinline__ uint32_t dma_offset(int pitch, int lane) {
+  const int l = lane < 48 ? lane : 0;
+  return (uint32_t)((l / 24) * pitch + (l % 24) * 16);
+}
+__device__ __forceinline__ void issue_tile_dma(const K1Args &a, const TilePos &p, int lane, uint8_t *raw,
+                                               uint32_t off) {
   const uint8_t *src = a.in + (long long)p.f * a.in_fs + (long long)(p.ty * TILE_H) * a.pitch +
                        p.tx * TILE_W * 3;
-  const int vb = p.valid_px * 3;
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t *)raw);
+  // right frame edge: only the valid columns
+  const bool on = lane < 48 && (p.valid_px == TILE_W || (lane % 24) * 16 < p.valid_px * 3);
+  // issued as asm so the compiler does not tie the next LDS read of `raw` to
+  // vmcnt(0) -- that wait would also drain the previous tile's coefficient
+  // stores; K1 waits for the DMA itself (dma_wait) before its first store,
+  // when the DMA has long landed
+  if (on) {
 #pragma unroll
-  for (int k = 0; k < TILE_RAW / 1024; k++) {
-    const int pos = 1024 * k + 16 * lane;
-    const int row = pos / (TILE_W * 3), col = pos - row * (TILE_W * 3);
-    if (col < vb) {
-      // issued as asm so the compiler does not tie the next LDS read of `raw`
-      // to vmcnt(0) -- that wait would also drain the previous tile's
-      // coefficient stores; K1 waits for the DMA itself (dma_wait) before
-      // its first store, when the DMA has long landed
-      const uint8_t *g = src + (long long)row * a.pitch + col;
-      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off"
+    for (int k = 0; k < DMA_K; k++)
+      asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1"
                    :
-                   : "v"(g), "s"(lds0 + 1024 * k)
+                   : "v"(off), "s"(src + (long long)(2 * k) * a.pitch), "s"(lds0 + 768 * k)
                    : "memory", "m0");
-    }
   }
 }
 
 // all of this wave's outstanding vector-memory operations (the tile DMA above
 // included) have completed; VMEM operations retire in issue order
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// the tile DMA has landed once at most the wave's 6 youngest VMEM operations
+// are outstanding: the coefficient variant issues 9 stores per tile (2
+// coefficient + 1 raw-DC store per N-tile) after it, so the previous tile's
+// stores stay in flight across the wait
+__device__ __forceinline__ void dma_wait_behind_stores() { asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); }
 
-// Colour conversion of 4 pixels (12 bytes) of one row, encoder.c:133-135
-// bit-exactly.  fp32 forms (error < 2e-5 Y, < 1e-5 Cb/Cr) give
-// the truncation everywhere except at exact-integer values, which need equal
-// parities and R == G (Cb) or B == G (Cr); there the device-built bitmaps say
-// whether the FP64 reference lands one below.  The bitmap reads of a 4-pixel
-// run are issued together under one wave-uniform branch.
 // byte N of w as float (v_cvt_f32_ubyteN); asm keeps the compiler from
 // rewriting fsub(cvt(a), cvt(b)) into cvt(sub(a, b)), which costs two slow
 // conversions instead of one
@@ -271,63 +285,120 @@ __device__ __forceinline__ float ubyte_f32(uint32_t w) {
   return r;
 }
 
-// Colour conversion of 4 pixels (12 bytes) of one row, encoder.c:133-135
-// bit-exactly.  fp32 forms (error < 2e-5 Y, < 1.1e-5 Cb/Cr)
-// give the truncation everywhere except at exact-integer values, which need
-// equal parities and R == G (Cb) or B == G (Cr); there the device-built
-// bitmaps say whether the FP64 reference lands one below.  The bitmap reads
-// of a 4-pixel run are issued together under one wave-uniform branch.
-__device__ __forceinline__ void convert4(uint32_t w0, uint32_t w1, uint32_t w2,
-                                         const uint32_t *__restrict__ lut, bool use_lut,
-                                         int (&y)[4], int (&cb)[4], int (&cr)[4]) {
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// Chroma in "magic" form: x + 1.5*2^23 rounds x to an integer held in the low
+// mantissa bits, so bits(x + MAGIC) - MAGIC_BITS = round(x) and four such bit
+// patterns add as integers.  The chroma expressions carry a -0.5 + 2^-16
+// bias (CH_BIAS = 128 - 0.5 + 2^-16), which turns the rounding into the
+// floor of the exact value.
+constexpr float CH_BIAS = 127.5f + 0x1p-16f;
+constexpr float MAGIC = 12582912.0f;  // 1.5 * 2^23
+constexpr uint32_t MAGIC_BITS = 0x4B400000u;
+
+// Colour conversion of 4 pixels (12 bytes) of one row, encoder.c:133-135.
+// fp32 forms (error < 2e-5 Y, < 1e-5 Cb/Cr) give the floor
+// of the exact value; the FP64 reference differs from it only at
+// exact-integer values, which need equal parities and R == G (Cb) or B == G
+// (Cr), or fract(Y) ~ 0: there the device-built bitmaps say whether the
+// reference lands one below.  This is the common path: it only flags a
+// 4-pixel run that holds such a point (a product of the R-G and B-G
+// differences, a min of the Y fractions); the bitmap corrections are
+// applied by y_fix / chroma_fix to the values already staged in LDS, so the
+// common path carries no merge copies.
+// Outputs: y = Y values, cbm/crm = chroma in magic form, fy = fract(Y+.0005),
+// cc/cy = the run holds a possible Cb/Cr resp. Y exception.
+struct Run4 {
+  int y[4];
+  uint32_t cbm[4], crm[4];
+  float fy[4];
+  bool cc, cy;
+};
+
+__device__ __forceinline__ void convert4(uint32_t w0, uint32_t w1, uint32_t w2, Run4 &o) {
   // BGR of pixel p: w0 = B0 G0 R0 B1, w1 = G1 R1 B2 G2, w2 = R2 B3 G3 R3
-  const float fb[4] = {ubyte_f32<0>(w0), ubyte_f32<3>(w0), ubyte_f32<2>(w1), ubyte_f32<1>(w2)};
-  const float fg[4] = {ubyte_f32<1>(w0), ubyte_f32<0>(w1), ubyte_f32<3>(w1), ubyte_f32<2>(w2)};
-  const float fr[4] = {ubyte_f32<2>(w0), ubyte_f32<1>(w1), ubyte_f32<0>(w2), ubyte_f32<3>(w2)};
-  bool cy = false, cc = false;
-  bool ey[4], eb[4], er[4];
+  const f2v fb[2] = {{ubyte_f32<0>(w0), ubyte_f32<3>(w0)}, {ubyte_f32<2>(w1), ubyte_f32<1>(w2)}};
+  const f2v fg[2] = {{ubyte_f32<1>(w0), ubyte_f32<0>(w1)}, {ubyte_f32<3>(w1), ubyte_f32<2>(w2)}};
+  const f2v fr[2] = {{ubyte_f32<2>(w0), ubyte_f32<1>(w1)}, {ubyte_f32<0>(w2), ubyte_f32<3>(w2)}};
+  f2v dr[2], db[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    dr[h] = fr[h] - fg[h];
+    db[h] = fb[h] - fg[h];
+    const f2v yf = __builtin_elementwise_fma((f2v)0.114f, db[h],
+                                             __builtin_elementwise_fma((f2v)0.299f, dr[h], fg[h])) +
+                   (f2v)0.0005f;
+    const f2v cb = __builtin_elementwise_fma((f2v)-0.168736f, dr[h],
+                                             __builtin_elementwise_fma((f2v)0.5f, db[h], (f2v)CH_BIAS)) +
+                   (f2v)MAGIC;
+    const f2v cr = __builtin_elementwise_fma((f2v)-0.081312f, db[h],
+                                             __builtin_elementwise_fma((f2v)0.5f, dr[h], (f2v)CH_BIAS)) +
+                   (f2v)MAGIC;
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      // (element copies first: __builtin_bit_cast of a vector element
+      // subscript yields element 0 with this compiler)
+      const float ye = yf[e], cbe = cb[e], cre = cr[e];
+      o.y[2 * h + e] = (int)ye;
+      o.fy[2 * h + e] = __builtin_amdgcn_fractf(ye);
+      o.cbm[2 * h + e] = __float_as_uint(cbe);
+      o.crm[2 * h + e] = __float_as_uint(cre);
+    }
+  }
+  // some pixel has R == G or B == G: the product of the 8 (exact, integer)
+  // differences is 0 (|product| <= 255^8, no underflow or overflow)
+  const f2v pd = (dr[0] * db[0]) * (dr[1] * db[1]);
+  o.cc = pd[0] * pd[1] == 0.0f;
+  // some pixel has an exact-integer Y: fract(Y + 0.0005) < 0.001
+  o.cy = fminf(fminf(o.fy[0], o.fy[1]), fminf(o.fy[2], o.fy[3])) < 0.001f;
+}
+
+// Rare path: the Y corrections of a run as a packed byte-wise subtrahend.
+__device__ __forceinline__ uint32_t y_fix(uint32_t w0, uint32_t w1, uint32_t w2, const float (&fy)[4],
+                                          const uint32_t *__restrict__ lut) {
+  const uint32_t Gv[4] = {(w0 >> 8) & 255, w1 & 255, w1 >> 24, (w2 >> 16) & 255};
+  const uint32_t Rv[4] = {(w0 >> 16) & 255, (w1 >> 8) & 255, w2 & 255, w2 >> 24};
+  uint32_t corr = 0;
 #pragma unroll
   for (int p = 0; p < 4; p++) {
-    const float dr = fr[p] - fg[p], db = fb[p] - fg[p];
-    const float yf = fmaf(0.114f, db, fmaf(0.299f, dr, fg[p])) + 0.0005f;
-    y[p] = (int)yf;
-    cb[p] = (int)fmaf(-0.168736f, dr, fmaf(0.5f, db, 128.0f));
-    cr[p] = (int)fmaf(-0.081312f, db, fmaf(0.5f, dr, 128.0f));
-    ey[p] = __builtin_amdgcn_fractf(yf) < 0.001f;  // exact-integer Y
-    eb[p] = dr == 0.0f;                            // only R == G can give an integer Cb
-    er[p] = db == 0.0f;                            // only B == G can give an integer Cr
-    cy |= ey[p];
-    cc |= eb[p] | er[p];
+    const uint32_t i = (Rv[p] << 7) | (Gv[p] >> 1);  // integer Y needs R == G (mod 2)
+    const uint32_t bit = (lut[i >> 5] >> (i & 31)) & 1u;
+    corr |= (fy[p] < 0.001f ? bit : 0u) << (8 * p);
   }
-  if (!use_lut) return;
-  if (__ballot(cc | cy)) {
-    const uint32_t Bv[4] = {w0 & 255, w0 >> 24, (w1 >> 16) & 255, (w2 >> 8) & 255};
-    const uint32_t Gv[4] = {(w0 >> 8) & 255, w1 & 255, w1 >> 24, (w2 >> 16) & 255};
-    const uint32_t Rv[4] = {(w0 >> 16) & 255, (w1 >> 8) & 255, w2 & 255, w2 >> 24};
-    if (__ballot(cc)) {
-      uint32_t wb[4], wr[4];
+  return corr;
+}
+
+// Rare path: Cb / Cr corrections (0/1 per pixel) of a run.
+__device__ __forceinline__ void chroma_fix(uint32_t w0, uint32_t w1, uint32_t w2,
+                                           const uint32_t *__restrict__ lut, uint32_t (&cbc)[4],
+                                           uint32_t (&crc)[4]) {
+  const uint32_t Bv[4] = {w0 & 255, w0 >> 24, (w1 >> 16) & 255, (w2 >> 8) & 255};
+  const uint32_t Gv[4] = {(w0 >> 8) & 255, w1 & 255, w1 >> 24, (w2 >> 16) & 255};
+  const uint32_t Rv[4] = {(w0 >> 16) & 255, (w1 >> 8) & 255, w2 & 255, w2 >> 24};
 #pragma unroll
-      for (int p = 0; p < 4; p++) {
-        wb[p] = lut[LUT_WORDS + ((Gv[p] << 2) | (Bv[p] >> 6))];
-        wr[p] = lut[2 * LUT_WORDS + ((Gv[p] << 2) | (Rv[p] >> 6))];
-      }
-#pragma unroll
-      for (int p = 0; p < 4; p++) {
-        // bit (G<<7 | B>>1) of the Cb table; valid when R == G and B == G (mod 2)
-        const uint32_t bb = (wb[p] >> ((Bv[p] >> 1) & 31)) & (eb[p] && !((Bv[p] ^ Gv[p]) & 1));
-        const uint32_t br = (wr[p] >> ((Rv[p] >> 1) & 31)) & (er[p] && !((Rv[p] ^ Gv[p]) & 1));
-        cb[p] -= (int)bb;
-        cr[p] -= (int)br;
-      }
-    }
-    if (__ballot(cy)) {
-#pragma unroll
-      for (int p = 0; p < 4; p++) {
-        const uint32_t i = (Rv[p] << 7) | (Gv[p] >> 1);  // integer Y needs R == G (mod 2)
-        if (ey[p]) y[p] -= (lut[i >> 5] >> (i & 31)) & 1;
-      }
-    }
+  for (int p = 0; p < 4; p++) {
+    const uint32_t wb = lut[LUT_WORDS + ((Gv[p] << 2) | (Bv[p] >> 6))];
+    const uint32_t wr = lut[2 * LUT_WORDS + ((Gv[p] << 2) | (Rv[p] >> 6))];
+    // bit (G<<7 | B>>1) of the Cb table; valid when R == G and B == G (mod 2)
+    const bool eb = Rv[p] == Gv[p] && !((Bv[p] ^ Gv[p]) & 1);
+    const bool er = Bv[p] == Gv[p] && !((Rv[p] ^ Gv[p]) & 1);
+    cbc[p] = (wb >> ((Bv[p] >> 1) & 31)) & (uint32_t)eb;
+    crc[p] = (wr >> ((Rv[p] >> 1) & 31)) & (uint32_t)er;
   }
+}
+
+__device__ __forceinline__ uint32_t pack_y(const int (&y)[4]) {
+  return (uint32_t)y[0] | ((uint32_t)y[1] << 8) | ((uint32_t)y[2] << 16) | ((uint32_t)y[3] << 24);
+}
+
+// encoder.c:137-138 -- floor((a+b+c+d)/4) of the truncated values of the
+// chroma quads (q = 0: pixels 0,1 of both rows; q = 1: pixels 2,3), from the
+// magic forms (sum - 4 * MAGIC_BITS is the integer sum) minus corrections c
+__device__ __forceinline__ uint32_t chroma_pair(const uint32_t (&r0)[4], const uint32_t (&r1)[4],
+                                                uint32_t c0, uint32_t c1) {
+  const uint32_t s0 = (r0[0] + r0[1] + r1[0] + r1[1] - 4u * MAGIC_BITS - c0) >> 2;
+  const uint32_t s1 = (r0[2] + r0[3] + r1[2] + r1[3] - 4u * MAGIC_BITS - c1) >> 2;
+  return s0 | (s1 << 8);
 }
 
 __device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int c4, int pr,
@@ -346,25 +417,40 @@ __device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int
 #pragma unroll
   for (int it = 0; it < 4; it++) {
     const int rp = 2 * it + pr;  // row pair 0..7 == chroma row
-    int cbs[2][4], crs[2][4];
+    Run4 r[2];
+    uint32_t py[2];
+    uint32_t *Yd[2];
 #pragma unroll
     for (int dy = 0; dy < 2; dy++) {
-      int yv[4];
-      convert4(w[it][dy][0], w[it][dy][1], w[it][dy][2], lut, use_lut, yv, cbs[dy], crs[dy]);
+      convert4(w[it][dy][0], w[it][dy][1], w[it][dy][2], r[dy]);
       const int yrow = 2 * rp + dy;  // 0..15
       const int by = yrow >> 3, bx = c4 >> 1;
-      const uint32_t packed = (uint32_t)yv[0] | ((uint32_t)yv[1] << 8) | ((uint32_t)yv[2] << 16) |
-                              ((uint32_t)yv[3] << 24);
-      *(uint32_t *)(L + (by * 16 + bx) * LDS_BLK + (yrow & 7) * 8 + (c4 & 1) * 4) = packed;
+      Yd[dy] = (uint32_t *)(L + (by * 16 + bx) * LDS_BLK + (yrow & 7) * 8 + (c4 & 1) * 4);
+      py[dy] = pack_y(r[dy].y);
+      *Yd[dy] = py[dy];
     }
-    // encoder.c:137-138 -- floor((a+b+c+d)/4) of the truncated values
-    const uint32_t cb0 = (uint32_t)(cbs[0][0] + cbs[0][1] + cbs[1][0] + cbs[1][1]) >> 2;
-    const uint32_t cb1 = (uint32_t)(cbs[0][2] + cbs[0][3] + cbs[1][2] + cbs[1][3]) >> 2;
-    const uint32_t cr0 = (uint32_t)(crs[0][0] + crs[0][1] + crs[1][0] + crs[1][1]) >> 2;
-    const uint32_t cr1 = (uint32_t)(crs[0][2] + crs[0][3] + crs[1][2] + crs[1][3]) >> 2;
     uint8_t *C0 = L + (32 + (c4 >> 2)) * LDS_BLK + rp * 8 + ((2 * c4) & 7);
-    *(uint16_t *)C0 = (uint16_t)(cb0 | (cb1 << 8));
-    *(uint16_t *)(C0 + 8 * LDS_BLK) = (uint16_t)(cr0 | (cr1 << 8));
+    *(uint16_t *)C0 = (uint16_t)chroma_pair(r[0].cbm, r[1].cbm, 0, 0);
+    *(uint16_t *)(C0 + 8 * LDS_BLK) = (uint16_t)chroma_pair(r[0].crm, r[1].crm, 0, 0);
+    if (!use_lut) continue;
+    // rare paths: rewrite the staged values of runs with exceptions
+#pragma unroll
+    for (int dy = 0; dy < 2; dy++)
+      if (__ballot(r[dy].cy)) {
+        const uint32_t corr = y_fix(w[it][dy][0], w[it][dy][1], w[it][dy][2], r[dy].fy, lut);
+        if (corr) *Yd[dy] = py[dy] - corr;  // no borrows: a corrected Y is >= 1
+      }
+    if (__ballot(r[0].cc | r[1].cc)) {
+      uint32_t cbc[2][4], crc[2][4];
+#pragma unroll
+      for (int dy = 0; dy < 2; dy++) chroma_fix(w[it][dy][0], w[it][dy][1], w[it][dy][2], lut, cbc[dy], crc[dy]);
+      const uint32_t nb0 = cbc[0][0] + cbc[0][1] + cbc[1][0] + cbc[1][1];
+      const uint32_t nb1 = cbc[0][2] + cbc[0][3] + cbc[1][2] + cbc[1][3];
+      const uint32_t nr0 = crc[0][0] + crc[0][1] + crc[1][0] + crc[1][1];
+      const uint32_t nr1 = crc[0][2] + crc[0][3] + crc[1][2] + crc[1][3];
+      if (nb0 | nb1) *(uint16_t *)C0 = (uint16_t)chroma_pair(r[0].cbm, r[1].cbm, nb0, nb1);
+      if (nr0 | nr1) *(uint16_t *)(C0 + 8 * LDS_BLK) = (uint16_t)chroma_pair(r[0].crm, r[1].crm, nr0, nr1);
+    }
   }
 }
 
@@ -479,11 +565,15 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
   constexpr bool TOK = MODE & K1M_TOK_OUT;
   constexpr int NW = k1_waves<MODE>();
   constexpr int NT = 64 * NW;  // threads per workgroup
+  // coefficient variant: FP64 replays are deferred to k_fix_blocks; the
+  // token variants replay in place (their tokens are emitted here)
+  constexpr bool DEFER = MODE == K1M_COEF_OUT;
   __shared__ __attribute__((aligned(16))) uint8_t s_raw[PIX ? NW : 1][TILE_RAW];
   __shared__ __attribute__((aligned(16))) uint8_t s_tile[PIX ? NW : 1][LDS_WAVE];
   __shared__ __attribute__((aligned(16))) int4 s_A[PIX ? 12 * 64 : 1];
   __shared__ __attribute__((aligned(16))) float s_fac[2][64];
   __shared__ float s_inv8q[2];
+  __shared__ uint32_t s_dctie[2][DCTIE_WORDS];
   __shared__ uint32_t s_lut[PIX ? 3 * LUT_WORDS : 1];
   __shared__ double s_cos[64];
   __shared__ int s_qint[2][64];
@@ -509,6 +599,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
   }
   if (threadIdx.x < 128) s_qint[threadIdx.x >> 6][threadIdx.x & 63] = T->qint[threadIdx.x >> 6][threadIdx.x & 63];
   if (threadIdx.x < 2) s_inv8q[threadIdx.x] = 1.0f / (float)(8 * T->qint[threadIdx.x][0]);
+  if (threadIdx.x < 2 * DCTIE_WORDS) (&s_dctie[0][0])[threadIdx.x] = (&T->dctie[0][0])[threadIdx.x];
   if (PIX) {
     for (int i = threadIdx.x; i < 12 * 64; i += NT) s_A[i] = T->mfma_a[i];
     for (int i = threadIdx.x; i < 3 * LUT_WORDS; i += NT) s_lut[i] = (&T->lut[0][0])[i];
@@ -534,20 +625,26 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
   if (t < tend) {
     uint8_t *raw = s_raw[PIX ? wave : 0];
     TilePos p = tile_pos(G, t);
-    if (PIX) issue_tile_dma(a, p, lane, raw);
+    const uint32_t doff = dma_offset(a.pitch, lane);
+    if (PIX) issue_tile_dma(a, p, lane, raw, doff);
     for (; t < tend; t += NW) {
       TilePos pn = p;
       if (PIX) {
-        // ---- 1. colour convert + subsample + stage.  This tile's DMA was
-        // waited for before the previous tile's stores (dma_wait), except for
-        // the first tile and when the DCT phase is skipped (diagnostics).
-        if (t == t0 + wave || (kflags & K1F_NO_DCT)) dma_wait();
+        // ---- 1. colour convert + subsample + stage.  Wait for this tile's
+        // DMA: the coefficient variant leaves the previous tile's stores in
+        // flight (counted wait); the token variants waited before their first
+        // store of the previous tile; the first tile and the diagnostic
+        // variants without stores drain everything.
+        if (t == t0 + wave || (kflags & (K1F_NO_DCT | K1F_NO_STORE)))
+          dma_wait();
+        else if (DEFER)
+          dma_wait_behind_stores();
         if (!(kflags & K1F_NO_COLOUR)) colour_stage(raw, L, c4, pr, s_lut, !(kflags & K1F_NO_LUT));
         wave_lds_sync();
         // ---- stream the wave's next tile into the freed raw buffer -----------
         if (t + NW < tend) {
           pn = tile_pos(G, t + NW);
-          issue_tile_dma(a, pn, lane, raw);
+          issue_tile_dma(a, pn, lane, raw, doff);
         }
       } else if (t + NW < tend) {
         pn = tile_pos(G, t + NW);
@@ -612,22 +709,25 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
       }
 
       // ---- 3-4. quantize, replay, store, emit -----------------------------------
-      auto finish = [&](const int nt, int (&o)[16]) {
-        const int comp = nt == 2 ? 1 : 0;
-        bool valid;
-        int blk;  // block index inside the frame's coefficient space
-        int seg;  // segment index inside the frame
+      // block (index inside the frame's coefficient space) of this lane's
+      // column in N-tile nt; false for columns beyond the frame edge
+      auto block_of = [&](const int nt, int &blk) -> bool {
         if (nt < 2) {
           const int bx = p.tx * 16 + bcol;
-          valid = bx < bw;
           blk = (2 * p.ty + nt) * bw + bx;
-          seg = (2 * p.ty + nt) * G.tiles_x + p.tx;
-        } else {
-          const int mx = p.tx * 8 + (bcol & 7);
-          valid = mx < mw;
-          blk = G.nY + (bcol >= 8 ? G.nC : 0) + p.ty * mw + mx;
-          seg = G.nsy + (bcol >= 8 ? G.nsc : 0) + p.ty * G.tiles_x + p.tx;
+          return bx < bw;
         }
+        const int mx = p.tx * 8 + (bcol & 7);
+        blk = G.nY + (bcol >= 8 ? G.nC : 0) + p.ty * mw + mx;
+        return mx < mw;
+      };
+      auto finish = [&](const int nt, int (&o)[16]) {
+        const int comp = nt == 2 ? 1 : 0;
+        int blk;
+        const bool valid = block_of(nt, blk);
+        // segment index inside the frame
+        const int seg = nt < 2 ? (2 * p.ty + nt) * G.tiles_x + p.tx
+                               : G.nsy + (bcol >= 8 ? G.nsc : 0) + p.ty * G.tiles_x + p.tx;
         if (!PIX) {  // coefficients from memory (drop-in write_jpg / init_huffman)
           const u4v c0 = pre[PIX ? 0 : nt][0], c1 = pre[PIX ? 0 : nt][1];
 #pragma unroll
@@ -692,9 +792,30 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
             const int dcv = dc_fast(acc[0][0], 8 * q_dc[comp], s_inv8q[comp], tie);
             if (g == 0) o[0] = dcv;
             if (__ballot(tie && g == 0))
-              if (g == 0 && tie) o[0] = dc_exact(acc[0][0], q_dc[comp]);
+              if (g == 0 && tie) o[0] = dc_tie(dcv, s_dctie[comp]);
           }
-          if (__ballot(hz != 0) && !(kflags & K1F_NO_REPLAY)) {
+          if constexpr (DEFER) {
+            // blocks with a straddling coefficient go to the fix list;
+            // k_fix_blocks recomputes them in FP64 after this kernel
+            const unsigned long long need = __ballot(hz != 0);
+            if (need && !(kflags & K1F_NO_REPLAY)) {
+              int blk;
+              const bool valid = block_of(nt, blk);
+              const unsigned long long vm = __ballot(valid);
+              const uint32_t m16 = (uint32_t)((need | need >> 16 | need >> 32 | need >> 48) & vm) & 0xFFFFu;
+              if (m16) {
+                uint32_t base = 0;
+                if (lane == 0) {
+                  base = atomicAdd(a.fix_count, (unsigned)__popc(m16));
+                  atomicAdd(a.replays, (unsigned)__popc(m16));
+                }
+                base = __builtin_amdgcn_readfirstlane(base);
+                if (g == 0 && ((m16 >> bcol) & 1u))
+                  a.fix_list[base + __popc(m16 & ((1u << bcol) - 1u))] = (uint32_t)p.f * (uint32_t)G.nblk + (uint32_t)blk;
+              }
+            }
+          }
+          if (!DEFER && __ballot(hz != 0) && !(kflags & K1F_NO_REPLAY)) {
             // rare path: find the straddling coefficients (same arithmetic) and
             // recompute them in FP64 exactly as encoder.c:87-109
             const uint8_t *Pb = L + (nt * 16 + bcol) * LDS_BLK;
@@ -720,7 +841,9 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
             }
             if (hm) atomicAdd(a.replays, (unsigned)__popc(hm));
           }
-          if (nt == 0) dma_wait();  // next tile's DMA has landed; no store is outstanding
+          // token variants: the next tile's DMA has landed before the first
+          // store (their VMEM count per tile varies)
+          if (nt == 0 && !DEFER) dma_wait();
           finish(nt, o);
         }
       } else if (!PIX) {
@@ -755,6 +878,96 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
   }
 }
 
+
+// ===========================================================================
+// k_fix_blocks: the blocks K1 listed (a coefficient whose fast-path error
+// interval straddles a truncation boundary, or a DC tie) recomputed exactly
+// as the reference computes them: colour conversion in FP64 with uint8_t
+// truncation (encoder.c:133-135), 4:2:0 integer averages (:137-138), the
+// FP64 DCT, quantisation, clip and zigzag (:81-112, :65-70).  One wave per
+// listed block: lane l stages pixel (l & 7, l >> 3), then computes zigzag
+// coefficient l.  Persistent grid over the device-side list length.
+// ===========================================================================
+__device__ __forceinline__ int y_ref(const uint8_t *px) {  // px = B, G, R
+  const double y = __dadd_rn(__dadd_rn(__dmul_rn(0.299, (double)px[2]), __dmul_rn(0.587, (double)px[1])),
+                             __dmul_rn(0.114, (double)px[0]));
+  return (int)(uint8_t)(int)y;
+}
+__device__ __forceinline__ int cb_ref(const uint8_t *px) {
+  const double v = __dadd_rn(__dadd_rn(__dadd_rn(128.0, -__dmul_rn(0.168736, (double)px[2])),
+                                       -__dmul_rn(0.331264, (double)px[1])),
+                             __dmul_rn(0.5, (double)px[0]));
+  return (int)(uint8_t)(int)v;
+}
+__device__ __forceinline__ int cr_ref(const uint8_t *px) {
+  const double v = __dadd_rn(__dadd_rn(__dadd_rn(128.0, __dmul_rn(0.5, (double)px[2])),
+                                       -__dmul_rn(0.418688, (double)px[1])),
+                             -__dmul_rn(0.081312, (double)px[0]));
+  return (int)(uint8_t)(int)v;
+}
+
+__global__ __launch_bounds__(256) void k_fix_blocks(K1Args a) {
+  __shared__ __attribute__((aligned(8))) uint8_t s_px[4][64];
+  __shared__ double s_inner[4][64];
+  __shared__ double s_cos[64];
+  __shared__ int s_q[2][64];
+  const Tables *__restrict__ T = a.tab;
+  if (threadIdx.x < 64) s_cos[threadIdx.x] = T->cosd[threadIdx.x];
+  if (threadIdx.x < 128) s_q[threadIdx.x >> 6][threadIdx.x & 63] = T->qint[threadIdx.x >> 6][threadIdx.x & 63];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const Geom G = a.g;
+  const int bw = G.w >> 3, mw = G.w >> 4;
+  const unsigned n = *a.fix_count;
+  const int x = lane & 7, y = lane >> 3;
+  // lane z's output coefficient: zigzag z = frequency (v, u) (encoder.c:38-46)
+  const int rz = c_zigzag[lane], v = rz >> 3, u = rz & 7;
+  for (unsigned e = blockIdx.x * 4 + wave; e < n; e += gridDim.x * 4) {
+    const uint32_t id = a.fix_list[e];
+    const int f = (int)(id / (uint32_t)G.nblk), blk = (int)(id - (uint32_t)f * (uint32_t)G.nblk);
+    const uint8_t *img = a.in + (long long)f * a.in_fs;
+    int pv, comp;
+    if (blk < G.nY) {  // lane = pixel (x, y) of the block
+      comp = 0;
+      const int bx = blk % bw, by = blk / bw;
+      pv = y_ref(img + (long long)(8 * by + y) * a.pitch + (8 * bx + x) * 3);
+    } else {
+      comp = 1;
+      const int c = blk - G.nY, cr = c >= G.nC, m = cr ? c - G.nC : c;
+      const int mx = m % mw, my = m / mw;
+      const uint8_t *q = img + (long long)(16 * my + 2 * y) * a.pitch + (16 * mx + 2 * x) * 3;
+      int sum = 0;
+      for (int dy = 0; dy < 2; dy++)
+        for (int dx = 0; dx < 2; dx++) {
+          const uint8_t *px = q + (long long)dy * a.pitch + dx * 3;
+          sum += cr ? cr_ref(px) : cb_ref(px);
+        }
+      pv = sum / 4;
+    }
+    s_px[wave][lane] = (uint8_t)pv;
+    wave_lds_sync();
+    {  // column pass, lane = (x_t = lane >> 3, y_f = lane & 7), summed from 0 in y_t order
+      const int xt = lane >> 3, yf = lane & 7;
+      double in = 0.0;
+      for (int yt = 0; yt < 8; yt++)
+        in = __dadd_rn(in, __dmul_rn((double)((int)s_px[wave][yt * 8 + xt] - 128), s_cos[yt * 8 + yf]));
+      s_inner[wave][xt * 8 + yf] = in;
+    }
+    wave_lds_sync();
+    // row pass for frequency (v, u), summed from 0 in x_t order, then the
+    // 1/sqrt2 factors (u first), /4, quantisation, clip
+    double freq = 0.0;
+    for (int xt = 0; xt < 8; xt++) freq = __dadd_rn(freq, __dmul_rn(s_inner[wave][xt * 8 + v], s_cos[xt * 8 + u]));
+    if (u == 0) freq = __dmul_rn(freq, SQRT1_2);
+    if (v == 0) freq = __dmul_rn(freq, SQRT1_2);
+    freq = __dmul_rn(freq, 0.25);
+    int o = (int)__ddiv_rn(freq, (double)s_q[comp][lane]);
+    o = o < -2048 ? -2048 : (o > 2047 ? 2047 : o);
+    a.coef[(long long)f * G.coef_fs + (long long)blk * 64 + lane] = (int16_t)o;
+    if (lane == 0) a.dc[(long long)f * G.nblk + blk] = (int16_t)o;
+    wave_lds_sync();
+  }
+}
 
 // ===========================================================================
 // DC differencing in place (encoder.c:168-177), for the drop-in rgb_to_dct
@@ -1411,6 +1624,10 @@ int k1_grid(int device, long long ntiles, int mode) {
   return (int)(want < cap ? want : cap);
 }
 
+hipError_t launch_fix_blocks(const K1Args &a, hipStream_t s) {
+  hipLaunchKernelGGL(k_fix_blocks, dim3(4096), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
 hipError_t launch_colour_lut(uint32_t *lut, hipStream_t s) {
   hipLaunchKernelGGL(k_colour_lut, dim3(128), dim3(256), 0, s, lut);
   return hipGetLastError();
