@@ -224,6 +224,8 @@ struct mij_batch {
   uint8_t *d_out = nullptr;
   int *d_err = nullptr;
   unsigned *d_replays = nullptr;
+  uint32_t *d_ffc = nullptr;      // k_emit_count: 0xFF bytes per scan chunk
+  uint32_t *d_choff = nullptr;    // k_emit_scan: output offset per scan chunk
   uint32_t *d_fix = nullptr;      // K1 fix list (frame * nblk + block), worst case every block
   unsigned *d_fix_count = nullptr;
   // bands of one large frame (mij_band_*, mij_assemble_*): per frame [4]
@@ -254,7 +256,7 @@ static void batch_free(mij_batch *b) {
   void *ptrs[] = {b->d_tab, b->own_in ? b->d_in : nullptr, b->d_coef, b->d_dc, b->d_hist,
                   b->d_ehuf, b->d_raw, b->d_tok, b->d_seg_ntok, b->d_seg_bits, b->d_seg_off,
                   b->d_scan_bits, b->d_out_len, b->d_hc, b->d_out, b->d_err, b->d_replays,
-                  b->d_dcpred, b->d_bitbase, b->d_stage, b->d_fix, b->d_fix_count};
+                  b->d_dcpred, b->d_bitbase, b->d_stage, b->d_fix, b->d_fix_count, b->d_ffc, b->d_choff};
   for (void *p : ptrs)
     if (p) hipFree(p);
   for (auto &row : b->evh)
@@ -313,6 +315,8 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
   HIP_TRY(dalloc(&b->d_err, F));
   HIP_TRY(dalloc(&b->d_replays, 1));
   HIP_TRY(dalloc(&b->d_fix, F * g.nblk));
+  HIP_TRY(dalloc(&b->d_ffc, F * 3 * emit_chunks(g)));
+  HIP_TRY(dalloc(&b->d_choff, F * 3 * emit_chunks(g)));
   HIP_TRY(dalloc(&b->d_fix_count, 1));
   HIP_TRY(hipMemsetAsync(b->d_replays, 0, sizeof(unsigned), b->stream));
   HIP_TRY(dalloc(&b->d_dcpred, F * 4));
@@ -394,6 +398,8 @@ static EntArgs ent_args(mij_batch *b, int nframes) {
   a.err = b->d_err;
   a.dc_pred = b->d_dcpred;
   a.bit_base = b->d_bitbase;
+  a.ffc = b->d_ffc;
+  a.choff = b->d_choff;
   return a;
 }
 

@@ -31,6 +31,10 @@ constexpr int MAX_BLOCK_BITS = 1729;              // 28 DC + 63 * 27 AC bits
 // k_pack assembles a group in LDS windows of PACK_WORDS words; a group wider
 // than one window (only near worst-case entropy) is packed in several passes.
 constexpr int PACK_WORDS = 4096;
+// JFIF assembly: scans are written in EMIT_CH-byte chunks by EMIT_SLOTS
+// workgroups per scan
+constexpr int EMIT_CH = 4096;
+constexpr int EMIT_SLOTS = 64;
 
 // Layout-identical to the reference huff_code (include/structs.h:5-13).
 struct HuffCode {
@@ -88,7 +92,8 @@ struct K1Args {
 };
 // K1 diagnostic switches (timing attribution; outputs are wrong when set)
 constexpr int K1F_NO_LUT = 1, K1F_NO_REPLAY = 2, K1F_NO_COLOUR = 4, K1F_NO_DCT = 8,
-              K1F_NO_STORE = 16, K1F_NO_QUANT = 32, K1F_NO_MFMA = 64;
+              K1F_NO_STORE = 16, K1F_NO_QUANT = 32, K1F_NO_MFMA = 64,
+              K1F_LINEAR_STORE = 128, K1F_PLAIN_STORE = 256;
 
 struct EntArgs {
   Geom g;
@@ -111,6 +116,13 @@ struct EntArgs {
   // one large frame split into bands (mij_band_*): per frame [4]
   const int16_t *dc_pred;   // DC predictor of each component's first block (null: 0)
   const uint32_t *bit_base; // bit offset of each scan inside its first word (null: 0)
+  uint32_t *ffc;            // per frame [3][emit_chunks]: 0xFF bytes per EMIT_CH chunk
+  uint32_t *choff;          // per frame [3][emit_chunks]: output offset of each chunk
 };
+
+// EMIT_CH chunks of the largest scan buffer (the per-scan stride of EntArgs::ffc)
+__host__ __device__ inline long long emit_chunks(const Geom &g) {
+  return (g.raw_words[0] * 4 + EMIT_CH - 1) / EMIT_CH;
+}
 
 }  // namespace mij

@@ -354,6 +354,8 @@ __device__ __forceinline__ void convert4(uint32_t w0, uint32_t w1, uint32_t w2, 
 }
 
 // Rare path: the Y corrections of a run as a packed byte-wise subtrahend.
+// Only the pixel slots that hold an exact-integer Y in some lane pay for the
+// bitmap read (one wave-uniform branch per slot).
 __device__ __forceinline__ uint32_t y_fix(uint32_t w0, uint32_t w1, uint32_t w2, const float (&fy)[4],
                                           const uint32_t *__restrict__ lut) {
   const uint32_t Gv[4] = {(w0 >> 8) & 255, w1 & 255, w1 >> 24, (w2 >> 16) & 255};
@@ -361,9 +363,12 @@ __device__ __forceinline__ uint32_t y_fix(uint32_t w0, uint32_t w1, uint32_t w2,
   uint32_t corr = 0;
 #pragma unroll
   for (int p = 0; p < 4; p++) {
-    const uint32_t i = (Rv[p] << 7) | (Gv[p] >> 1);  // integer Y needs R == G (mod 2)
-    const uint32_t bit = (lut[i >> 5] >> (i & 31)) & 1u;
-    corr |= (fy[p] < 0.001f ? bit : 0u) << (8 * p);
+    const bool ey = fy[p] < 0.001f;
+    if (__ballot(ey)) {
+      const uint32_t i = (Rv[p] << 7) | (Gv[p] >> 1);  // integer Y needs R == G (mod 2)
+      const uint32_t bit = (lut[i >> 5] >> (i & 31)) & 1u;
+      corr |= (ey ? bit : 0u) << (8 * p);
+    }
   }
   return corr;
 }
@@ -746,8 +751,18 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
             s0[k] = (uint32_t)(uint16_t)o[2 * k] | ((uint32_t)o[2 * k + 1] << 16);
             s1[k] = (uint32_t)(uint16_t)o[8 + 2 * k] | ((uint32_t)o[9 + 2 * k] << 16);
           }
-          __builtin_nontemporal_store(s0, (u4v *)dst);
-          __builtin_nontemporal_store(s1, (u4v *)(dst + 8));
+          if (kflags & K1F_LINEAR_STORE) {  // diagnostics: timing of fully contiguous stores
+            const long long b0 = nt < 2 ? blk - bcol : G.nY + (long long)p.ty * mw + p.tx * 8;
+            int16_t *lin = a.coef + (long long)p.f * G.coef_fs + b0 * 64 + 8 * lane;
+            __builtin_nontemporal_store(s0, (u4v *)lin);
+            __builtin_nontemporal_store(s1, (u4v *)(lin + 512));
+          } else if (kflags & K1F_PLAIN_STORE) {  // diagnostics: default cache policy
+            *(u4v *)dst = s0;
+            *(u4v *)(dst + 8) = s1;
+          } else {
+            __builtin_nontemporal_store(s0, (u4v *)dst);
+            __builtin_nontemporal_store(s1, (u4v *)(dst + 8));
+          }
         }
         if (PIX && valid && g == 0) a.dc[(long long)p.f * G.nblk + blk] = (int16_t)o[0];
         if (TOK) {
@@ -1452,29 +1467,88 @@ __global__ __launch_bounds__(256) void k_pack(EntArgs a) {
 }
 
 // ===========================================================================
-// k_emit: one workgroup per frame assembles the JFIF stream (encoder.c
-// :549-644): SOI/APP0, DQT x2, DHT x4, SOF0, then per component SOS + the
-// scan bytes with 0xFF 0x00 stuffing (:405-408) + the pad byte of
-// fill_last_byte (:425-432: 1-bits OR-ed into the free low bits, a whole 0xFF
-// when the scan ended byte-aligned, never stuffed), then EOI.
+// JFIF assembly (encoder.c:549-644): SOI/APP0, DQT x2, DHT x4, SOF0, then per
+// component SOS + the scan bytes with 0xFF 0x00 stuffing (:405-408) + the pad
+// byte of fill_last_byte (:425-432: 1-bits OR-ed into the free low bits, a
+// whole 0xFF when the scan ended byte-aligned, never stuffed), then EOI.
+//
+// Each scan is cut into EMIT_CH-byte chunks.  k_emit_count counts the 0xFF
+// bytes of every chunk; k_emit_write then knows every chunk's output offset
+// (header + earlier scans + earlier chunks' stuffing) and writes the chunks
+// independently: the stuffed bytes are laid out in LDS and leave in
+// coalesced stores.  Workgroup (frame, comp, j) takes chunks j, j+EMIT_SLOTS..
 // ===========================================================================
-__global__ __launch_bounds__(256) void k_emit(EntArgs a) {
-  __shared__ uint32_t s_ff[256];
-  __shared__ unsigned long long s_pos;
-  const int f = blockIdx.x, tid = threadIdx.x;
-  {
-    unsigned long long need = 1024;  // headers, markers, pads
-    for (int c = 0; c < 3; c++) need += 2 * (a.scan_bits[f * 3 + c] >> 3) + 2;
-    if (a.err[f] || need > (unsigned long long)a.g.out_cap ||
-        a.scan_bits[f * 3 + 0] > 32ull * a.g.raw_words[0] ||
-        a.scan_bits[f * 3 + 1] > 32ull * a.g.raw_words[1] ||
-        a.scan_bits[f * 3 + 2] > 32ull * a.g.raw_words[2]) {
-      if (tid == 0) a.out_len[f] = 0;
-      return;
+__device__ __forceinline__ bool emit_frame_ok(const EntArgs &a, int f) {
+  unsigned long long need = 1024;  // headers, markers, pads
+  for (int c = 0; c < 3; c++) need += 2 * (a.scan_bits[f * 3 + c] >> 3) + 2;
+  return !a.err[f] && need <= (unsigned long long)a.g.out_cap &&
+         a.scan_bits[f * 3 + 0] <= 32ull * a.g.raw_words[0] &&
+         a.scan_bits[f * 3 + 1] <= 32ull * a.g.raw_words[1] &&
+         a.scan_bits[f * 3 + 2] <= 32ull * a.g.raw_words[2];
+}
+
+__device__ __forceinline__ const uint32_t *scan_raw(const EntArgs &a, int f, int comp) {
+  return a.raw + (long long)f * a.g.raw_fs +
+         (comp == 0 ? 0 : a.g.raw_words[0] + (comp == 2 ? a.g.raw_words[1] : 0));
+}
+
+// 0xFF bytes among the first `lim` (0..4) bytes of a big-endian stream word
+__device__ __forceinline__ int ff_bytes(uint32_t w, int lim) {
+  const uint32_t x = ~w;
+  const uint32_t t = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // 0x80 per zero byte of x
+  const uint32_t keep = lim >= 4 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (8 * lim));
+  return __popc(t & keep);
+}
+
+__device__ __forceinline__ int block_sum256(int v, int *red) {
+  for (int off = 32; off; off >>= 1) v += __shfl_xor(v, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const int t = red[0] + red[1] + red[2] + red[3];
+  __syncthreads();
+  return t;
+}
+
+__global__ __launch_bounds__(256) void k_emit_count(EntArgs a) {
+  __shared__ int red[4];
+  const int slot = blockIdx.x % EMIT_SLOTS, fc = blockIdx.x / EMIT_SLOTS;
+  const int f = fc / 3, comp = fc - f * 3;
+  const unsigned long long nbytes = a.scan_bits[f * 3 + comp] >> 3;
+  if (nbytes > 4ull * a.g.raw_words[comp]) return;  // k_emit_write drops the frame
+  const uint32_t *raw = scan_raw(a, f, comp);
+  const long long nch = (long long)((nbytes + EMIT_CH - 1) / EMIT_CH);
+  uint32_t *ffc = a.ffc + (long long)fc * emit_chunks(a.g);
+  for (long long c = slot; c < nch; c += EMIT_SLOTS) {
+    const unsigned long long b0 = (unsigned long long)c * EMIT_CH + threadIdx.x * (EMIT_CH / 256);
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < EMIT_CH / 4096; k++) {
+      const unsigned long long mb = b0 + 16 * k;
+      if (mb < nbytes) {
+        const uint4 v = *(const uint4 *)(raw + (mb >> 2));
+        const long long rem = (long long)(nbytes - mb);
+        cnt += ff_bytes(v.x, (int)min(rem, 4ll)) + ff_bytes(v.y, (int)max(0ll, min(rem - 4, 4ll))) +
+               ff_bytes(v.z, (int)max(0ll, min(rem - 8, 4ll))) + ff_bytes(v.w, (int)max(0ll, min(rem - 12, 4ll)));
+      }
     }
+    const int tot = block_sum256(cnt, red);
+    if (threadIdx.x == 0) ffc[c] = (uint32_t)tot;
+  }
+}
+
+// k_emit_scan: one workgroup per frame.  Headers (encoder.c:549-600), the
+// SOS of each scan, the output offset of every chunk (exclusive scan of the
+// 0xFF counts), the pad bytes (:425-432), EOI and the frame's length.
+__global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
+  __shared__ int red[4];
+  const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (!emit_frame_ok(a, f)) {
+    if (tid == 0) a.out_len[f] = 0;
+    return;
   }
   uint8_t *out = a.out + (long long)f * a.g.out_cap;
   const HuffCode *hc = a.hc + (long long)f * 4;
+  const long long nchmax = emit_chunks(a.g);
   if (tid == 0) {
     unsigned long long p = 0;
     const uint8_t app0[20] = {0xFF, 0xD8, 0xFF, 0xE0, 0x00, 0x10, 0x4A, 0x46, 0x49, 0x46,
@@ -1500,75 +1574,138 @@ __global__ __launch_bounds__(256) void k_emit(EntArgs a) {
                              (uint8_t)(W >> 8), (uint8_t)W, 0x03, 0x01, 0x22, 0x00,
                              0x02, 0x11, 0x01, 0x03, 0x11, 0x01};
     for (int i = 0; i < 19; i++) out[p++] = sof[i];
-    s_pos = p;
   }
-  __syncthreads();
+  // header length: APP0 20 + DQT 2 x 69 + DHT 4 x (21 + n) + SOF0 19
+  int hn = tid < 64 ? hc[tid >> 4].code_len_freq[1 + (tid & 15)] : 0;
+  unsigned long long pos = 20 + 2 * 69 + 19 + 4 * 21 + (unsigned long long)block_sum256(hn, red);
   for (int comp = 0; comp < 3; comp++) {
-    if (tid == 0) {
-      unsigned long long p = s_pos;
+    if (tid == 0) {  // SOS (encoder.c:601-620)
       const uint8_t sos[10] = {0xFF, 0xDA, 0x00, 0x08, 0x01, (uint8_t)(comp + 1),
                                (uint8_t)(comp ? 0x11 : 0x00), 0x00, 0x3F, 0x00};
-      for (int i = 0; i < 10; i++) out[p++] = sos[i];
-      s_pos = p;
+      for (int i = 0; i < 10; i++) out[pos + i] = sos[i];
     }
-    __syncthreads();
-    const uint32_t *raw = a.raw + (long long)f * a.g.raw_fs +
-                          (comp == 0 ? 0 : a.g.raw_words[0] + (comp == 2 ? a.g.raw_words[1] : 0));
-    const unsigned long long nbits = a.scan_bits[f * 3 + comp];
-    const unsigned long long nbytes = nbits >> 3;
-    unsigned long long pos = s_pos;
-    for (unsigned long long b0 = 0; b0 < nbytes; b0 += 256 * 16) {
-      const unsigned long long mb = b0 + (unsigned long long)tid * 16;
-      uint32_t w4[4] = {0, 0, 0, 0};
-      int cnt = 0;
-      if (mb < nbytes) {
-        const uint4 v = *(const uint4 *)(raw + (mb >> 2));
-        w4[0] = v.x; w4[1] = v.y; w4[2] = v.z; w4[3] = v.w;
-        const int lim = (int)min(16ull, nbytes - mb);
-        for (int k = 0; k < lim; k++) cnt += ((w4[k >> 2] >> (24 - 8 * (k & 3))) & 255u) == 255u;
-      }
-      // workgroup exclusive scan of the 0xFF counts
-      int xs = cnt;
-      const int lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(xs, off);
-        if (lane >= off) xs += y;
-      }
-      if (lane == 63) s_ff[wave] = (uint32_t)xs;
+    pos += 10;
+    const unsigned long long nbits = a.scan_bits[f * 3 + comp], nbytes = nbits >> 3;
+    const long long nch = (long long)((nbytes + EMIT_CH - 1) / EMIT_CH);
+    const uint32_t *cnt = a.ffc + (long long)(f * 3 + comp) * nchmax;
+    uint32_t *off = a.choff + (long long)(f * 3 + comp) * nchmax;
+    unsigned long long carry = 0;  // 0xFF bytes of the earlier chunks
+    for (long long c0 = 0; c0 < nch; c0 += 256) {
+      const long long c = c0 + tid;
+      const int v = c < nch ? (int)cnt[c] : 0;
+      const int incl = (int)wave_scan64((uint32_t)v);
+      if (lane == 63) red[wave] = incl;
       __syncthreads();
       int wb = 0, tot = 0;
-      for (int w = 0; w < 4; w++) { if (w < wave) wb += (int)s_ff[w]; tot += (int)s_ff[w]; }
-      if (mb < nbytes) {
-        unsigned long long o = pos + (unsigned long long)tid * 16 + (unsigned long long)(wb + xs - cnt);
-        const int lim = (int)min(16ull, nbytes - mb);
-        for (int k = 0; k < lim; k++) {
-          const uint8_t byte = (uint8_t)(w4[k >> 2] >> (24 - 8 * (k & 3)));
-          out[o++] = byte;
-          if (byte == 0xFF) out[o++] = 0x00;
-        }
+      for (int q = 0; q < 4; q++) {
+        if (q < wave) wb += red[q];
+        tot += red[q];
       }
-      const unsigned long long step = min(256ull * 16, nbytes - b0);
-      pos += step + (unsigned long long)tot;
       __syncthreads();
+      if (c < nch) off[c] = (uint32_t)(pos + (unsigned long long)c * EMIT_CH + carry + wb + incl - v);
+      carry += tot;
     }
-    if (tid == 0) {
+    pos += nbytes + carry;
+    if (tid == 0) {  // the pad byte of fill_last_byte, never stuffed
+      const uint32_t *raw = scan_raw(a, f, comp);
       const int r = (int)(nbits & 7);
       uint8_t pad = 0xFF;
       if (r) {
         const uint8_t part = (uint8_t)(raw[nbytes >> 2] >> (24 - 8 * (nbytes & 3)));
         pad = (uint8_t)(part | ((1u << (8 - r)) - 1u));
       }
-      out[pos++] = pad;
-      s_pos = pos;
+      out[pos] = pad;
     }
-    __syncthreads();
+    pos += 1;
   }
   if (tid == 0) {
-    unsigned long long p = s_pos;
-    out[p++] = 0xFF;
-    out[p++] = 0xD9;
-    a.out_len[f] = p;
+    out[pos] = 0xFF;
+    out[pos + 1] = 0xD9;
+    a.out_len[f] = pos + 2;
+  }
+}
+
+// k_emit_write: the stuffed bytes of every chunk at the offset k_emit_scan gave.
+__global__ __launch_bounds__(256) void k_emit_write(EntArgs a) {
+  __shared__ uint8_t s_out[2 * EMIT_CH];
+  __shared__ int red[4];
+  const int slot = blockIdx.x % EMIT_SLOTS, fc = blockIdx.x / EMIT_SLOTS;
+  const int f = fc / 3, comp = fc - f * 3;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (!emit_frame_ok(a, f)) return;
+  uint8_t *out = a.out + (long long)f * a.g.out_cap;
+  const long long nchmax = emit_chunks(a.g);
+  const unsigned long long nbytes = a.scan_bits[f * 3 + comp] >> 3;
+  const uint32_t *raw = scan_raw(a, f, comp);
+  const long long nch = (long long)((nbytes + EMIT_CH - 1) / EMIT_CH);
+  const uint32_t *cnt = a.ffc + (long long)fc * nchmax;
+  const uint32_t *offs = a.choff + (long long)fc * nchmax;
+  constexpr int WPW = EMIT_CH / 16;  // stream words per wave
+  for (long long c = slot; c < nch; c += EMIT_SLOTS) {
+    const unsigned long long cb = (unsigned long long)c * EMIT_CH;
+    const unsigned long long o0 = offs[c];
+    const int tot = (int)cnt[c];
+    // Stuffed bytes into LDS, chunk-relative.  Wave v takes stream words
+    // [WPW v, WPW v + WPW) of the chunk, lane l word 64 k + l of it in round
+    // k: consecutive lanes write consecutive bytes (no LDS bank conflicts).
+    // All of the lane's words are loaded at once; a word's offset is 4 w +
+    // the 0xFF bytes before it (wave totals through LDS, a wave scan per round).
+    const unsigned long long wb0 = cb + (unsigned long long)wave * (4 * WPW);
+    uint32_t wds[WPW / 64];
+    int lims[WPW / 64];
+    int wcnt = 0;
+#pragma unroll
+    for (int k = 0; k < WPW / 64; k++) {
+      const unsigned long long mb = wb0 + 4ull * (64 * k + lane);
+      lims[k] = mb < nbytes ? (int)min(nbytes - mb, 4ull) : 0;
+      wds[k] = lims[k] ? raw[mb >> 2] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < WPW / 64; k++) wcnt += lims[k] ? ff_bytes(wds[k], lims[k]) : 0;
+    for (int off = 32; off; off >>= 1) wcnt += __shfl_xor(wcnt, off);
+    if (lane == 0) red[wave] = wcnt;
+    __syncthreads();
+    int carry = wave * 4 * WPW;
+    for (int q = 0; q < wave; q++) carry += red[q];
+#pragma unroll
+    for (int k = 0; k < WPW / 64; k++) {
+      const int lim = lims[k];
+      const uint32_t wd = wds[k];
+      const int cf = lim ? ff_bytes(wd, lim) : 0;
+      const int incl = (int)wave_scan64((uint32_t)(lim + cf));
+      int op = carry + incl - (lim + cf);
+      carry += __shfl(incl, 63);
+      if (cf == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if (j < lim) s_out[op + j] = (uint8_t)(wd >> (24 - 8 * j));
+      } else {
+        for (int j = 0; j < lim; j++) {
+          const uint8_t byte = (uint8_t)(wd >> (24 - 8 * j));
+          s_out[op++] = byte;
+          if (byte == 0xFF) s_out[op++] = 0x00;
+        }
+      }
+    }
+    __syncthreads();
+    // copy out: head bytes up to a 4-byte boundary, whole words (re-aligned
+    // from LDS words with v_alignbyte), tail bytes; every byte of
+    // [o0, o0 + clen) belongs to this chunk alone
+    const int clen = (int)min((unsigned long long)EMIT_CH, nbytes - cb) + tot;
+    const int head = min(clen, (int)((4 - (o0 & 3)) & 3));
+    const int nwd = (clen - head) >> 2;
+    if (tid < head) out[o0 + tid] = s_out[tid];
+    const int tl = clen - head - 4 * nwd;
+    if (tid < tl) out[o0 + head + 4 * nwd + tid] = s_out[head + 4 * nwd + tid];
+    const uint32_t *s32 = (const uint32_t *)s_out;
+    uint32_t *d32 = (uint32_t *)(out + o0 + head);
+    const int sh = head & 3;  // LDS byte offset of output word j = head + 4j
+    for (int j = tid; j < nwd; j += 256) {
+      const int m = (head >> 2) + j;
+      const uint32_t lo = s32[m];
+      d32[j] = sh ? __builtin_amdgcn_alignbyte(s32[m + 1], lo, sh) : lo;
+    }
+    __syncthreads();
   }
 }
 
@@ -1689,7 +1826,9 @@ hipError_t launch_pack(const EntArgs &a, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t launch_emit(const EntArgs &a, hipStream_t s) {
-  hipLaunchKernelGGL(k_emit, dim3(a.nframes), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_emit_count, dim3(a.nframes * 3 * EMIT_SLOTS), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_emit_scan, dim3(a.nframes), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_emit_write, dim3(a.nframes * 3 * EMIT_SLOTS), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_mfma_probe(const int4 *A, const int4 *B, int4 *D, hipStream_t s) {
