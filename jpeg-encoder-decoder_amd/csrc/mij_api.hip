@@ -28,6 +28,7 @@ hipError_t launch_ehuf_struct(const HuffCode *hc, uint32_t *ehuf, hipStream_t s)
 hipError_t launch_bits(const EntArgs &a, hipStream_t s);
 hipError_t launch_scan(const EntArgs &a, hipStream_t s);
 hipError_t launch_pack(const EntArgs &a, hipStream_t s);
+hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s);
 hipError_t launch_emit(const EntArgs &a, hipStream_t s);
 hipError_t launch_or_words(uint32_t *dst, const uint32_t *src, long long n, hipStream_t s);
 hipError_t launch_mfma_probe(const int4 *A, const int4 *B, int4 *D, hipStream_t s);
@@ -226,6 +227,8 @@ struct mij_batch {
   unsigned *d_replays = nullptr;
   uint32_t *d_ffc = nullptr;      // k_emit_count: 0xFF bytes per scan chunk
   uint32_t *d_choff = nullptr;    // k_emit_scan: output offset per scan chunk
+  unsigned long long *d_pack_state = nullptr;  // k_pack_lb look-back words, per pack group
+  unsigned *d_pack_ticket = nullptr;
   uint32_t *d_fix = nullptr;      // K1 fix list (frame * nblk + block), worst case every block
   unsigned *d_fix_count = nullptr;
   // bands of one large frame (mij_band_*, mij_assemble_*): per frame [4]
@@ -256,7 +259,8 @@ static void batch_free(mij_batch *b) {
   void *ptrs[] = {b->d_tab, b->own_in ? b->d_in : nullptr, b->d_coef, b->d_dc, b->d_hist,
                   b->d_ehuf, b->d_raw, b->d_tok, b->d_seg_ntok, b->d_seg_bits, b->d_seg_off,
                   b->d_scan_bits, b->d_out_len, b->d_hc, b->d_out, b->d_err, b->d_replays,
-                  b->d_dcpred, b->d_bitbase, b->d_stage, b->d_fix, b->d_fix_count, b->d_ffc, b->d_choff};
+                  b->d_dcpred, b->d_bitbase, b->d_stage, b->d_fix, b->d_fix_count, b->d_ffc, b->d_choff,
+                  b->d_pack_state, b->d_pack_ticket};
   for (void *p : ptrs)
     if (p) hipFree(p);
   for (auto &row : b->evh)
@@ -317,6 +321,8 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
   HIP_TRY(dalloc(&b->d_fix, F * g.nblk));
   HIP_TRY(dalloc(&b->d_ffc, F * 3 * emit_chunks(g)));
   HIP_TRY(dalloc(&b->d_choff, F * 3 * emit_chunks(g)));
+  HIP_TRY(dalloc(&b->d_pack_state, F * ((g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((g.nsc + PACK_SEGS - 1) / PACK_SEGS))));
+  HIP_TRY(dalloc(&b->d_pack_ticket, 1));
   HIP_TRY(dalloc(&b->d_fix_count, 1));
   HIP_TRY(hipMemsetAsync(b->d_replays, 0, sizeof(unsigned), b->stream));
   HIP_TRY(dalloc(&b->d_dcpred, F * 4));
@@ -400,12 +406,14 @@ static EntArgs ent_args(mij_batch *b, int nframes) {
   a.bit_base = b->d_bitbase;
   a.ffc = b->d_ffc;
   a.choff = b->d_choff;
+  a.pack_state = b->d_pack_state;
+  a.pack_ticket = b->d_pack_ticket;
   return a;
 }
 
 // mode: K1 mode bits (1 coefficient planes out, 2 tokens + histograms out,
 // 4 coefficient planes in)
-static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0) {
+static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int seg_dc_inline = 0) {
   K1Args k;
   memset(&k, 0, sizeof(k));
   k.in = b->d_in;
@@ -431,6 +439,7 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0) {
   grid = (ntiles + per_wg - 1) / per_wg;
   k.per_wg = (int)per_wg;
   k.dc_diffed = dc_diffed;
+  k.seg_dc_inline = seg_dc_inline;
   // the coefficient variant lists hazard blocks; k_fix_blocks recomputes
   // them in FP64 right after it, on the same stream
   if (mode == 1) HIP_TRY(hipMemsetAsync(b->d_fix_count, 0, sizeof(unsigned), b->stream));
@@ -450,11 +459,11 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   if (t) HIP_TRY(hipEventRecord(b->ev[3], b->stream));
   if (!tables_given) HIP_TRY(launch_tables(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[4], b->stream));
-  HIP_TRY(launch_bits(a, b->stream));
+  // segment bits, scan and packing in one look-back pass (the bits / scan
+  // stage events stay, empty, so the stage list keeps its shape)
   if (t) HIP_TRY(hipEventRecord(b->ev[5], b->stream));
-  HIP_TRY(launch_scan(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[6], b->stream));
-  HIP_TRY(launch_pack(a, b->stream));
+  HIP_TRY(launch_pack_lb(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[7], b->stream));
   HIP_TRY(launch_emit(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[8], b->stream));
@@ -468,13 +477,13 @@ static int encode_frames(mij_batch *b, int nframes) {
   if (b->split) {
     if (run_k1(b, nframes, 1)) return g_err;
     if (b->timing) HIP_TRY(hipEventRecord(b->ev[1], b->stream));
-    if (run_k1(b, nframes, 6, 0)) return g_err;
+    if (run_k1(b, nframes, 6, 0, 1)) return g_err;  // segment-first DCs inline: no k_seg_dc
   } else {
     if (run_k1(b, nframes, b->keep_coefs ? 3 : 2)) return g_err;
     if (b->timing) HIP_TRY(hipEventRecord(b->ev[1], b->stream));
   }
   if (b->timing) HIP_TRY(hipEventRecord(b->ev[2], b->stream));
-  return run_entropy(b, nframes, true, false);
+  return run_entropy(b, nframes, !b->split, false);
 }
 
 static void next_slot(mij_batch *b) {

@@ -84,6 +84,8 @@ struct K1Args {
   int flags;                // diagnostics only (MIJ_K1_FLAGS): K1F_* bits
   int per_wg;               // tiles per workgroup (<= tiles_per_frame)
   int dc_diffed;            // coefficient input holds DC differences (drop-in)
+  int seg_dc_inline;        // coefficient input: first DC of each segment from the raw DCs
+  const int16_t *dc_pred;   // coefficient input, inline: DC predictor per frame [4] (null: 0)
   uint32_t *tok;            // token mode: per segment SEG_TOK tokens
   uint32_t *seg_ntok;       // token mode: tokens per segment
   uint32_t *hist;           // token mode: per frame [4][257] histograms
@@ -118,6 +120,8 @@ struct EntArgs {
   const uint32_t *bit_base; // bit offset of each scan inside its first word (null: 0)
   uint32_t *ffc;            // per frame [3][emit_chunks]: 0xFF bytes per EMIT_CH chunk
   uint32_t *choff;          // per frame [3][emit_chunks]: output offset of each chunk
+  unsigned long long *pack_state;  // k_pack_lb: per pack group, flag << 62 | bits
+  unsigned int *pack_ticket;       // k_pack_lb: next group to claim
 };
 
 // EMIT_CH chunks of the largest scan buffer (the per-scan stride of EntArgs::ffc)

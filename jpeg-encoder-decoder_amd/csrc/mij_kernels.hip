@@ -471,10 +471,12 @@ constexpr uint32_t TOK_AC = 1u << 10;
 // Tokens of a block, in bitstream order (encoder.c:462-502): its DC
 // difference (:434-446), the AC run/size symbols (:448-460, ZRLs folded in,
 // :490-494), then EOB unless coefficient 63 is nonzero (:479-484).  The DC of
-// a segment's first block depends on the previous segment, so unless
-// dc_diffed it is left for k_seg_dc.
+// a segment's first block depends on the previous segment: with first_pred
+// the caller supplies that block's predecessor DC (pred0), otherwise (token
+// variant fed from pixels) it is left for k_seg_dc.
 __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g, int bcol,
                                             bool valid, bool chroma, bool dc_diffed,
+                                            bool first_pred, int pred0,
                                             uint32_t *segtok, uint32_t *segcnt, uint32_t *hDC,
                                             uint32_t *hAC, int16_t (*st)[16]) {
   u4v c0, c1;
@@ -520,8 +522,8 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
   if (g == 0) {
     if (pos == (chroma ? 7 : 15)) *segcnt = incl;
     if (valid) {
-      if (dc_diffed || pos != 0) {
-        const int diff = dc_diffed ? dc0 : dc0 - prev;  // :168-177
+      if (dc_diffed || pos != 0 || first_pred) {
+        const int diff = dc_diffed ? dc0 : dc0 - (pos != 0 ? prev : pred0);  // :168-177
         const int cls = mag_class(diff);
         segtok[base] = (uint32_t)cls | (mag_bits(diff, cls) << 16);
         atomicAdd(&hDC[cls], 1u);
@@ -768,7 +770,18 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
         if (TOK) {
           const long long fs = (long long)p.f * G.nseg + seg;
           const int slot = p.f - f0;
-          emit_tokens(o, lane, g, bcol, valid, comp == 1, !PIX && a.dc_diffed, a.tok + fs * SEG_TOK,
+          // the coefficient-input variant predicts a segment's first DC from the
+          // raw DC K1 stored for the block before it (0 at a component start,
+          // or the band predictor), unless k_seg_dc runs (seg_dc_inline == 0)
+          int pred0 = 0;
+          const bool first_pred = !PIX && a.seg_dc_inline;
+          if (first_pred && valid && g == 0 && (comp == 1 ? (bcol & 7) : bcol) == 0) {
+            const int cstart = comp == 0 ? 0 : (bcol >= 8 ? G.nY + G.nC : G.nY);
+            pred0 = blk == cstart ? (a.dc_pred ? (int)a.dc_pred[p.f * 4 + (comp == 0 ? 0 : (bcol >= 8 ? 2 : 1))] : 0)
+                                  : (int)a.dc[(long long)p.f * G.nblk + blk - 1];
+          }
+          emit_tokens(o, lane, g, bcol, valid, comp == 1, !PIX && a.dc_diffed, first_pred, pred0,
+                      a.tok + fs * SEG_TOK,
                       a.seg_ntok + fs, s_hdc[TOK ? slot : 0][comp][bcol & (HREP - 1)],
                       s_hac[TOK ? slot : 0][comp][bcol & (HREP - 1)],
                       s_st[TOK ? wave : 0]);
@@ -1467,6 +1480,192 @@ __global__ __launch_bounds__(256) void k_pack(EntArgs a) {
 }
 
 // ===========================================================================
+// k_pack_lb: segment bits, scan offsets and bit packing in one pass.  Each
+// workgroup takes the next pack group of PACK_SEGS segments of one scan (a
+// ticket keeps groups claimed in scan order), sums its segments' token bits,
+// and finds the group's start bit by decoupled look-back over the groups
+// before it in the same scan (per group: aggregate, then inclusive prefix,
+// published in one 64-bit word).  The shared edge words: a group zeroes its
+// last word before it publishes its prefix (the next group ORs into that
+// word only after reading the prefix) and ORs both of its edge words;
+// interior words are stored plainly.  Then it packs as k_pack does.
+// ===========================================================================
+constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1;
+
+__global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
+  __shared__ uint32_t buf[PACK_WORDS];
+  __shared__ uint32_t tab[2][256];
+  __shared__ uint32_t s_bits[PACK_SEGS], s_off[PACK_SEGS];
+  __shared__ unsigned long long s_prefix;
+  __shared__ int s_ticket;
+  const Geom &G = a.g;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_ticket = (int)atomicAdd(a.pack_ticket, 1u);
+  __syncthreads();
+  const int gid = s_ticket;  // groups in (frame, scan, q) order
+  const int gy = (G.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (G.nsc + PACK_SEGS - 1) / PACK_SEGS;
+  const int gpf = gy + 2 * gc;
+  const int f = gid / gpf;
+  int q = gid - f * gpf, comp, sbase, ns;
+  if (q < gy) {
+    comp = 0; sbase = 0; ns = G.nsy;
+  } else {
+    q -= gy;
+    comp = 1 + (q >= gc);
+    if (q >= gc) q -= gc;
+    sbase = comp == 1 ? G.nsy : G.nsy + G.nsc;
+    ns = G.nsc;
+  }
+  const int nq = comp == 0 ? gy : gc;
+  const int gscan0 = gid - q;  // ticket of the scan's first group
+  const int chroma = comp != 0;
+  const int s0 = q * PACK_SEGS, s1 = min(ns, s0 + PACK_SEGS), nsg = s1 - s0;
+  const long long fs0 = (long long)f * G.nseg + sbase;
+  for (int i = tid; i < 512; i += 256) tab[i >> 8][i & 255] = a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + i];
+  __syncthreads();
+  const uint32_t zac = tab[1][0xF0];
+  const int Lz = (int)(zac >> 16);
+  // ---- 1. bits of each segment (16 lanes per segment) --------------------
+  const int sub = tid & 15, row = tid >> 4;
+  for (int sl = row; sl < nsg; sl += 16) {
+    const long long fs = fs0 + s0 + sl;
+    const int n = min((int)a.seg_ntok[fs], SEG_TOK);
+    const uint32_t *tk = a.tok + fs * SEG_TOK;
+    uint32_t b = 0;
+    for (int i0 = 0; i0 < n; i0 += 64) {
+      uint32_t t[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int i = i0 + 16 * u + sub;
+        t[u] = i < n ? tk[i] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint32_t tk4 = t[u], sym = tk4 & 255u;
+        if (i0 + 16 * u + sub < n)
+          b += (tab[(tk4 & TOK_AC) ? 1 : 0][sym] >> 16) + (sym & 15u) + ((tk4 >> 8) & 3u) * (uint32_t)Lz;
+      }
+    }
+    b = row_scan16(b);
+    if (sub == 15) s_bits[sl] = b;
+  }
+  __syncthreads();
+  // ---- 2. offsets inside the group, group total, look-back -----------------
+  if (wave == 0) {
+    const uint32_t v = lane < nsg ? s_bits[lane] : 0u;
+    const uint32_t incl = wave_scan64(v);
+    if (lane < nsg) s_off[lane] = incl - v;
+    const unsigned long long T = __shfl(incl, 63);
+    const unsigned long long base = a.bit_base ? a.bit_base[f * 4 + comp] : 0u;
+    unsigned long long *st = a.pack_state;
+    unsigned long long prefix = base;
+    if (q > 0) {
+      if (lane == 0) __hip_atomic_store(&st[gid], LB_AGG | T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      prefix = 0;
+      long long j = gid - 1;
+      while (true) {
+        const long long jj = j - lane;
+        unsigned long long sv = jj >= gscan0 ? __hip_atomic_load(&st[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                             : (LB_INC | base);
+        const unsigned long long m2 = __ballot((sv >> 62) == 2), m0 = __ballot((sv >> 62) == 0);
+        const unsigned long long upto = m2 ? (m2 & (~m2 + 1)) : 0ull;  // lowest inclusive lane
+        if (m0 & (upto ? upto - 1 : ~0ull)) {  // a group before it has not published yet
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        const int k = upto ? __ffsll((long long)m2) - 1 : 63;
+        unsigned long long add = lane <= k ? (sv & LB_VAL) : 0ull;
+        for (int off = 32; off; off >>= 1) add += __shfl_xor(add, off);
+        prefix += add;
+        if (upto) break;
+        j -= 64;
+      }
+    }
+    if (lane == 0) {
+      // zero the group's last word before the next group may OR into it; the
+      // first word of a scan is zeroed by its first group; a last word that is
+      // also the first word of a group starting mid-word belongs to the
+      // previous group, which zeroed it
+      const unsigned long long wf = prefix >> 5, wl = (prefix + T - 1) >> 5;
+      uint32_t *raw = a.raw + (long long)f * G.raw_fs +
+                      (comp == 0 ? 0 : G.raw_words[0] + (comp == 2 ? G.raw_words[1] : 0));
+      const bool ok = T > 0 && wl + 1 < (unsigned long long)G.raw_words[comp];
+      // (atomics: the per-XCD L2s are not coherent, so a plain store could be
+      // written back over the next group's OR; the state words need no fence,
+      // they carry their own data, relaxed at agent scope = coherent sc1 access)
+      if (ok && q == 0) atomicAnd(&raw[wf], 0u);
+      if (ok && (wl != wf || (prefix & 31) == 0)) atomicAnd(&raw[wl], 0u);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(&st[gid], LB_INC | (prefix + T), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (q == nq - 1) a.scan_bits[f * 3 + comp] = prefix + T;
+      s_prefix = prefix;
+    }
+  }
+  __syncthreads();
+  // ---- 3. pack the group's tokens (as k_pack) -------------------------------
+  const unsigned long long gbase = s_prefix;
+  const uint32_t bit0 = (uint32_t)(gbase & 31);
+  const unsigned long long gbits = (unsigned long long)(nsg ? s_off[nsg - 1] + s_bits[nsg - 1] : 0u);
+  uint32_t nw = (uint32_t)((bit0 + gbits + 31) >> 5);  // words of the group
+  if ((gbase >> 5) + nw + 1 > (unsigned long long)G.raw_words[comp]) {  // cannot happen for valid
+    if (tid == 0) a.err[f] = 2;                                          // tokens; never write OOB
+    nw = 0;
+  }
+  uint32_t *raw = a.raw + (long long)f * G.raw_fs +
+                  (comp == 0 ? 0 : G.raw_words[0] + (comp == 2 ? G.raw_words[1] : 0)) + (gbase >> 5);
+  for (uint32_t w0 = 0; w0 < nw; w0 += PACK_WORDS) {
+    const uint32_t wn = min((uint32_t)PACK_WORDS, nw - w0);
+    const uint32_t lo_bit = w0 * 32, hi_bit = (w0 + wn) * 32;
+    for (uint32_t i = tid; i < wn; i += 256) buf[i] = 0;
+    __syncthreads();
+    for (int sl = row; sl < nsg; sl += 16) {
+      const long long fs = fs0 + s0 + sl;
+      const uint32_t sb = bit0 + s_off[sl];
+      if (sb >= hi_bit || sb + s_bits[sl] <= lo_bit) continue;  // row-uniform
+      const int n = min((int)a.seg_ntok[fs], SEG_TOK);
+      const uint32_t *tk = a.tok + fs * SEG_TOK;
+      uint32_t pos0 = sb;
+      uint32_t tq[4];  // tokens of the next 64, loaded ahead (latency-bound loop)
+#pragma unroll
+      for (int u = 0; u < 4; u++) tq[u] = 16 * u + sub < n ? tk[16 * u + sub] : 0u;
+      for (int i0 = 0; i0 < n; i0 += 16) {
+        const int i = i0 + sub;
+        const uint32_t t = tq[0];
+        tq[0] = tq[1];
+        tq[1] = tq[2];
+        tq[2] = tq[3];
+        tq[3] = i + 64 < n ? tk[i + 64] : 0u;
+        const uint32_t sym = t & 255u, cls = sym & 15u;
+        const uint32_t e = i < n ? tab[(t & TOK_AC) ? 1 : 0][sym] : 0u;
+        const uint32_t nz = (t >> 8) & 3u;
+        const uint32_t L = (e >> 16) + cls;
+        const uint32_t nb = i < n ? L + nz * (uint32_t)Lz : 0u;
+        const uint32_t x = row_scan16(nb);
+        uint32_t pos = pos0 + x - nb;
+        if (nb && pos < hi_bit && pos + nb > lo_bit) {
+          for (uint32_t k = nz; k; k--) {  // encoder.c:490-494 ZRL
+            put_bits_window(buf, pos, lo_bit, hi_bit, zac & 0xFFFFu, Lz);
+            pos += Lz;
+          }
+          if (L) put_bits_window(buf, pos, lo_bit, hi_bit, ((e & 0xFFFFu) << cls) | (t >> 16), (int)L);
+        }
+        pos0 += __shfl(x, 15, 16);
+      }
+    }
+    __syncthreads();
+    // the first word is shared with the previous group only when the group
+    // starts mid-word (then that group zeroed it); the last word was zeroed
+    // before the prefix was published
+    for (uint32_t i = tid; i < wn; i += 256) {
+      const uint32_t wi = w0 + i;
+      if ((wi == 0 && bit0) || wi == nw - 1) atomicOr(&raw[wi], buf[i]);
+      else raw[wi] = buf[i];
+    }
+    __syncthreads();
+  }
+}
+
+// ===========================================================================
 // JFIF assembly (encoder.c:549-644): SOI/APP0, DQT x2, DHT x4, SOF0, then per
 // component SOS + the scan bytes with 0xFF 0x00 stuffing (:405-408) + the pad
 // byte of fill_last_byte (:425-432: 1-bits OR-ed into the free low bits, a
@@ -1823,6 +2022,15 @@ hipError_t launch_or_words(uint32_t *dst, const uint32_t *src, long long n, hipS
 hipError_t launch_pack(const EntArgs &a, hipStream_t s) {
   const int gy = (a.g.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (a.g.nsc + PACK_SEGS - 1) / PACK_SEGS;
   hipLaunchKernelGGL(k_pack, dim3(a.nframes * (gy + 2 * gc)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s) {
+  const int gy = (a.g.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (a.g.nsc + PACK_SEGS - 1) / PACK_SEGS;
+  const long long groups = (long long)a.nframes * (gy + 2 * gc);
+  hipError_t e = hipMemsetAsync(a.pack_state, 0, sizeof(unsigned long long) * groups, s);
+  if (e == hipSuccess) e = hipMemsetAsync(a.pack_ticket, 0, sizeof(unsigned), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_pack_lb, dim3((unsigned)groups), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_emit(const EntArgs &a, hipStream_t s) {
