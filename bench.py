@@ -360,7 +360,9 @@ def main():
                     for k, v in kernels.items()},
         "stages_ms": stage_avg,
         "verified_frames": verified,
-        "fp64_replays_per_frame": round(batch.replays() / (F * (args.warmup + args.steps)), 2),
+        # blocks re-encoded in FP64 by k_fix_blocks (split pipeline) or coefficients
+        # replayed in place (fused pipeline), per frame
+        "fp64_fixups_per_frame": round(batch.replays() / (F * (args.warmup + args.steps)), 2),
     }
     traffic, src = pmc_traffic(dom, res["config"])
     if traffic is not None:

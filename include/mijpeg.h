@@ -134,21 +134,24 @@ int mij_batch_coefs(mij_batch *b, int frame, int16_t *Y, int16_t *Cb,
 int mij_batch_tables(mij_batch *b, int frame, huff_code out[4]);
 /* timing: when enabled, HIP events bracket each stage of the next encode;
  * mij_batch_stage_ms returns up to n (<= MIJ_NSTAGES) stage durations (ms) of
- * the last one: [0]=K1 colour+DCT+quant (+tokens when fused), [1]=tokenize
- * (split pipeline), [2]=stats (segment DC fixup), [3]=tables, [4]=bits,
- * [5]=scan, [6]=pack, [7]=emit, [8]=whole encode */
-#define MIJ_NSTAGES 9
+ * the last one: [0]=K1 colour+DCT+quant (+tokens when fused), [1]=fix (FP64
+ * re-encode of the blocks K1 listed), [2]=tokenize (split pipeline),
+ * [3]=stats (segment DC fixup, fused pipeline), [4]=tables, [5]=pack
+ * (segment bits + offsets + bit packing), [6]=emit (JFIF assembly),
+ * [7]=whole encode */
+#define MIJ_NSTAGES 8
 int mij_batch_set_timing(mij_batch *b, int on);
 int mij_batch_stage_ms(mij_batch *b, float *ms, int n);
 /* the same for each of the last `steps` encodes (<= 64) issued while timing
- * was on, oldest first: ms[step*8 + stage]; returns the count filled */
+ * was on, oldest first: ms[step*MIJ_NSTAGES + stage]; returns the count filled */
 int mij_batch_stage_history(mij_batch *b, float *ms, int steps);
 /* symbol tokens K1 emitted for the last encode of nframes frames (4 bytes
  * each; used for the bandwidth accounting of the fused kernel) */
 unsigned long long mij_batch_token_count(mij_batch *b, int nframes);
 /* {w, h, 8x8 blocks per frame, segments per frame, K1 tiles per frame} */
 int mij_batch_geometry(mij_batch *b, long long *out, int n);
-/* coefficients recomputed in FP64 since creation (hazard replays) */
+/* FP64 fix-ups since creation: blocks re-encoded by the fix-up kernel after
+ * K1 (split pipeline) plus coefficients replayed in place (fused pipeline) */
 unsigned long long mij_batch_replays(mij_batch *b);
 /* the batch's hipStream_t, as an opaque pointer */
 void *mij_batch_stream(mij_batch *b);

@@ -444,7 +444,9 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int se
   // them in FP64 right after it, on the same stream
   if (mode == 1) HIP_TRY(hipMemsetAsync(b->d_fix_count, 0, sizeof(unsigned), b->stream));
   HIP_TRY(launch_k1(k, (int)grid, mode, b->stream));
+  if (b->timing && mode != 6) HIP_TRY(hipEventRecord(b->ev[1], b->stream));
   if (mode == 1) HIP_TRY(launch_fix_blocks(k, b->stream));
+  if (b->timing && mode != 6) HIP_TRY(hipEventRecord(b->ev[2], b->stream));
   return MIJ_OK;
 }
 
@@ -456,17 +458,14 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   EntArgs a = ent_args(b, nframes);
   const bool t = b->timing;
   if (dc_fix) HIP_TRY(launch_seg_dc(a, b->stream));
-  if (t) HIP_TRY(hipEventRecord(b->ev[3], b->stream));
-  if (!tables_given) HIP_TRY(launch_tables(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[4], b->stream));
-  // segment bits, scan and packing in one look-back pass (the bits / scan
-  // stage events stay, empty, so the stage list keeps its shape)
+  if (!tables_given) HIP_TRY(launch_tables(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[5], b->stream));
-  if (t) HIP_TRY(hipEventRecord(b->ev[6], b->stream));
+  // segment bits, scan offsets and packing in one look-back pass
   HIP_TRY(launch_pack_lb(a, b->stream));
-  if (t) HIP_TRY(hipEventRecord(b->ev[7], b->stream));
+  if (t) HIP_TRY(hipEventRecord(b->ev[6], b->stream));
   HIP_TRY(launch_emit(a, b->stream));
-  if (t) HIP_TRY(hipEventRecord(b->ev[8], b->stream));
+  if (t) HIP_TRY(hipEventRecord(b->ev[7], b->stream));
   return MIJ_OK;
 }
 
@@ -475,14 +474,12 @@ static int encode_frames(mij_batch *b, int nframes) {
   HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * nframes, b->stream));
   if (b->timing) HIP_TRY(hipEventRecord(b->ev[0], b->stream));
   if (b->split) {
-    if (run_k1(b, nframes, 1)) return g_err;
-    if (b->timing) HIP_TRY(hipEventRecord(b->ev[1], b->stream));
+    if (run_k1(b, nframes, 1)) return g_err;  // records events 1 and 2 around the fixer
     if (run_k1(b, nframes, 6, 0, 1)) return g_err;  // segment-first DCs inline: no k_seg_dc
   } else {
-    if (run_k1(b, nframes, b->keep_coefs ? 3 : 2)) return g_err;
-    if (b->timing) HIP_TRY(hipEventRecord(b->ev[1], b->stream));
+    if (run_k1(b, nframes, b->keep_coefs ? 3 : 2)) return g_err;  // events 1 and 2 (no fixer)
   }
-  if (b->timing) HIP_TRY(hipEventRecord(b->ev[2], b->stream));
+  if (b->timing) HIP_TRY(hipEventRecord(b->ev[3], b->stream));
   return run_entropy(b, nframes, !b->split, false);
 }
 
@@ -516,9 +513,9 @@ extern "C" int mij_batch_dct(mij_batch *b, int nframes) {
   HIP_TRY(hipSetDevice(b->dev));
   next_slot(b);
   if (b->timing) HIP_TRY(hipEventRecord(b->ev[0], b->stream));
-  if (run_k1(b, nframes, 1)) return g_err;
+  if (run_k1(b, nframes, 1)) return g_err;  // events 1, 2
   if (b->timing)
-    for (int k = 1; k < MIJ_NSTAGES; k++) HIP_TRY(hipEventRecord(b->ev[k], b->stream));
+    for (int k = 3; k < MIJ_NSTAGES; k++) HIP_TRY(hipEventRecord(b->ev[k], b->stream));
   return MIJ_OK;
 }
 
@@ -544,8 +541,10 @@ static float elapsed(hipEvent_t a, hipEvent_t z) {
 }
 
 // stage i spans events (i, i+1); the last one is the whole encode
-static const int k_stage_pairs[MIJ_NSTAGES][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5},
-                                                  {5, 6}, {6, 7}, {7, 8}, {0, 8}};
+// events: 0 start, 1 after K1, 2 after the fixer, 3 after tokenize, 4 after
+// the segment DC fixup, 5 after the tables, 6 after pack, 7 after emit
+static const int k_stage_pairs[MIJ_NSTAGES][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4},
+                                                  {4, 5}, {5, 6}, {6, 7}, {0, 7}};
 
 extern "C" int mij_batch_stage_history(mij_batch *b, float *ms, int steps) {
   if (!b || !ms || steps < 1) return fail(MIJ_EINVAL, "stage_history: bad args");

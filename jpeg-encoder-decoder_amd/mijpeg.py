@@ -196,8 +196,7 @@ def encode(frame_bgr: np.ndarray, quality: int = 50, region=None) -> bytes:
 # ---- device-resident batch ---------------------------------------------------
 
 class Batch:
-    STAGES = ["k1_colour_dct_quant", "tokenize", "stats", "tables", "bits", "scan", "pack", "emit",
-              "total"]
+    STAGES = ["k1_colour_dct_quant", "fix", "tokenize", "stats", "tables", "pack", "emit", "total"]
 
     def __init__(self, w: int, h: int, max_frames: int, quality: int = 50, device: int = 0,
                  keep_coefs: bool = False):
