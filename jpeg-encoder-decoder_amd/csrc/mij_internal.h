@@ -95,7 +95,8 @@ struct K1Args {
 // K1 diagnostic switches (timing attribution; outputs are wrong when set)
 constexpr int K1F_NO_LUT = 1, K1F_NO_REPLAY = 2, K1F_NO_COLOUR = 4, K1F_NO_DCT = 8,
               K1F_NO_STORE = 16, K1F_NO_QUANT = 32, K1F_NO_MFMA = 64,
-              K1F_LINEAR_STORE = 128, K1F_PLAIN_STORE = 256;
+              K1F_LINEAR_STORE = 128, K1F_PLAIN_STORE = 256,
+              K1F_NO_HIST = 512, K1F_NO_TOKSTORE = 1024;
 
 struct EntArgs {
   Geom g;

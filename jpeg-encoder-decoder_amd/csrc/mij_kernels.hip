@@ -478,7 +478,7 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
                                             bool valid, bool chroma, bool dc_diffed,
                                             bool first_pred, int pred0,
                                             uint32_t *segtok, uint32_t *segcnt, uint32_t *hDC,
-                                            uint32_t *hAC, int16_t (*st)[16]) {
+                                            uint32_t *hAC, int16_t (*st)[16], int kflags = 0) {
   u4v c0, c1;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
@@ -545,10 +545,13 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
       const int run = z - (63 - __clzll(before | 1ull)) - 1;
       const int cls = mag_class(cz);
       const int sym = ((run & 15) << 4) | cls;
-      segtok[base + 1 + __popcll(before)] =
-          (uint32_t)sym | ((uint32_t)(run >> 4) << 8) | TOK_AC | (mag_bits(cz, cls) << 16);
-      atomicAdd(&hAC[sym], 1u);
-      if (run >= 16) atomicAdd(&hAC[0xF0], (unsigned)(run >> 4));
+      if (!(kflags & K1F_NO_TOKSTORE))
+        segtok[base + 1 + __popcll(before)] =
+            (uint32_t)sym | ((uint32_t)(run >> 4) << 8) | TOK_AC | (mag_bits(cz, cls) << 16);
+      if (!(kflags & K1F_NO_HIST)) {
+        atomicAdd(&hAC[sym], 1u);
+        if (run >= 16) atomicAdd(&hAC[0xF0], (unsigned)(run >> 4));
+      }
     }
   }
   wave_lds_sync();
@@ -634,6 +637,31 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
     TilePos p = tile_pos(G, t);
     const uint32_t doff = dma_offset(a.pitch, lane);
     if (PIX) issue_tile_dma(a, p, lane, raw, doff);
+    // coefficient input: the three N-tiles' 32 B per lane of a tile
+    auto load_coefs = [&](const TilePos &pp, u4v (&dst)[PIX ? 1 : 3][2]) {
+#pragma unroll
+      for (int nt = 0; nt < 3; nt++) {
+        bool valid;
+        long long blk;
+        if (nt < 2) {
+          const int bx = pp.tx * 16 + bcol;
+          valid = bx < bw;
+          blk = (long long)(2 * pp.ty + nt) * bw + bx;
+        } else {
+          const int mx = pp.tx * 8 + (bcol & 7);
+          valid = mx < mw;
+          blk = G.nY + (bcol >= 8 ? G.nC : 0) + (long long)pp.ty * mw + mx;
+        }
+        dst[PIX ? 0 : nt][0] = dst[PIX ? 0 : nt][1] = u4v{0, 0, 0, 0};
+        if (valid) {
+          const int16_t *src = a.coef + (long long)pp.f * G.coef_fs + blk * 64 + 16 * g;
+          dst[PIX ? 0 : nt][0] = *(const u4v *)src;
+          dst[PIX ? 0 : nt][1] = *(const u4v *)(src + 8);
+        }
+      }
+    };
+    u4v cnext[PIX ? 1 : 3][2];
+    if (!PIX) load_coefs(p, cnext);
     for (; t < tend; t += NW) {
       TilePos pn = p;
       if (PIX) {
@@ -690,29 +718,16 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
           }
       };
 
-      // coefficient input: all three N-tiles' loads in flight at once
+      // coefficient input: this tile's planes were loaded one tile ahead;
+      // the next tile's loads go out now, in flight during this tile's work
       u4v pre[PIX ? 1 : 3][2];
       if (!PIX) {
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
-          bool valid;
-          long long blk;
-          if (nt < 2) {
-            const int bx = p.tx * 16 + bcol;
-            valid = bx < bw;
-            blk = (long long)(2 * p.ty + nt) * bw + bx;
-          } else {
-            const int mx = p.tx * 8 + (bcol & 7);
-            valid = mx < mw;
-            blk = G.nY + (bcol >= 8 ? G.nC : 0) + (long long)p.ty * mw + mx;
-          }
-          pre[PIX ? 0 : nt][0] = pre[PIX ? 0 : nt][1] = u4v{0, 0, 0, 0};
-          if (valid) {
-            const int16_t *src = a.coef + (long long)p.f * G.coef_fs + blk * 64 + 16 * g;
-            pre[PIX ? 0 : nt][0] = *(const u4v *)src;
-            pre[PIX ? 0 : nt][1] = *(const u4v *)(src + 8);
-          }
+          pre[PIX ? 0 : nt][0] = cnext[PIX ? 0 : nt][0];
+          pre[PIX ? 0 : nt][1] = cnext[PIX ? 0 : nt][1];
         }
+        if (t + NW < tend) load_coefs(pn, cnext);
       }
 
       // ---- 3-4. quantize, replay, store, emit -----------------------------------
@@ -784,7 +799,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
                       a.tok + fs * SEG_TOK,
                       a.seg_ntok + fs, s_hdc[TOK ? slot : 0][comp][bcol & (HREP - 1)],
                       s_hac[TOK ? slot : 0][comp][bcol & (HREP - 1)],
-                      s_st[TOK ? wave : 0]);
+                      s_st[TOK ? wave : 0], kflags);
         }
       };
       if (PIX && do_dct) {
