@@ -443,7 +443,38 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int se
   // the coefficient variant lists hazard blocks; k_fix_blocks recomputes
   // them in FP64 right after it, on the same stream
   if (mode == 1) HIP_TRY(hipMemsetAsync(b->d_fix_count, 0, sizeof(unsigned), b->stream));
+  // diagnostics (MIJ_K1_WTIME with the diag build): per-wave lifetimes of K1
+  static const bool wtime = getenv("MIJ_K1_WTIME") != nullptr;
+  unsigned long long *d_wt = nullptr;
+  const long long nw = grid * 16;
+  if (wtime && mode == 1) {
+    HIP_TRY(hipMalloc(&d_wt, sizeof(unsigned long long) * 3 * nw));
+    HIP_TRY(hipMemsetAsync(d_wt, 0, sizeof(unsigned long long) * 3 * nw, b->stream));
+    k.wtime = d_wt;
+  }
   HIP_TRY(launch_k1(k, (int)grid, mode, b->stream));
+  if (d_wt) {
+    std::vector<unsigned long long> h(3 * nw);
+    HIP_TRY(hipMemcpyAsync(h.data(), d_wt, sizeof(unsigned long long) * 3 * nw, hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    HIP_TRY(hipFree(d_wt));
+    unsigned long long s0 = ~0ull, e1 = 0, e0 = ~0ull;
+    double sum = 0, smin = 1e30, smax = 0;
+    long long n = 0, tiles = 0;
+    for (long long i = 0; i < nw; i++) {
+      if (!h[3 * i + 1]) continue;
+      const unsigned long long a0 = h[3 * i], a1 = h[3 * i + 1];
+      s0 = std::min(s0, a0); e1 = std::max(e1, a1); e0 = std::min(e0, a1);
+      const double d = (double)(a1 - a0);
+      sum += d; smin = std::min(smin, d); smax = std::max(smax, d); n++; tiles += (long long)h[3 * i + 2];
+    }
+    if (const char *path = getenv("MIJ_K1_WTIME_DUMP")) {  // raw per-wave records
+      if (FILE *fp = fopen(path, "ab")) { fwrite(h.data(), sizeof(unsigned long long), 3 * nw, fp); fclose(fp); }
+    }
+    // s_memrealtime ticks at 100 MHz
+    fprintf(stderr, "K1 waves %lld tiles %lld: span %.1f us, first end %.1f us, wave life mean %.1f min %.1f max %.1f us\n",
+            n, tiles, (e1 - s0) / 100.0, (e0 - s0) / 100.0, sum / n / 100.0, smin / 100.0, smax / 100.0);
+  }
   if (b->timing && mode != 6) HIP_TRY(hipEventRecord(b->ev[1], b->stream));
   if (mode == 1) HIP_TRY(launch_fix_blocks(k, b->stream));
   if (b->timing && mode != 6) HIP_TRY(hipEventRecord(b->ev[2], b->stream));

@@ -91,6 +91,7 @@ struct K1Args {
   uint32_t *hist;           // token mode: per frame [4][257] histograms
   uint32_t *fix_list;       // coefficient mode: blocks (frame * nblk + blk) for k_fix_blocks
   unsigned int *fix_count;  // coefficient mode: length of fix_list
+  unsigned long long *wtime;  // diagnostics only (MIJ_K1_WTIME): per wave start, end, tiles
 };
 // K1 diagnostic switches (timing attribution; outputs are wrong when set)
 constexpr int K1F_NO_LUT = 1, K1F_NO_REPLAY = 2, K1F_NO_COLOUR = 4, K1F_NO_DCT = 8,

@@ -593,6 +593,11 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
   constexpr int HREP = PIX ? 1 : 4;
   __shared__ uint32_t s_hac[TOK ? 2 : 1][2][HREP][256];
   __shared__ uint32_t s_hdc[TOK ? 2 : 1][2][HREP][16];
+  // next unclaimed tile of this workgroup's range: waves claim tiles
+  // dynamically, so waves the SIMD arbiter favours do more of them and the
+  // workgroup's waves finish together (static round-robin left the youngest
+  // wave of each SIMD running alone for the last third of the launch)
+  __shared__ int s_next;
 
   const Tables *__restrict__ T = a.tab;
   // diagnostic switches exist only in the MIJ_K1_DIAG build (make diag): in
@@ -617,6 +622,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
   for (int i = threadIdx.x; i < 128; i += NT) {
     s_fac[i >> 6][i & 63] = T->qfac[i >> 6][i & 63];
   }
+  if (threadIdx.x == 0) s_next = (int)blockIdx.x * a.per_wg + NW;
   __syncthreads();
 
   const int lane = threadIdx.x & 63;
@@ -632,6 +638,10 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
   const int f0 = t0 / G.tiles_per_frame;      // a workgroup spans <= 2 frames
   const int tend = min(ntiles, t0 + a.per_wg);
   int t = t0 + wave;
+#ifdef MIJ_K1_DIAG
+  const unsigned long long w_t0 = __builtin_amdgcn_s_memrealtime();
+  int w_ntiles = 0;
+#endif
   if (t < tend) {
     uint8_t *raw = s_raw[PIX ? wave : 0];
     TilePos p = tile_pos(G, t);
@@ -662,27 +672,33 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
     };
     u4v cnext[PIX ? 1 : 3][2];
     if (!PIX) load_coefs(p, cnext);
-    for (; t < tend; t += NW) {
+    bool first = true;
+    for (;;) {
       TilePos pn = p;
+      // claim the wave's next tile now: the LDS atomic's result is needed only
+      // after the colour stage, when the next tile's DMA goes out
+      int tn = 0;
+      if (lane == 0) tn = atomicAdd(&s_next, 1);
+      tn = __builtin_amdgcn_readfirstlane(tn);
       if (PIX) {
         // ---- 1. colour convert + subsample + stage.  Wait for this tile's
         // DMA: the coefficient variant leaves the previous tile's stores in
         // flight (counted wait); the token variants waited before their first
         // store of the previous tile; the first tile and the diagnostic
         // variants without stores drain everything.
-        if (t == t0 + wave || (kflags & (K1F_NO_DCT | K1F_NO_STORE)))
+        if (first || (kflags & (K1F_NO_DCT | K1F_NO_STORE)))
           dma_wait();
         else if (DEFER)
           dma_wait_behind_stores();
         if (!(kflags & K1F_NO_COLOUR)) colour_stage(raw, L, c4, pr, s_lut, !(kflags & K1F_NO_LUT));
         wave_lds_sync();
         // ---- stream the wave's next tile into the freed raw buffer -----------
-        if (t + NW < tend) {
-          pn = tile_pos(G, t + NW);
+        if (tn < tend) {
+          pn = tile_pos(G, tn);
           issue_tile_dma(a, pn, lane, raw, doff);
         }
-      } else if (t + NW < tend) {
-        pn = tile_pos(G, t + NW);
+      } else if (tn < tend) {
+        pn = tile_pos(G, tn);
       }
 
       // ---- 2. DCT on MFMA, one 16-block N-tile at a time ----------------------
@@ -727,7 +743,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
           pre[PIX ? 0 : nt][0] = cnext[PIX ? 0 : nt][0];
           pre[PIX ? 0 : nt][1] = cnext[PIX ? 0 : nt][1];
         }
-        if (t + NW < tend) load_coefs(pn, cnext);
+        if (tn < tend) load_coefs(pn, cnext);
       }
 
       // ---- 3-4. quantize, replay, store, emit -----------------------------------
@@ -897,9 +913,23 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
         }
       }
       if (PIX) wave_lds_sync();
+#ifdef MIJ_K1_DIAG
+      w_ntiles++;
+#endif
+      if (tn >= tend) break;
       p = pn;
+      t = tn;
+      first = false;
     }
   }
+#ifdef MIJ_K1_DIAG
+  if (a.wtime && lane == 0) {
+    unsigned long long *w = a.wtime + 3 * ((long long)blockIdx.x * NW + wave);
+    w[0] = w_t0;
+    w[1] = __builtin_amdgcn_s_memrealtime();
+    w[2] = (unsigned long long)w_ntiles;
+  }
+#endif
   if (TOK) {  // per-frame histograms of this workgroup
     __syncthreads();
     for (int i = threadIdx.x; i < 2 * 2 * 256; i += NT) {
