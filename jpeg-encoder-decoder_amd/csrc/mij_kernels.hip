@@ -287,6 +287,20 @@ __device__ __forceinline__ float ubyte_f32(uint32_t w) {
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
+// low 16 bits of lo | low 16 bits of hi << 16 (one v_perm_b32)
+__device__ __forceinline__ uint32_t pack_i16x2(int lo, int hi) {
+  return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u);
+}
+
+// a + k in both halves (v_pk_add_f32 with k in an SGPR): the compiler would
+// otherwise split a packed add of a non-inline constant into two VALU adds
+__device__ __forceinline__ f2v pk_add_k(f2v a, float k) {
+  f2v r;
+  const unsigned long long kk = __float_as_uint(k);
+  asm("v_pk_add_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(a), "s"(kk));
+  return r;
+}
+
 // Chroma in "magic" form: x + 1.5*2^23 rounds x to an integer held in the low
 // mantissa bits, so bits(x + MAGIC) - MAGIC_BITS = round(x) and four such bit
 // patterns add as integers.  The chroma expressions carry a -0.5 + 2^-16
@@ -325,15 +339,15 @@ __device__ __forceinline__ void convert4(uint32_t w0, uint32_t w1, uint32_t w2, 
   for (int h = 0; h < 2; h++) {
     dr[h] = fr[h] - fg[h];
     db[h] = fb[h] - fg[h];
-    const f2v yf = __builtin_elementwise_fma((f2v)0.114f, db[h],
-                                             __builtin_elementwise_fma((f2v)0.299f, dr[h], fg[h])) +
-                   (f2v)0.0005f;
-    const f2v cb = __builtin_elementwise_fma((f2v)-0.168736f, dr[h],
-                                             __builtin_elementwise_fma((f2v)0.5f, db[h], (f2v)CH_BIAS)) +
-                   (f2v)MAGIC;
-    const f2v cr = __builtin_elementwise_fma((f2v)-0.081312f, db[h],
-                                             __builtin_elementwise_fma((f2v)0.5f, dr[h], (f2v)CH_BIAS)) +
-                   (f2v)MAGIC;
+    const f2v yf = pk_add_k(__builtin_elementwise_fma((f2v)0.114f, db[h],
+                                                      __builtin_elementwise_fma((f2v)0.299f, dr[h], fg[h])),
+                            0.0005f);
+    const f2v cb = pk_add_k(__builtin_elementwise_fma((f2v)-0.168736f, dr[h],
+                                                      __builtin_elementwise_fma((f2v)0.5f, db[h], (f2v)CH_BIAS)),
+                            MAGIC);
+    const f2v cr = pk_add_k(__builtin_elementwise_fma((f2v)-0.081312f, db[h],
+                                                      __builtin_elementwise_fma((f2v)0.5f, dr[h], (f2v)CH_BIAS)),
+                            MAGIC);
 #pragma unroll
     for (int e = 0; e < 2; e++) {
       // (element copies first: __builtin_bit_cast of a vector element
@@ -781,8 +795,8 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
           u4v s0, s1;
 #pragma unroll
           for (int k = 0; k < 4; k++) {
-            s0[k] = (uint32_t)(uint16_t)o[2 * k] | ((uint32_t)o[2 * k + 1] << 16);
-            s1[k] = (uint32_t)(uint16_t)o[8 + 2 * k] | ((uint32_t)o[9 + 2 * k] << 16);
+            s0[k] = pack_i16x2(o[2 * k], o[2 * k + 1]);
+            s1[k] = pack_i16x2(o[8 + 2 * k], o[9 + 2 * k]);
           }
           if (kflags & K1F_LINEAR_STORE) {  // diagnostics: timing of fully contiguous stores
             const long long b0 = nt < 2 ? blk - bcol : G.nY + (long long)p.ty * mw + p.tx * 8;
@@ -826,7 +840,10 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
           float lc;  // per block: error bound of N in N units
           dct_ntile(nt, acc, lc);
           int o[16];
-          uint32_t hz = 0;  // nonzero iff some coefficient's +-tau interval straddles a boundary
+          // trunc(t - tau) is the output; the lane's sums of trunc(t - tau)
+          // and trunc(t + tau) differ iff some coefficient's +-tau interval
+          // straddles a truncation boundary (each hi >= its lo)
+          int slo = 0, shi = 0;
           if (kflags & K1F_NO_QUANT) {
 #pragma unroll
             for (int k = 0; k < 16; k++) o[k] = acc[k >> 2][k & 3];
@@ -834,18 +851,24 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
 #pragma unroll
           for (int m = 0; m < 4; m++) {
             const float4 fac = *(const float4 *)&s_fac[comp][16 * g + 4 * m];
-            const float fa[4] = {fac.x, fac.y, fac.z, fac.w};
+            const f2v lc2 = {lc, lc};
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-              const float nf = (float)acc[m][r];
-              // tau = fac * lc + 1e-6
-              const float tv = fmaf(fa[r], lc, 1.0e-6f);
-              const int lo = (int)fmaf(nf, fa[r], -tv);
-              const int hi = (int)fmaf(nf, fa[r], tv);
-              o[4 * m + r] = lo;
-              hz |= (uint32_t)(hi ^ lo);
+            for (int h = 0; h < 2; h++) {
+              const f2v fa = h ? f2v{fac.z, fac.w} : f2v{fac.x, fac.y};
+              const f2v nf = {(float)acc[m][2 * h], (float)acc[m][2 * h + 1]};
+              // tau = fac * lc + 1e-6, packed over two coefficients
+              const f2v tv = __builtin_elementwise_fma(fa, lc2, (f2v)1.0e-6f);
+              const f2v lo = __builtin_elementwise_fma(nf, fa, -tv);
+              const f2v hi = __builtin_elementwise_fma(nf, fa, tv);
+              const float lo0 = lo[0], lo1 = lo[1], hi0 = hi[0], hi1 = hi[1];
+              const int l0 = (int)lo0, l1 = (int)lo1;
+              o[4 * m + 2 * h] = l0;
+              o[4 * m + 2 * h + 1] = l1;
+              slo += l0 + l1;
+              shi += (int)hi0 + (int)hi1;
             }
           }
+          const uint32_t hz = (uint32_t)(slo ^ shi);  // nonzero iff a hazard
           {  // z = 0: exact from the pixel sum (fac = 0 above)
             bool tie;
             const int dcv = dc_fast(acc[0][0], 8 * q_dc[comp], s_inv8q[comp], tie);
