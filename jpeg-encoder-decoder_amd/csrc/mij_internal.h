@@ -31,6 +31,8 @@ constexpr int MAX_BLOCK_BITS = 1729;              // 28 DC + 63 * 27 AC bits
 // k_pack assembles a group in LDS windows of PACK_WORDS words; a group wider
 // than one window (only near worst-case entropy) is packed in several passes.
 constexpr int PACK_WORDS = 4096;
+// k_pack_lb: tokens per lane loaded in one batch (16 lanes per segment)
+constexpr int PACK_BATCH = 16;
 // JFIF assembly: scans are written in EMIT_CH-byte chunks by EMIT_SLOTS
 // workgroups per scan
 constexpr int EMIT_CH = 4096;
@@ -97,7 +99,8 @@ struct K1Args {
 constexpr int K1F_NO_LUT = 1, K1F_NO_REPLAY = 2, K1F_NO_COLOUR = 4, K1F_NO_DCT = 8,
               K1F_NO_STORE = 16, K1F_NO_QUANT = 32, K1F_NO_MFMA = 64,
               K1F_LINEAR_STORE = 128, K1F_PLAIN_STORE = 256,
-              K1F_NO_HIST = 512, K1F_NO_TOKSTORE = 1024;
+              K1F_NO_HIST = 512, K1F_NO_TOKSTORE = 1024,
+              K1F_EXTRA_LDS = 2048;
 
 struct EntArgs {
   Geom g;
@@ -124,6 +127,7 @@ struct EntArgs {
   uint32_t *choff;          // per frame [3][emit_chunks]: output offset of each chunk
   unsigned long long *pack_state;  // k_pack_lb: per pack group, flag << 62 | bits
   unsigned int *pack_ticket;       // k_pack_lb: next group to claim
+  unsigned long long *dbg;         // diagnostics only (MIJ_PACK_TIME, diag build)
 };
 
 // EMIT_CH chunks of the largest scan buffer (the per-scan stride of EntArgs::ffc)

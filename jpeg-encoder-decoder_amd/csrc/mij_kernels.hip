@@ -55,6 +55,10 @@ __device__ __forceinline__ uint32_t row_scan16(uint32_t x) {
   x += row_shr0<8>(x);
   return x;
 }
+// lane 15 of each 16-lane row, broadcast to the row (DPP row_newbcast:15)
+__device__ __forceinline__ uint32_t row_last(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x15F, 0xF, 0xF, false);
+}
 // inclusive prefix sum over the wave (row scans + row_bcast:15 / row_bcast:31)
 __device__ __forceinline__ uint32_t wave_scan64(uint32_t x) {
   x = row_scan16(x);
@@ -256,7 +260,7 @@ __device__ __forceinline__ void issue_tile_dma(const K1Args &a, const TilePos &p
   if (on) {
 #pragma unroll
     for (int k = 0; k < DMA_K; k++)
-      asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1"
+      asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1 nt"
                    :
                    : "v"(off), "s"(src + (long long)(2 * k) * a.pitch), "s"(lds0 + 768 * k)
                    : "memory", "m0");
@@ -741,6 +745,12 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
 #pragma unroll
           for (int m = 0; m < 4; m++) {
             const int4 F = s_A[(3 * m + d) * 64 + lane];
+#ifdef MIJ_K1_DIAG
+            if (kflags & K1F_EXTRA_LDS) {  // diagnostics: a second, unused read of the fragment
+              v4i dummy;
+              asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(dummy) : "v"((uint32_t)(uintptr_t)(lds_void_t *)&s_A[(3 * m + d) * 64 + lane]) : "memory");
+            }
+#endif
             const v4i Fv = {F.x, F.y, F.z, F.w};
             const v4i c = d == 0 ? v4i{0, 0, 0, 0} : acc[m] << 7;
             acc[m] = (kflags & K1F_NO_MFMA) ? c + Fv + Bf
@@ -1717,7 +1727,7 @@ __global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
           }
           if (L) put_bits_window(buf, pos, lo_bit, hi_bit, ((e & 0xFFFFu) << cls) | (t >> 16), (int)L);
         }
-        pos0 += __shfl(x, 15, 16);
+        pos0 += row_last(x);
       }
     }
     __syncthreads();

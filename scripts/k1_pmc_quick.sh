@@ -4,8 +4,8 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 out=gpurun_out/k1pmc${TAG:-}; rm -rf $out; mkdir -p $out
-timeout -k 10 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS --kernel-include-regex "mcu_dct<1>" --output-format csv -d $out -o run -- \
-  python3 bench.py --mode dct --steps 2 --warmup 1 --no-cpu-baseline --verify 0 > $out/log 2>&1 || { tail -3 $out/log; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS --kernel-include-regex "${KRE:-mcu_dct<1>}" --output-format csv -d $out -o run -- \
+  python3 bench.py --mode ${MODE:-dct} --steps 2 --warmup 1 --no-cpu-baseline --verify 0 > $out/log 2>&1 || { tail -3 $out/log; exit 1; }
 python3 - $out <<'PY'
 import csv, glob, sys, collections
 pc = collections.defaultdict(dict)
