@@ -507,13 +507,15 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
   *(u4v *)&st[lane][8] = c1;
   // nonzero mask: min(half, 1) per packed int16 pair puts coefficient 2k's
   // flag at bit 2k and 2k+1's at bit 16+2k
+  // (v_pk_min_u16 in asm: the compiler rewrites min(h, 1) into compares and
+  // selects, three times the instructions)
   uint32_t pm = 0;
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     const uint32_t w = k < 4 ? c0[k] : c1[k - 4];
-    us2 h = __builtin_bit_cast(us2, w);
-    h = __builtin_elementwise_min(h, (us2){1, 1});
-    pm |= __builtin_bit_cast(uint32_t, h) << (2 * k);
+    uint32_t h;
+    asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(h) : "v"(w));
+    pm |= h << (2 * k);
   }
   uint32_t m16 = (pm & 0x5555u) | ((pm >> 15) & 0xAAAAu);
   if (g == 0) m16 &= ~1u;  // the DC is not part of the AC run structure
