@@ -80,8 +80,10 @@ enum {
     MIJ_ENODEV = 2,     /* no usable HIP device / runtime */
     MIJ_EHIP = 3,       /* a HIP runtime call failed */
     MIJ_ENOSPC = 4,     /* output capacity too small */
-    MIJ_ETABLE = 5      /* Huffman construction outside the reference's
+    MIJ_ETABLE = 5,     /* Huffman construction outside the reference's
                            defined behaviour (code length >= 32 etc.) */
+    MIJ_EPPM = 6,       /* PPM rejected by the rules of utils/original.c:294-365 */
+    MIJ_EIO = 7         /* file could not be opened, read or written */
 };
 int mij_last_error(void);
 const char *mij_strerror(int code);
@@ -119,6 +121,10 @@ int mij_batch_encode(mij_batch *b, int nframes);     /* full path, async */
  * second pass tokenizes them; fused (set_split(b, 0)) -- K1 emits the symbol
  * tokens directly.  Same output bytes either way. */
 int mij_batch_set_split(mij_batch *b, int on);
+/* input frames in R, G, B byte order (PPM files, brain.c:25-42) instead of the
+ * encoder's B, G, R (encoder.c:133); the channels are swapped inside K1, at no
+ * cost.  Split pipeline only. */
+int mij_batch_set_rgb(mij_batch *b, int on);
 /* fused pipeline only: also keep the coefficient planes (for
  * mij_batch_coefs); the split pipeline always has them */
 int mij_batch_keep_coefs(mij_batch *b, int on);
@@ -155,6 +161,46 @@ int mij_batch_geometry(mij_batch *b, long long *out, int n);
 unsigned long long mij_batch_replays(mij_batch *b);
 /* the batch's hipStream_t, as an opaque pointer */
 void *mij_batch_stream(mij_batch *b);
+
+/* ---- PPM ingest -----------------------------------
+ * Header rules of the reference's reader, utils/original.c:294-365, kept
+ * exactly: "P6" then a newline straight after it; then lines up to the first
+ * one that does not start with '#' (comment lines, :303-316), which must hold
+ * "W H" (sscanf "%d %d", :318); W and H multiples of 16 (:324-328); the depth
+ * read with fscanf("%d\n") -- which also swallows whitespace bytes that begin
+ * the pixel data, so such a file then fails the length check, as in the
+ * reference -- must be 255 (:330-337); the bytes left must be exactly 3*W*H
+ * (:339-344).  Extra rules where the reference is undefined: a line longer
+ * than 1023 bytes or missing its newline is a parse error, W or H <= 0 is
+ * rejected.  Errors: MIJ_EIO (open/read), MIJ_EPPM (rules above). */
+int mij_ppm_header(const char *path, int *w, int *h, long long *data_offset);
+/* pixels of a PPM into dst (rows dst_pitch bytes apart); to_bgr != 0 swaps
+ * to the encoder's B, G, R order (what rgb_to_dct / mij_encode expect) */
+int mij_ppm_read(const char *path, uint8_t *dst, size_t cap, int dst_pitch, int to_bgr);
+
+/* ---- streaming encoder: PPM files -> .jpg files ----------------------------
+ * Frames of one geometry flow through two batches in ping-pong: host threads
+ * read chunk k+1 into pinned memory (no channel swap: K1 reads RGB) while the
+ * GPU encodes chunk k; each chunk is uploaded, encoded, its lengths fetched,
+ * its JPEG bytes copied back and written by host threads, all overlapped with
+ * the other batch's chunk.  Output bytes are those of mij_encode /
+ * write_jpg for the same image. */
+typedef struct mij_stream mij_stream;
+mij_stream *mij_stream_create(int device, int width, int height, int chunk_frames,
+                              int quality, int host_threads);
+void mij_stream_destroy(mij_stream *s);
+/* encode n PPM files (all width x height) to out_paths; stops at the first
+ * failing file (its index in *failed, -1 if none) */
+int mij_stream_encode_files(mij_stream *s, const char *const *in_paths,
+                            const char *const *out_paths, int n, int *failed);
+/* in-memory variant: n RGB frames (packed rows) -> outs[i] (caps[i] bytes),
+ * lengths in lens[i] */
+int mij_stream_encode_frames(mij_stream *s, const uint8_t *const *rgb, int n,
+                             uint8_t *const *outs, const size_t *caps, size_t *lens);
+/* seconds of the last encode_*: {wall, host read, host write, gpu (events),
+ * frames, bytes in, bytes out} */
+#define MIJ_STREAM_NSTATS 7
+int mij_stream_stats(mij_stream *s, double *out, int n);
 
 /* ---- one large frame over several ranks -------
  * Rank r encodes band r -- an MCU-row range [row0, row0 + rows) with rows a

@@ -11,6 +11,7 @@
 #include <mutex>
 #include <vector>
 
+#include "mij_host.h"
 #include "mij_internal.h"
 #include "mijpeg.h"
 
@@ -41,16 +42,29 @@ using namespace mij;
 // ---------------------------------------------------------------------------
 static thread_local int g_err = MIJ_OK;
 
-static int fail(int code, const char *fmt, ...) {
+static int vfail(int code, const char *fmt, va_list ap) {
   g_err = code;
-  va_list ap;
-  va_start(ap, fmt);
   fprintf(stderr, "mijpeg: ");
   vfprintf(stderr, fmt, ap);
   fprintf(stderr, "\n");
+  return code;
+}
+static int fail(int code, const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vfail(code, fmt, ap);
   va_end(ap);
   return code;
 }
+// for the other host translation units (mij_stream.hip)
+int mij_fail(int code, const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vfail(code, fmt, ap);
+  va_end(ap);
+  return code;
+}
+void mij_clear_error() { g_err = MIJ_OK; }
 
 #define HIP_TRY(x)                                                          \
   do {                                                                      \
@@ -69,6 +83,8 @@ extern "C" const char *mij_strerror(int code) {
     case MIJ_EHIP: return "HIP runtime error";
     case MIJ_ENOSPC: return "output buffer too small";
     case MIJ_ETABLE: return "Huffman table outside the reference's defined behaviour";
+    case MIJ_EPPM: return "PPM rejected (utils/original.c read_ppm rules)";
+    case MIJ_EIO: return "file I/O error";
   }
   return "unknown error";
 }
@@ -238,6 +254,7 @@ struct mij_batch {
   size_t stage_words = 0;
   std::vector<unsigned long long> band_words;  // per frame x 3: packed words after mij_band_pack
   bool keep_coefs = false;  // encode also writes coefficient planes
+  bool rgb = false;         // input frames in R, G, B byte order (PPM) instead of B, G, R
   bool split = true;        // K1 writes coefficients, a second pass tokenizes
   bool timing = false;
   static constexpr int HIST = 64;
@@ -430,6 +447,7 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int se
   k.hist = b->d_hist;
   k.fix_list = b->d_fix;
   k.fix_count = b->d_fix_count;
+  k.rgb = b->rgb && mode == 1;
   static const int k1_flags = getenv("MIJ_K1_FLAGS") ? atoi(getenv("MIJ_K1_FLAGS")) : 0;
   k.flags = k1_flags;
   const long long ntiles = (long long)nframes * b->g.tiles_per_frame;
@@ -501,6 +519,7 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
 }
 
 static int encode_frames(mij_batch *b, int nframes) {
+  if (b->rgb && !b->split) return fail(MIJ_EINVAL, "encode: RGB input needs the split pipeline");
   HIP_TRY(hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * nframes * 4 * 257, b->stream));
   HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * nframes, b->stream));
   if (b->timing) HIP_TRY(hipEventRecord(b->ev[0], b->stream));
@@ -530,6 +549,36 @@ extern "C" int mij_batch_encode(mij_batch *b, int nframes) {
 extern "C" int mij_batch_keep_coefs(mij_batch *b, int on) {
   if (!b) return fail(MIJ_EINVAL, "keep_coefs: null batch");
   b->keep_coefs = on != 0;
+  return MIJ_OK;
+}
+
+extern "C" int mij_batch_set_rgb(mij_batch *b, int on) {
+  if (!b) return fail(MIJ_EINVAL, "set_rgb: null batch");
+  b->rgb = on != 0;
+  return MIJ_OK;
+}
+
+// ---- asynchronous host transfers for the streaming engine (mij_stream.hip):
+// queued on the batch stream, no synchronisation
+int mij_batch_upload_async(mij_batch *b, const uint8_t *host, int nframes) {
+  if (!b || !host || nframes < 1 || nframes > b->cap || !b->own_in)
+    return fail(MIJ_EINVAL, "upload_async: bad args");
+  HIP_TRY(hipSetDevice(b->dev));
+  HIP_TRY(hipMemcpyAsync(b->d_in, host, (size_t)nframes * b->in_fs, hipMemcpyHostToDevice, b->stream));
+  return MIJ_OK;
+}
+int mij_batch_lengths_async(mij_batch *b, uint64_t *h_len, int *h_err, int nframes) {
+  if (!b || nframes < 1 || nframes > b->cap) return fail(MIJ_EINVAL, "lengths_async: bad args");
+  HIP_TRY(hipSetDevice(b->dev));
+  HIP_TRY(hipMemcpyAsync(h_len, b->d_out_len, sizeof(uint64_t) * nframes, hipMemcpyDeviceToHost, b->stream));
+  HIP_TRY(hipMemcpyAsync(h_err, b->d_err, sizeof(int) * nframes, hipMemcpyDeviceToHost, b->stream));
+  return MIJ_OK;
+}
+int mij_batch_output_async(mij_batch *b, int frame, uint8_t *dst, size_t n) {
+  if (!b || frame < 0 || frame >= b->cap || n > (size_t)b->g.out_cap)
+    return fail(MIJ_EINVAL, "output_async: bad args");
+  HIP_TRY(hipSetDevice(b->dev));
+  HIP_TRY(hipMemcpyAsync(dst, b->d_out + (long long)frame * b->g.out_cap, n, hipMemcpyDeviceToHost, b->stream));
   return MIJ_OK;
 }
 

@@ -1,0 +1,16 @@
+// mij_host.h -- host-side helpers shared between the translation units of
+// libmijpeg.so (mij_api.hip <-> mij_stream.hip).  Not a public header.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mijpeg.h"
+
+// error state of the C ABI (mij_last_error): set and print like the API does
+int mij_fail(int code, const char *fmt, ...);
+void mij_clear_error();
+
+// asynchronous transfers on the batch's stream (no synchronisation)
+int mij_batch_upload_async(mij_batch *b, const uint8_t *host, int nframes);
+int mij_batch_lengths_async(mij_batch *b, uint64_t *h_len, int *h_err, int nframes);
+int mij_batch_output_async(mij_batch *b, int frame, uint8_t *dst, size_t n);

@@ -94,6 +94,7 @@ struct K1Args {
   uint32_t *fix_list;       // coefficient mode: blocks (frame * nblk + blk) for k_fix_blocks
   unsigned int *fix_count;  // coefficient mode: length of fix_list
   unsigned long long *wtime;  // diagnostics only (MIJ_K1_WTIME): per wave start, end, tiles
+  int rgb;                  // input bytes in R, G, B order (PPM) instead of B, G, R
 };
 // K1 diagnostic switches (timing attribution; outputs are wrong when set)
 constexpr int K1F_NO_LUT = 1, K1F_NO_REPLAY = 2, K1F_NO_COLOUR = 4, K1F_NO_DCT = 8,

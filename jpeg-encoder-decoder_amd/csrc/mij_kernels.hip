@@ -333,11 +333,15 @@ struct Run4 {
   bool cc, cy;
 };
 
+template <bool RGB>
 __device__ __forceinline__ void convert4(uint32_t w0, uint32_t w1, uint32_t w2, Run4 &o) {
   // BGR of pixel p: w0 = B0 G0 R0 B1, w1 = G1 R1 B2 G2, w2 = R2 B3 G3 R3
-  const f2v fb[2] = {{ubyte_f32<0>(w0), ubyte_f32<3>(w0)}, {ubyte_f32<2>(w1), ubyte_f32<1>(w2)}};
+  // (RGB input -- PPM order -- swaps the first and third byte of each pixel)
+  const f2v f0[2] = {{ubyte_f32<0>(w0), ubyte_f32<3>(w0)}, {ubyte_f32<2>(w1), ubyte_f32<1>(w2)}};
   const f2v fg[2] = {{ubyte_f32<1>(w0), ubyte_f32<0>(w1)}, {ubyte_f32<3>(w1), ubyte_f32<2>(w2)}};
-  const f2v fr[2] = {{ubyte_f32<2>(w0), ubyte_f32<1>(w1)}, {ubyte_f32<0>(w2), ubyte_f32<3>(w2)}};
+  const f2v f2[2] = {{ubyte_f32<2>(w0), ubyte_f32<1>(w1)}, {ubyte_f32<0>(w2), ubyte_f32<3>(w2)}};
+  const f2v(&fb)[2] = RGB ? f2 : f0;
+  const f2v(&fr)[2] = RGB ? f0 : f2;
   f2v dr[2], db[2];
 #pragma unroll
   for (int h = 0; h < 2; h++) {
@@ -374,10 +378,13 @@ __device__ __forceinline__ void convert4(uint32_t w0, uint32_t w1, uint32_t w2, 
 // Rare path: the Y corrections of a run as a packed byte-wise subtrahend.
 // Only the pixel slots that hold an exact-integer Y in some lane pay for the
 // bitmap read (one wave-uniform branch per slot).
+template <bool RGB>
 __device__ __forceinline__ uint32_t y_fix(uint32_t w0, uint32_t w1, uint32_t w2, const float (&fy)[4],
                                           const uint32_t *__restrict__ lut) {
   const uint32_t Gv[4] = {(w0 >> 8) & 255, w1 & 255, w1 >> 24, (w2 >> 16) & 255};
-  const uint32_t Rv[4] = {(w0 >> 16) & 255, (w1 >> 8) & 255, w2 & 255, w2 >> 24};
+  const uint32_t B0[4] = {w0 & 255, w0 >> 24, (w1 >> 16) & 255, (w2 >> 8) & 255};
+  const uint32_t R0[4] = {(w0 >> 16) & 255, (w1 >> 8) & 255, w2 & 255, w2 >> 24};
+  const uint32_t(&Rv)[4] = RGB ? B0 : R0;
   uint32_t corr = 0;
 #pragma unroll
   for (int p = 0; p < 4; p++) {
@@ -392,12 +399,15 @@ __device__ __forceinline__ uint32_t y_fix(uint32_t w0, uint32_t w1, uint32_t w2,
 }
 
 // Rare path: Cb / Cr corrections (0/1 per pixel) of a run.
+template <bool RGB>
 __device__ __forceinline__ void chroma_fix(uint32_t w0, uint32_t w1, uint32_t w2,
                                            const uint32_t *__restrict__ lut, uint32_t (&cbc)[4],
                                            uint32_t (&crc)[4]) {
-  const uint32_t Bv[4] = {w0 & 255, w0 >> 24, (w1 >> 16) & 255, (w2 >> 8) & 255};
+  const uint32_t B0[4] = {w0 & 255, w0 >> 24, (w1 >> 16) & 255, (w2 >> 8) & 255};
   const uint32_t Gv[4] = {(w0 >> 8) & 255, w1 & 255, w1 >> 24, (w2 >> 16) & 255};
-  const uint32_t Rv[4] = {(w0 >> 16) & 255, (w1 >> 8) & 255, w2 & 255, w2 >> 24};
+  const uint32_t R0[4] = {(w0 >> 16) & 255, (w1 >> 8) & 255, w2 & 255, w2 >> 24};
+  const uint32_t(&Bv)[4] = RGB ? R0 : B0;
+  const uint32_t(&Rv)[4] = RGB ? B0 : R0;
 #pragma unroll
   for (int p = 0; p < 4; p++) {
     const uint32_t wb = lut[LUT_WORDS + ((Gv[p] << 2) | (Bv[p] >> 6))];
@@ -424,6 +434,7 @@ __device__ __forceinline__ uint32_t chroma_pair(const uint32_t (&r0)[4], const u
   return s0 | (s1 << 8);
 }
 
+template <bool RGB>
 __device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int c4, int pr,
                                              const uint32_t *__restrict__ lut, bool use_lut) {
   // all 8 row pieces of this lane up front: the exception branches below
@@ -445,7 +456,7 @@ __device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int
     uint32_t *Yd[2];
 #pragma unroll
     for (int dy = 0; dy < 2; dy++) {
-      convert4(w[it][dy][0], w[it][dy][1], w[it][dy][2], r[dy]);
+      convert4<RGB>(w[it][dy][0], w[it][dy][1], w[it][dy][2], r[dy]);
       const int yrow = 2 * rp + dy;  // 0..15
       const int by = yrow >> 3, bx = c4 >> 1;
       Yd[dy] = (uint32_t *)(L + (by * 16 + bx) * LDS_BLK + (yrow & 7) * 8 + (c4 & 1) * 4);
@@ -460,13 +471,13 @@ __device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int
 #pragma unroll
     for (int dy = 0; dy < 2; dy++)
       if (__ballot(r[dy].cy)) {
-        const uint32_t corr = y_fix(w[it][dy][0], w[it][dy][1], w[it][dy][2], r[dy].fy, lut);
+        const uint32_t corr = y_fix<RGB>(w[it][dy][0], w[it][dy][1], w[it][dy][2], r[dy].fy, lut);
         if (corr) *Yd[dy] = py[dy] - corr;  // no borrows: a corrected Y is >= 1
       }
     if (__ballot(r[0].cc | r[1].cc)) {
       uint32_t cbc[2][4], crc[2][4];
 #pragma unroll
-      for (int dy = 0; dy < 2; dy++) chroma_fix(w[it][dy][0], w[it][dy][1], w[it][dy][2], lut, cbc[dy], crc[dy]);
+      for (int dy = 0; dy < 2; dy++) chroma_fix<RGB>(w[it][dy][0], w[it][dy][1], w[it][dy][2], lut, cbc[dy], crc[dy]);
       const uint32_t nb0 = cbc[0][0] + cbc[0][1] + cbc[1][0] + cbc[1][1];
       const uint32_t nb1 = cbc[0][2] + cbc[0][3] + cbc[1][2] + cbc[1][3];
       const uint32_t nr0 = crc[0][0] + crc[0][1] + crc[1][0] + crc[1][1];
@@ -581,23 +592,25 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
 constexpr int K1M_COEF_OUT = 1;  // write zigzag coefficient planes
 constexpr int K1M_TOK_OUT = 2;   // write per-segment token streams + histograms
 constexpr int K1M_COEF_IN = 4;   // read coefficient planes (DC differences) instead of pixels
+constexpr int K1M_RGB = 8;       // pixels in RGB order (PPM) instead of BGR (encoder.c:133)
 
 // Waves per workgroup: the coefficient-only variant runs one 12-wave
 // workgroup per CU (3 waves per SIMD: 120 KB of per-wave tile buffers + the
 // shared tables fit the 160 KB LDS, <= 168 VGPRs); the token variants carry
 // per-wave token staging and run 4-wave workgroups, two per CU.
 template <int MODE>
-constexpr int k1_waves() { return MODE == K1M_COEF_OUT ? 12 : 4; }
+constexpr int k1_waves() { return (MODE & ~K1M_RGB) == K1M_COEF_OUT ? 12 : 4; }
 
 template <int MODE>
-__global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2) void k_mcu_dct(K1Args a) {
+__global__ __launch_bounds__(64 * k1_waves<MODE>(), (MODE & ~K1M_RGB) == K1M_COEF_OUT ? 1 : 2) void k_mcu_dct(K1Args a) {
   constexpr bool PIX = !(MODE & K1M_COEF_IN);
   constexpr bool TOK = MODE & K1M_TOK_OUT;
   constexpr int NW = k1_waves<MODE>();
   constexpr int NT = 64 * NW;  // threads per workgroup
   // coefficient variant: FP64 replays are deferred to k_fix_blocks; the
   // token variants replay in place (their tokens are emitted here)
-  constexpr bool DEFER = MODE == K1M_COEF_OUT;
+  constexpr bool DEFER = (MODE & ~K1M_RGB) == K1M_COEF_OUT;
+  constexpr bool RGB = MODE & K1M_RGB;
   __shared__ __attribute__((aligned(16))) uint8_t s_raw[PIX ? NW : 1][TILE_RAW];
   __shared__ __attribute__((aligned(16))) uint8_t s_tile[PIX ? NW : 1][LDS_WAVE];
   __shared__ __attribute__((aligned(16))) int4 s_A[PIX ? 12 * 64 : 1];
@@ -710,7 +723,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
           dma_wait();
         else if (DEFER)
           dma_wait_behind_stores();
-        if (!(kflags & K1F_NO_COLOUR)) colour_stage(raw, L, c4, pr, s_lut, !(kflags & K1F_NO_LUT));
+        if (!(kflags & K1F_NO_COLOUR)) colour_stage<RGB>(raw, L, c4, pr, s_lut, !(kflags & K1F_NO_LUT));
         wave_lds_sync();
         // ---- stream the wave's next tile into the freed raw buffer -----------
         if (tn < tend) {
@@ -996,21 +1009,22 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), MODE == K1M_COEF_OUT ? 1 : 2
 // listed block: lane l stages pixel (l & 7, l >> 3), then computes zigzag
 // coefficient l.  Persistent grid over the device-side list length.
 // ===========================================================================
-__device__ __forceinline__ int y_ref(const uint8_t *px) {  // px = B, G, R
-  const double y = __dadd_rn(__dadd_rn(__dmul_rn(0.299, (double)px[2]), __dmul_rn(0.587, (double)px[1])),
-                             __dmul_rn(0.114, (double)px[0]));
+// px = B, G, R (ib = 0, ir = 2) or R, G, B (ib = 2, ir = 0)
+__device__ __forceinline__ int y_ref(const uint8_t *px, int ib, int ir) {
+  const double y = __dadd_rn(__dadd_rn(__dmul_rn(0.299, (double)px[ir]), __dmul_rn(0.587, (double)px[1])),
+                             __dmul_rn(0.114, (double)px[ib]));
   return (int)(uint8_t)(int)y;
 }
-__device__ __forceinline__ int cb_ref(const uint8_t *px) {
-  const double v = __dadd_rn(__dadd_rn(__dadd_rn(128.0, -__dmul_rn(0.168736, (double)px[2])),
+__device__ __forceinline__ int cb_ref(const uint8_t *px, int ib, int ir) {
+  const double v = __dadd_rn(__dadd_rn(__dadd_rn(128.0, -__dmul_rn(0.168736, (double)px[ir])),
                                        -__dmul_rn(0.331264, (double)px[1])),
-                             __dmul_rn(0.5, (double)px[0]));
+                             __dmul_rn(0.5, (double)px[ib]));
   return (int)(uint8_t)(int)v;
 }
-__device__ __forceinline__ int cr_ref(const uint8_t *px) {
-  const double v = __dadd_rn(__dadd_rn(__dadd_rn(128.0, __dmul_rn(0.5, (double)px[2])),
+__device__ __forceinline__ int cr_ref(const uint8_t *px, int ib, int ir) {
+  const double v = __dadd_rn(__dadd_rn(__dadd_rn(128.0, __dmul_rn(0.5, (double)px[ir])),
                                        -__dmul_rn(0.418688, (double)px[1])),
-                             -__dmul_rn(0.081312, (double)px[0]));
+                             -__dmul_rn(0.081312, (double)px[ib]));
   return (int)(uint8_t)(int)v;
 }
 
@@ -1030,6 +1044,7 @@ __global__ __launch_bounds__(256) void k_fix_blocks(K1Args a) {
   const int x = lane & 7, y = lane >> 3;
   // lane z's output coefficient: zigzag z = frequency (v, u) (encoder.c:38-46)
   const int rz = c_zigzag[lane], v = rz >> 3, u = rz & 7;
+  const int ib = a.rgb ? 2 : 0, ir = 2 - ib;
   for (unsigned e = blockIdx.x * 4 + wave; e < n; e += gridDim.x * 4) {
     const uint32_t id = a.fix_list[e];
     const int f = (int)(id / (uint32_t)G.nblk), blk = (int)(id - (uint32_t)f * (uint32_t)G.nblk);
@@ -1038,7 +1053,7 @@ __global__ __launch_bounds__(256) void k_fix_blocks(K1Args a) {
     if (blk < G.nY) {  // lane = pixel (x, y) of the block
       comp = 0;
       const int bx = blk % bw, by = blk / bw;
-      pv = y_ref(img + (long long)(8 * by + y) * a.pitch + (8 * bx + x) * 3);
+      pv = y_ref(img + (long long)(8 * by + y) * a.pitch + (8 * bx + x) * 3, ib, ir);
     } else {
       comp = 1;
       const int c = blk - G.nY, cr = c >= G.nC, m = cr ? c - G.nC : c;
@@ -1048,7 +1063,7 @@ __global__ __launch_bounds__(256) void k_fix_blocks(K1Args a) {
       for (int dy = 0; dy < 2; dy++)
         for (int dx = 0; dx < 2; dx++) {
           const uint8_t *px = q + (long long)dy * a.pitch + dx * 3;
-          sum += cr ? cr_ref(px) : cb_ref(px);
+          sum += cr ? cr_ref(px, ib, ir) : cb_ref(px, ib, ir);
         }
       pv = sum / 4;
     }
@@ -2052,7 +2067,10 @@ hipError_t launch_colour_lut(uint32_t *lut, hipStream_t s) {
 hipError_t launch_k1(const K1Args &a, int grid, int mode, hipStream_t s) {
   switch (mode) {
     case K1M_COEF_OUT:
-      hipLaunchKernelGGL((k_mcu_dct<K1M_COEF_OUT>), dim3(grid), dim3(64 * k1_waves<K1M_COEF_OUT>()), 0, s, a);
+      if (a.rgb)
+        hipLaunchKernelGGL((k_mcu_dct<K1M_COEF_OUT | K1M_RGB>), dim3(grid), dim3(64 * k1_waves<K1M_COEF_OUT>()), 0, s, a);
+      else
+        hipLaunchKernelGGL((k_mcu_dct<K1M_COEF_OUT>), dim3(grid), dim3(64 * k1_waves<K1M_COEF_OUT>()), 0, s, a);
       break;
     case K1M_TOK_OUT: hipLaunchKernelGGL((k_mcu_dct<K1M_TOK_OUT>), dim3(grid), dim3(256), 0, s, a); break;
     case K1M_COEF_OUT | K1M_TOK_OUT:

@@ -1,0 +1,353 @@
+// mij_stream.hip -- PPM ingest and the streaming encoder (host code of
+// libmijpeg.so).
+//
+// * mij_ppm_header / mij_ppm_read: the reference's PPM reader
+//   (utils/original.c:294-365) restated with its acceptance rules intact.
+// * mij_stream_*: PPM files (or host frames) -> JPEG files (or host buffers)
+//   through two device batches used in ping-pong.  Chunk k+1 is read into
+//   pinned memory by host threads while the GPU encodes chunk k; every chunk
+//   is uploaded, encoded, its lengths fetched, its bytes copied back and
+//   written out by host threads, overlapped with the other batch's chunk.
+//   Frames stay in PPM byte order (R, G, B): K1 swaps channels as it loads.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <functional>
+#include <thread>
+#include <vector>
+
+#include "mij_host.h"
+
+// ---------------------------------------------------------------------------
+// PPM header, utils/original.c:294-365
+// ---------------------------------------------------------------------------
+// On success the stream is positioned at the first pixel byte.
+static int ppm_parse(FILE *f, const char *path, int *w, int *h, long long *off) {
+  // :296-300 magic number; :302-303 a newline right after it
+  if (fgetc(f) != 'P' || fgetc(f) != '6')
+    return mij_fail(MIJ_EPPM, "%s: Could not find magic number for this PPM!", path);
+  if (fgetc(f) != '\n') return mij_fail(MIJ_EPPM, "%s: Could not parse the PPM file properly", path);
+  // :305-316 lines until the first one that is not a '#' comment (the
+  // reference's unbounded line loop is bounded here: 1023 bytes and a
+  // newline before EOF, otherwise a parse error)
+  char buf[1024];
+  for (;;) {
+    int n = 0, c;
+    while ((c = fgetc(f)) != '\n') {
+      if (c == EOF || n == 1023) return mij_fail(MIJ_EPPM, "%s: Could not parse the PPM file properly", path);
+      buf[n++] = (char)c;
+    }
+    buf[n] = '\0';
+    if (buf[0] != '#') break;
+  }
+  int W = 0, H = 0, depth = 0;
+  if (sscanf(buf, "%d %d\n", &W, &H) != 2)  // :318
+    return mij_fail(MIJ_EPPM, "%s: Could not parse the PPM file properly", path);
+  if (W % 16 != 0 || H % 16 != 0)  // :324-328
+    return mij_fail(MIJ_EPPM, "%s: Only pictures with dimensions which are multiples of 16 are supported!", path);
+  // :330-331 -- "%d\n": the newline directive skips every whitespace byte,
+  // including leading pixel bytes 0x09-0x0d / 0x20 (the length check below
+  // then rejects the file, as the reference does)
+  if (fscanf(f, "%d\n", &depth) != 1) return mij_fail(MIJ_EPPM, "%s: Could not parse the PPM file properly", path);
+  if (depth != 255)  // :333-337
+    return mij_fail(MIJ_EPPM, "%s: For simplicity, only a bit-depth of 256 is supported!", path);
+  // :339-344 the rest of the file is exactly the pixels
+  const long pos = ftell(f);
+  if (pos < 0 || fseek(f, 0L, SEEK_END) != 0) return mij_fail(MIJ_EIO, "%s: cannot seek", path);
+  const long end = ftell(f);
+  if (fseek(f, pos, SEEK_SET) != 0) return mij_fail(MIJ_EIO, "%s: cannot seek", path);
+  if ((long long)(end - pos) != 3LL * W * H)
+    return mij_fail(MIJ_EPPM, "%s: Could not parse the PPM file properly", path);
+  if (W <= 0 || H <= 0) return mij_fail(MIJ_EINVAL, "%s: empty image %dx%d", path, W, H);
+  *w = W;
+  *h = H;
+  *off = pos;
+  return MIJ_OK;
+}
+
+extern "C" int mij_ppm_header(const char *path, int *w, int *h, long long *data_offset) {
+  if (!path || !w || !h) return mij_fail(MIJ_EINVAL, "ppm_header: null argument");
+  FILE *f = fopen(path, "rb");
+  if (!f) return mij_fail(MIJ_EIO, "Cannot open file '%s'!", path);
+  long long off = 0;
+  const int rc = ppm_parse(f, path, w, h, &off);
+  fclose(f);
+  if (rc) return rc;
+  if (data_offset) *data_offset = off;
+  mij_clear_error();
+  return MIJ_OK;
+}
+
+static void swap_rb(uint8_t *row, int w) {
+  for (int x = 0; x < w; x++) std::swap(row[3 * x], row[3 * x + 2]);
+}
+
+// reads one PPM into dst; expect_w/h > 0 also checks the geometry
+static int ppm_load(const char *path, uint8_t *dst, size_t cap, int pitch, int to_bgr, int expect_w,
+                    int expect_h) {
+  FILE *f = fopen(path, "rb");
+  if (!f) return mij_fail(MIJ_EIO, "Cannot open file '%s'!", path);
+  int w = 0, h = 0;
+  long long off = 0;
+  int rc = ppm_parse(f, path, &w, &h, &off);
+  if (!rc && expect_w > 0 && (w != expect_w || h != expect_h))
+    rc = mij_fail(MIJ_EINVAL, "%s: %dx%d, the stream encodes %dx%d", path, w, h, expect_w, expect_h);
+  if (!rc && (pitch < 3 * w || (size_t)(h - 1) * pitch + 3 * (size_t)w > cap))
+    rc = mij_fail(MIJ_ENOSPC, "%s: destination too small", path);
+  if (!rc) {
+    if (pitch == 3 * w) {
+      if (fread(dst, 1, (size_t)3 * w * h, f) != (size_t)3 * w * h) rc = mij_fail(MIJ_EIO, "%s: short read", path);
+    } else {
+      for (int y = 0; y < h && !rc; y++)
+        if (fread(dst + (size_t)y * pitch, 1, (size_t)3 * w, f) != (size_t)3 * w)
+          rc = mij_fail(MIJ_EIO, "%s: short read", path);
+    }
+  }
+  fclose(f);
+  if (!rc && to_bgr)
+    for (int y = 0; y < h; y++) swap_rb(dst + (size_t)y * pitch, w);
+  return rc;
+}
+
+extern "C" int mij_ppm_read(const char *path, uint8_t *dst, size_t cap, int dst_pitch, int to_bgr) {
+  if (!path || !dst) return mij_fail(MIJ_EINVAL, "ppm_read: null argument");
+  const int rc = ppm_load(path, dst, cap, dst_pitch, to_bgr, 0, 0);
+  if (!rc) mij_clear_error();
+  return rc;
+}
+
+// ---------------------------------------------------------------------------
+// streaming encoder
+// ---------------------------------------------------------------------------
+#define S_TRY(x)                                                              \
+  do {                                                                        \
+    hipError_t e_ = (x);                                                      \
+    if (e_ != hipSuccess)                                                     \
+      return mij_fail(MIJ_EHIP, "%s: %s", #x, hipGetErrorString(e_));         \
+  } while (0)
+
+struct mij_stream {
+  int dev = 0, w = 0, h = 0, chunk = 0, threads = 1;
+  size_t fbytes = 0;
+  mij_batch *b[2] = {nullptr, nullptr};
+  hipStream_t st[2] = {nullptr, nullptr};
+  uint8_t *h_in[2] = {nullptr, nullptr};
+  uint64_t *h_len[2] = {nullptr, nullptr};
+  int *h_err[2] = {nullptr, nullptr};
+  uint8_t *h_out[2] = {nullptr, nullptr};
+  size_t h_out_cap[2] = {0, 0};
+  std::vector<size_t> off[2];
+  hipEvent_t ev_len[2] = {}, ev_out[2] = {}, ev_t0[2] = {}, ev_t1[2] = {};
+  double stats[MIJ_STREAM_NSTATS] = {};
+};
+
+static void stream_free(mij_stream *s) {
+  if (!s) return;
+  hipSetDevice(s->dev);
+  for (int i = 0; i < 2; i++) {
+    if (s->st[i]) hipStreamSynchronize(s->st[i]);
+    if (s->b[i]) mij_batch_destroy(s->b[i]);
+    if (s->h_in[i]) hipHostFree(s->h_in[i]);
+    if (s->h_len[i]) hipHostFree(s->h_len[i]);
+    if (s->h_err[i]) hipHostFree(s->h_err[i]);
+    if (s->h_out[i]) hipHostFree(s->h_out[i]);
+    for (hipEvent_t e : {s->ev_len[i], s->ev_out[i], s->ev_t0[i], s->ev_t1[i]})
+      if (e) hipEventDestroy(e);
+  }
+  delete s;
+}
+
+static int stream_init(mij_stream *s, int device, int w, int h, int chunk, int quality, int threads) {
+  s->dev = device;
+  s->w = w;
+  s->h = h;
+  s->chunk = chunk;
+  s->threads = threads > 0 ? threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  s->fbytes = (size_t)3 * w * h;
+  for (int i = 0; i < 2; i++) {
+    s->b[i] = mij_batch_create(device, w, h, chunk, quality);
+    if (!s->b[i]) return mij_last_error();
+    if (mij_batch_set_rgb(s->b[i], 1)) return mij_last_error();
+    s->st[i] = (hipStream_t)mij_batch_stream(s->b[i]);
+  }
+  S_TRY(hipSetDevice(device));
+  for (int i = 0; i < 2; i++) {
+    S_TRY(hipHostMalloc((void **)&s->h_in[i], s->fbytes * chunk, hipHostMallocDefault));
+    S_TRY(hipHostMalloc((void **)&s->h_len[i], sizeof(uint64_t) * chunk, hipHostMallocDefault));
+    S_TRY(hipHostMalloc((void **)&s->h_err[i], sizeof(int) * chunk, hipHostMallocDefault));
+    s->h_out_cap[i] = std::max<size_t>(1 << 20, s->fbytes / 4 * chunk);  // grows on demand
+    S_TRY(hipHostMalloc((void **)&s->h_out[i], s->h_out_cap[i], hipHostMallocDefault));
+    s->off[i].assign(chunk + 1, 0);
+    for (hipEvent_t *e : {&s->ev_len[i], &s->ev_out[i], &s->ev_t0[i], &s->ev_t1[i]}) S_TRY(hipEventCreate(e));
+  }
+  return MIJ_OK;
+}
+
+extern "C" mij_stream *mij_stream_create(int device, int width, int height, int chunk_frames,
+                                         int quality, int host_threads) {
+  if (width <= 0 || height <= 0 || width % 16 || height % 16 || chunk_frames < 1 || quality < 1 ||
+      quality > 100) {
+    mij_fail(MIJ_EINVAL, "stream_create: bad geometry %dx%d, chunk %d or quality %d", width, height,
+             chunk_frames, quality);
+    return nullptr;
+  }
+  mij_stream *s = new mij_stream;
+  if (stream_init(s, device, width, height, chunk_frames, quality, host_threads)) {
+    stream_free(s);
+    return nullptr;
+  }
+  mij_clear_error();
+  return s;
+}
+
+extern "C" void mij_stream_destroy(mij_stream *s) { stream_free(s); }
+
+extern "C" int mij_stream_stats(mij_stream *s, double *out, int n) {
+  if (!s || !out) return mij_fail(MIJ_EINVAL, "stream_stats: null argument");
+  for (int i = 0; i < n && i < MIJ_STREAM_NSTATS; i++) out[i] = s->stats[i];
+  return MIJ_OK;
+}
+
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// runs job(i) for i in [0, n) on up to `threads` host threads; returns the
+// first nonzero result (by index) or 0
+static int parallel_for(int n, int threads, const std::function<int(int)> &job, int *failed) {
+  std::vector<int> rc(n, 0);
+  std::atomic<int> next{0};
+  auto worker = [&]() {
+    for (int i; (i = next.fetch_add(1)) < n;) rc[i] = job(i);
+  };
+  const int nt = std::min(n, threads);
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; t++) pool.emplace_back(worker);
+  worker();
+  for (auto &t : pool) t.join();
+  for (int i = 0; i < n; i++)
+    if (rc[i]) {
+      if (failed) *failed = i;
+      return rc[i];
+    }
+  return 0;
+}
+
+// fill(i, dst): frame i into pinned dst (fbytes, RGB rows); drain(i, src, len)
+using FillFn = std::function<int(int, uint8_t *)>;
+using DrainFn = std::function<int(int, const uint8_t *, size_t)>;
+
+static int stream_run(mij_stream *s, int n, const FillFn &fill, const DrainFn &drain, int *failed) {
+  if (failed) *failed = -1;
+  S_TRY(hipSetDevice(s->dev));
+  for (double &v : s->stats) v = 0.0;
+  const double t_start = now_s();
+  const int nchunks = (n + s->chunk - 1) / s->chunk;
+  auto count = [&](int k) { return std::min(s->chunk, n - k * s->chunk); };
+
+  auto enqueue = [&](int k) -> int {
+    const int sl = k & 1, first = k * s->chunk, cnt = count(k);
+    const double t0 = now_s();
+    int bad = -1;
+    int rc = parallel_for(cnt, s->threads, [&](int i) { return fill(first + i, s->h_in[sl] + (size_t)i * s->fbytes); }, &bad);
+    s->stats[1] += now_s() - t0;
+    if (rc) {
+      if (failed) *failed = first + bad;
+      return rc;
+    }
+    if ((rc = mij_batch_upload_async(s->b[sl], s->h_in[sl], cnt))) return rc;
+    S_TRY(hipEventRecord(s->ev_t0[sl], s->st[sl]));
+    if ((rc = mij_batch_encode(s->b[sl], cnt))) return rc;
+    S_TRY(hipEventRecord(s->ev_t1[sl], s->st[sl]));
+    if ((rc = mij_batch_lengths_async(s->b[sl], s->h_len[sl], s->h_err[sl], cnt))) return rc;
+    S_TRY(hipEventRecord(s->ev_len[sl], s->st[sl]));
+    s->stats[5] += (double)cnt * s->fbytes;
+    return MIJ_OK;
+  };
+
+  auto finish = [&](int k) -> int {
+    const int sl = k & 1, first = k * s->chunk, cnt = count(k);
+    S_TRY(hipEventSynchronize(s->ev_len[sl]));
+    std::vector<size_t> &off = s->off[sl];
+    off[0] = 0;
+    for (int i = 0; i < cnt; i++) {
+      if (s->h_err[sl][i]) {
+        if (failed) *failed = first + i;
+        return mij_fail(MIJ_ETABLE, "stream: frame %d: Huffman table construction failed", first + i);
+      }
+      off[i + 1] = off[i] + (size_t)s->h_len[sl][i];
+    }
+    if (off[cnt] > s->h_out_cap[sl]) {  // the previous D2H into this slot has completed
+      S_TRY(hipHostFree(s->h_out[sl]));
+      s->h_out_cap[sl] = off[cnt] + off[cnt] / 4;
+      S_TRY(hipHostMalloc((void **)&s->h_out[sl], s->h_out_cap[sl], hipHostMallocDefault));
+    }
+    for (int i = 0; i < cnt; i++) {
+      const int rc = mij_batch_output_async(s->b[sl], i, s->h_out[sl] + off[i], (size_t)s->h_len[sl][i]);
+      if (rc) return rc;
+    }
+    S_TRY(hipEventRecord(s->ev_out[sl], s->st[sl]));
+    S_TRY(hipEventSynchronize(s->ev_out[sl]));
+    float ms = 0.f;
+    S_TRY(hipEventElapsedTime(&ms, s->ev_t0[sl], s->ev_t1[sl]));
+    s->stats[3] += ms * 1e-3;
+    const double t0 = now_s();
+    int bad = -1;
+    const int rc = parallel_for(cnt, s->threads,
+                                [&](int i) { return drain(first + i, s->h_out[sl] + off[i], off[i + 1] - off[i]); }, &bad);
+    s->stats[2] += now_s() - t0;
+    s->stats[4] += cnt;
+    s->stats[6] += (double)off[cnt];
+    if (rc && failed) *failed = first + bad;
+    return rc;
+  };
+
+  int rc = nchunks ? enqueue(0) : MIJ_OK;
+  for (int k = 0; k < nchunks && !rc; k++) {
+    if (k + 1 < nchunks) rc = enqueue(k + 1);  // chunk k+1 is read while the GPU works on chunk k
+    const int rc2 = finish(k);
+    if (!rc) rc = rc2;
+    if (rc && k + 1 < nchunks) {  // drain what is still queued before returning
+      hipStreamSynchronize(s->st[0]);
+      hipStreamSynchronize(s->st[1]);
+    }
+  }
+  s->stats[0] = now_s() - t_start;
+  if (!rc) mij_clear_error();
+  return rc;
+}
+
+extern "C" int mij_stream_encode_files(mij_stream *s, const char *const *in_paths,
+                                       const char *const *out_paths, int n, int *failed) {
+  if (!s || !in_paths || !out_paths || n < 0) return mij_fail(MIJ_EINVAL, "stream_encode_files: bad args");
+  auto fill = [&](int i, uint8_t *dst) -> int {
+    return ppm_load(in_paths[i], dst, s->fbytes, 3 * s->w, 0, s->w, s->h);
+  };
+  auto drain = [&](int i, const uint8_t *src, size_t len) -> int {
+    FILE *f = fopen(out_paths[i], "wb");
+    if (!f) return mij_fail(MIJ_EIO, "cannot create '%s'", out_paths[i]);
+    const bool ok = fwrite(src, 1, len, f) == len;
+    return (fclose(f) == 0 && ok) ? MIJ_OK : mij_fail(MIJ_EIO, "cannot write '%s'", out_paths[i]);
+  };
+  return stream_run(s, n, fill, drain, failed);
+}
+
+extern "C" int mij_stream_encode_frames(mij_stream *s, const uint8_t *const *rgb, int n,
+                                        uint8_t *const *outs, const size_t *caps, size_t *lens) {
+  if (!s || !rgb || !outs || !caps || !lens || n < 0) return mij_fail(MIJ_EINVAL, "stream_encode_frames: bad args");
+  auto fill = [&](int i, uint8_t *dst) -> int {
+    memcpy(dst, rgb[i], s->fbytes);
+    return MIJ_OK;
+  };
+  auto drain = [&](int i, const uint8_t *src, size_t len) -> int {
+    lens[i] = len;
+    if (len > caps[i]) return mij_fail(MIJ_ENOSPC, "stream: frame %d needs %zu bytes", i, len);
+    memcpy(outs[i], src, len);
+    return MIJ_OK;
+  };
+  return stream_run(s, n, fill, drain, nullptr);
+}

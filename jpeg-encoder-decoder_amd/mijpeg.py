@@ -28,6 +28,9 @@ EXPORTS = [
     "mij_band_analyze", "mij_band_histograms", "mij_band_tables", "mij_band_pack", "mij_band_words",
     "mij_assemble_begin", "mij_assemble_words", "mij_assemble_end",
     "mij_probe_mfma", "mij_colour_lut", "mij_build_target",
+    "mij_batch_set_rgb", "mij_ppm_header", "mij_ppm_read",
+    "mij_stream_create", "mij_stream_destroy", "mij_stream_encode_files",
+    "mij_stream_encode_frames", "mij_stream_stats",
 ]
 
 
@@ -116,6 +119,18 @@ def load() -> C.CDLL:
     lib.mij_probe_mfma.argtypes = [p, p, p]
     lib.mij_colour_lut.argtypes = [p]
     lib.mij_build_target.restype = C.c_char_p
+    lib.mij_batch_set_rgb.argtypes = [p, i]
+    lib.mij_ppm_header.argtypes = [C.c_char_p, C.POINTER(i), C.POINTER(i), C.POINTER(C.c_longlong)]
+    lib.mij_ppm_read.argtypes = [C.c_char_p, p, sz, i, i]
+    lib.mij_stream_create.restype = p
+    lib.mij_stream_create.argtypes = [i, i, i, i, i, i]
+    lib.mij_stream_destroy.argtypes = [p]
+    lib.mij_stream_destroy.restype = None
+    lib.mij_stream_encode_files.argtypes = [p, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), i,
+                                            C.POINTER(i)]
+    lib.mij_stream_encode_frames.argtypes = [p, C.POINTER(p), i, C.POINTER(p), C.POINTER(sz),
+                                             C.POINTER(sz)]
+    lib.mij_stream_stats.argtypes = [p, p, i]
     _lib = lib
     return lib
 
@@ -222,6 +237,10 @@ class Batch:
 
     def set_split(self, on: bool) -> None:
         _check(self.lib.mij_batch_set_split(self.h_, int(on)), "set_split")
+
+    def set_rgb(self, on: bool) -> None:
+        """frames in R, G, B byte order (PPM) instead of the encoder's B, G, R"""
+        _check(self.lib.mij_batch_set_rgb(self.h_, int(on)), "set_rgb")
 
     def upload(self, frames_bgr: np.ndarray, first: int = 0) -> None:
         frames_bgr = np.ascontiguousarray(frames_bgr, np.uint8)
@@ -343,6 +362,78 @@ class Batch:
     def assemble_end(self, n: int, total_bits: np.ndarray) -> None:
         t = np.ascontiguousarray(total_bits, np.uint64).reshape(n, 3)
         _check(self.lib.mij_assemble_end(self.h_, n, _ptr(t)), "assemble_end")
+
+
+# ---- PPM ingest (utils/original.c:294-365 rules) and the streaming encoder ----
+
+def ppm_header(path: str):
+    """(width, height, pixel data offset) of a P6 file; raises MijError with
+    the reference reader's message class (MIJ_EPPM / MIJ_EIO) otherwise."""
+    w, h, off = C.c_int(0), C.c_int(0), C.c_longlong(0)
+    _check(load().mij_ppm_header(path.encode(), C.byref(w), C.byref(h), C.byref(off)),
+           f"ppm_header({path})")
+    return w.value, h.value, off.value
+
+
+def ppm_read(path: str, to_bgr: bool = False) -> np.ndarray:
+    w, h, _ = ppm_header(path)
+    out = np.zeros((h, w, 3), np.uint8)
+    _check(load().mij_ppm_read(path.encode(), _ptr(out), out.nbytes, 3 * w, int(to_bgr)),
+           f"ppm_read({path})")
+    return out
+
+
+class Stream:
+    """mij_stream: PPM files / RGB frames -> JPEG through two device batches
+    in ping-pong (include/mijpeg.h)."""
+    STATS = ["wall_s", "read_s", "write_s", "gpu_s", "frames", "bytes_in", "bytes_out"]
+
+    def __init__(self, w: int, h: int, chunk: int, quality: int = 50, device: int = 0,
+                 threads: int = 0):
+        self.lib = load()
+        self.w, self.h = w, h
+        self.h_ = self.lib.mij_stream_create(device, w, h, chunk, quality, threads)
+        if not self.h_:
+            raise MijError(f"mij_stream_create failed: "
+                           f"{self.lib.mij_strerror(self.lib.mij_last_error()).decode()}")
+
+    def close(self) -> None:
+        if self.h_:
+            self.lib.mij_stream_destroy(self.h_)
+            self.h_ = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def encode_files(self, ins, outs) -> None:
+        n = len(ins)
+        a = (C.c_char_p * n)(*[s.encode() for s in ins])
+        b = (C.c_char_p * n)(*[s.encode() for s in outs])
+        failed = C.c_int(-1)
+        rc = self.lib.mij_stream_encode_files(self.h_, a, b, n, C.byref(failed))
+        if rc:
+            raise MijError(f"stream_encode_files: {self.lib.mij_strerror(rc).decode()} ({rc}), "
+                           f"file {failed.value}")
+
+    def encode_frames(self, frames_rgb) -> list:
+        n = len(frames_rgb)
+        frames = [np.ascontiguousarray(f, np.uint8) for f in frames_rgb]
+        cap = max_jpg_bytes(self.w, self.h)
+        outs = [np.zeros(cap, np.uint8) for _ in range(n)]
+        ins = (C.c_void_p * n)(*[_ptr(f) for f in frames])
+        ops = (C.c_void_p * n)(*[_ptr(o) for o in outs])
+        caps = (C.c_size_t * n)(*([cap] * n))
+        lens = (C.c_size_t * n)()
+        _check(self.lib.mij_stream_encode_frames(self.h_, ins, n, ops, caps, lens), "stream_encode_frames")
+        return [o[:lens[i]].tobytes() for i, o in enumerate(outs)]
+
+    def stats(self) -> dict:
+        v = np.zeros(len(self.STATS), np.float64)
+        _check(self.lib.mij_stream_stats(self.h_, _ptr(v), len(v)), "stream_stats")
+        return dict(zip(self.STATS, [float(x) for x in v]))
 
 
 def probe_mfma(A: np.ndarray, B: np.ndarray) -> np.ndarray:
