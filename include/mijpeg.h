@@ -117,13 +117,14 @@ int mij_batch_upload(mij_batch *b, const uint8_t *bgr, int first, int nframes);
 int mij_batch_set_input(mij_batch *b, const void *d_bgr, long long frame_stride,
                         int pitch);
 int mij_batch_encode(mij_batch *b, int nframes);     /* full path, async */
-/* pipeline: split (default) -- K1 writes zigzag coefficient planes and a
- * second pass tokenizes them; fused (set_split(b, 0)) -- K1 emits the symbol
- * tokens directly.  Same output bytes either way. */
+/* pipeline: fused (default) -- K1 emits the symbol tokens directly, the
+ * coefficient planes never reach HBM; split (set_split(b, 1)) -- K1 writes
+ * zigzag coefficient planes and a second pass tokenizes them.  Same output
+ * bytes either way. */
 int mij_batch_set_split(mij_batch *b, int on);
 /* input frames in R, G, B byte order (PPM files, brain.c:25-42) instead of the
  * encoder's B, G, R (encoder.c:133); the channels are swapped inside K1, at no
- * cost.  Split pipeline only. */
+ * cost.  Both pipelines. */
 int mij_batch_set_rgb(mij_batch *b, int on);
 /* fused pipeline only: also keep the coefficient planes (for
  * mij_batch_coefs); the split pipeline always has them */

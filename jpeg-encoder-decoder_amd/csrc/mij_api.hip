@@ -255,7 +255,8 @@ struct mij_batch {
   std::vector<unsigned long long> band_words;  // per frame x 3: packed words after mij_band_pack
   bool keep_coefs = false;  // encode also writes coefficient planes
   bool rgb = false;         // input frames in R, G, B byte order (PPM) instead of B, G, R
-  bool split = true;        // K1 writes coefficients, a second pass tokenizes
+  bool split = false;       // true: K1 writes coefficients, a second pass tokenizes;
+                            // false (default): K1 emits the tokens itself
   bool timing = false;
   static constexpr int HIST = 64;
   hipEvent_t evh[HIST][MIJ_NSTAGES] = {};  // per-step events while timing is on
@@ -447,7 +448,7 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int se
   k.hist = b->d_hist;
   k.fix_list = b->d_fix;
   k.fix_count = b->d_fix_count;
-  k.rgb = b->rgb && mode == 1;
+  k.rgb = b->rgb && (mode & 4) == 0;  // pixel-input variants
   static const int k1_flags = getenv("MIJ_K1_FLAGS") ? atoi(getenv("MIJ_K1_FLAGS")) : 0;
   k.flags = k1_flags;
   const long long ntiles = (long long)nframes * b->g.tiles_per_frame;
@@ -519,7 +520,6 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
 }
 
 static int encode_frames(mij_batch *b, int nframes) {
-  if (b->rgb && !b->split) return fail(MIJ_EINVAL, "encode: RGB input needs the split pipeline");
   HIP_TRY(hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * nframes * 4 * 257, b->stream));
   HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * nframes, b->stream));
   if (b->timing) HIP_TRY(hipEventRecord(b->ev[0], b->stream));

@@ -599,10 +599,12 @@ constexpr int K1M_RGB = 8;       // pixels in RGB order (PPM) instead of BGR (en
 // shared tables fit the 160 KB LDS, <= 168 VGPRs); the token variants carry
 // per-wave token staging and run 4-wave workgroups, two per CU.
 template <int MODE>
-constexpr int k1_waves() { return (MODE & ~K1M_RGB) == K1M_COEF_OUT ? 12 : 4; }
+constexpr bool k1_wide() { return (MODE & ~K1M_RGB) == K1M_COEF_OUT || (MODE & ~K1M_RGB) == K1M_TOK_OUT; }
+template <int MODE>
+constexpr int k1_waves() { return k1_wide<MODE>() ? 12 : 4; }
 
 template <int MODE>
-__global__ __launch_bounds__(64 * k1_waves<MODE>(), (MODE & ~K1M_RGB) == K1M_COEF_OUT ? 1 : 2) void k_mcu_dct(K1Args a) {
+__global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) void k_mcu_dct(K1Args a) {
   constexpr bool PIX = !(MODE & K1M_COEF_IN);
   constexpr bool TOK = MODE & K1M_TOK_OUT;
   constexpr int NW = k1_waves<MODE>();
@@ -617,7 +619,11 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), (MODE & ~K1M_RGB) == K1M_COE
   __shared__ __attribute__((aligned(16))) float s_fac[2][64];
   __shared__ float s_inv8q[2];
   __shared__ uint32_t s_dctie[2][DCTIE_WORDS];
-  __shared__ uint32_t s_lut[PIX ? 3 * LUT_WORDS : 1];
+  // colour-exception bitmaps: in LDS for the coefficient variant; the wide
+  // token variant reads them from global memory (rare path, L1/L2 hits) to
+  // fit its token staging into the 160 KB
+  constexpr bool LUT_LDS = PIX && !(TOK && NW == 12);
+  __shared__ uint32_t s_lut[LUT_LDS ? 3 * LUT_WORDS : 1];
   __shared__ double s_cos[64];
   __shared__ int s_qint[2][64];
   __shared__ __attribute__((aligned(16))) int16_t s_st[TOK ? NW : 1][64][16];  // token staging
@@ -650,8 +656,10 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), (MODE & ~K1M_RGB) == K1M_COE
   if (threadIdx.x < 2 * DCTIE_WORDS) (&s_dctie[0][0])[threadIdx.x] = (&T->dctie[0][0])[threadIdx.x];
   if (PIX) {
     for (int i = threadIdx.x; i < 12 * 64; i += NT) s_A[i] = T->mfma_a[i];
-    for (int i = threadIdx.x; i < 3 * LUT_WORDS; i += NT) s_lut[i] = (&T->lut[0][0])[i];
+    if (LUT_LDS)
+      for (int i = threadIdx.x; i < 3 * LUT_WORDS; i += NT) s_lut[i] = (&T->lut[0][0])[i];
   }
+  const uint32_t *__restrict__ lut = LUT_LDS ? (const uint32_t *)s_lut : &T->lut[0][0];
   for (int i = threadIdx.x; i < 128; i += NT) {
     s_fac[i >> 6][i & 63] = T->qfac[i >> 6][i & 63];
   }
@@ -723,7 +731,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), (MODE & ~K1M_RGB) == K1M_COE
           dma_wait();
         else if (DEFER)
           dma_wait_behind_stores();
-        if (!(kflags & K1F_NO_COLOUR)) colour_stage<RGB>(raw, L, c4, pr, s_lut, !(kflags & K1F_NO_LUT));
+        if (!(kflags & K1F_NO_COLOUR)) colour_stage<RGB>(raw, L, c4, pr, lut, !(kflags & K1F_NO_LUT));
         wave_lds_sync();
         // ---- stream the wave's next tile into the freed raw buffer -----------
         if (tn < tend) {
@@ -2041,7 +2049,10 @@ int k1_grid(int device, long long ntiles, int mode) {
       per_cu = k1_blocks_per_cu<K1M_COEF_OUT>();
       nw = k1_waves<K1M_COEF_OUT>();
       break;
-    case K1M_TOK_OUT: per_cu = k1_blocks_per_cu<K1M_TOK_OUT>(); break;
+    case K1M_TOK_OUT:
+      per_cu = k1_blocks_per_cu<K1M_TOK_OUT>();
+      nw = k1_waves<K1M_TOK_OUT>();
+      break;
     case K1M_COEF_OUT | K1M_TOK_OUT: per_cu = k1_blocks_per_cu<K1M_COEF_OUT | K1M_TOK_OUT>(); break;
     default: per_cu = k1_blocks_per_cu<K1M_COEF_IN | K1M_TOK_OUT>(); break;
   }
@@ -2072,9 +2083,17 @@ hipError_t launch_k1(const K1Args &a, int grid, int mode, hipStream_t s) {
       else
         hipLaunchKernelGGL((k_mcu_dct<K1M_COEF_OUT>), dim3(grid), dim3(64 * k1_waves<K1M_COEF_OUT>()), 0, s, a);
       break;
-    case K1M_TOK_OUT: hipLaunchKernelGGL((k_mcu_dct<K1M_TOK_OUT>), dim3(grid), dim3(256), 0, s, a); break;
+    case K1M_TOK_OUT:
+      if (a.rgb)
+        hipLaunchKernelGGL((k_mcu_dct<K1M_TOK_OUT | K1M_RGB>), dim3(grid), dim3(64 * k1_waves<K1M_TOK_OUT>()), 0, s, a);
+      else
+        hipLaunchKernelGGL((k_mcu_dct<K1M_TOK_OUT>), dim3(grid), dim3(64 * k1_waves<K1M_TOK_OUT>()), 0, s, a);
+      break;
     case K1M_COEF_OUT | K1M_TOK_OUT:
-      hipLaunchKernelGGL((k_mcu_dct<K1M_COEF_OUT | K1M_TOK_OUT>), dim3(grid), dim3(256), 0, s, a);
+      if (a.rgb)
+        hipLaunchKernelGGL((k_mcu_dct<K1M_COEF_OUT | K1M_TOK_OUT | K1M_RGB>), dim3(grid), dim3(256), 0, s, a);
+      else
+        hipLaunchKernelGGL((k_mcu_dct<K1M_COEF_OUT | K1M_TOK_OUT>), dim3(grid), dim3(256), 0, s, a);
       break;
     case K1M_COEF_IN | K1M_TOK_OUT:
       hipLaunchKernelGGL((k_mcu_dct<K1M_COEF_IN | K1M_TOK_OUT>), dim3(grid), dim3(256), 0, s, a);

@@ -98,10 +98,12 @@ def test_stream_create_validates_before_device_use():
 # ---------------------------------------------------------------------------
 
 @pytest.mark.gpu
-def test_batch_rgb_input_same_bytes_as_bgr():
+@pytest.mark.parametrize("split", [False, True])
+def test_batch_rgb_input_same_bytes_as_bgr(split):
     """K1 reading R, G, B (PPM order) gives the bytes of the B, G, R path."""
     rgb = np.stack([recipes.sample("sample_640x640"), recipes.sample("sample_640x640_diffs")])
     b = mijpeg.Batch(640, 640, 2)
+    b.set_split(split)
     b.set_rgb(True)
     b.upload(rgb)
     b.encode(2)
