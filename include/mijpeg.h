@@ -163,6 +163,29 @@ unsigned long long mij_batch_replays(mij_batch *b);
 /* the batch's hipStream_t, as an opaque pointer */
 void *mij_batch_stream(mij_batch *b);
 
+/* ---- region batches: many areas of one frame -----
+ * The reference's workload (main.c:142-155): the change detector returns up
+ * to 100 rectangles of a frame and each is encoded on its own with
+ * rgb_to_dct / init_huffman / write_jpg.  A region batch does all of them in
+ * one launch sequence: the batch is created with the largest region's size
+ * (the canvas) and slot i holds region i, w_i x h_i, at the top-left of its
+ * slot.  Each region gets its own tables and JFIF (SOF0 = w_i x h_i); the
+ * bytes are those of the three drop-in calls on that region. */
+/* per-frame sizes of the next encodes (multiples of 16, at most the batch
+ * geometry); wh = {w0, h0, w1, h1, ...}; NULL restores the batch geometry */
+int mij_batch_set_frame_dims(mij_batch *b, const int *wh, int nframes);
+/* regions of a device-resident BGR frame (rows pitch bytes apart) into
+ * slots 0..n-1 (one gather launch) and their sizes as the frame dims */
+int mij_batch_gather_regions(mij_batch *b, const void *d_frame, long long pitch,
+                             int frame_w, int frame_h, const area_t *regions, int n);
+/* the same from a host frame of stride_px pixels per row (uploaded once) */
+int mij_batch_upload_regions(mij_batch *b, const uint8_t *bgr, int stride_px, int frame_h,
+                             const area_t *regions, int n);
+/* one call: every region of a host BGR frame to its own JPEG; the n streams
+ * are written back to back into out (cap bytes), their lengths into lens */
+int mij_encode_regions(const uint8_t *bgr, int stride_px, int frame_h, const area_t *regions,
+                       int n, int quality, uint8_t *out, size_t cap, size_t *lens);
+
 /* ---- PPM ingest -----------------------------------
  * Header rules of the reference's reader, utils/original.c:294-365, kept
  * exactly: "P6" then a newline straight after it; then lines up to the first

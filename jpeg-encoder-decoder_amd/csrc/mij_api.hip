@@ -23,7 +23,7 @@ hipError_t launch_k1(const K1Args &a, int grid, int mode, hipStream_t s);
 hipError_t launch_fix_blocks(const K1Args &a, hipStream_t s);
 hipError_t launch_seg_dc(const EntArgs &a, hipStream_t s);
 hipError_t launch_dc_diff(int16_t *coef, const int16_t *dc, const Geom &g, int nframes,
-                          hipStream_t s);
+                          const int2 *fd, hipStream_t s);
 hipError_t launch_tables(const EntArgs &a, hipStream_t s);
 hipError_t launch_ehuf_struct(const HuffCode *hc, uint32_t *ehuf, hipStream_t s);
 hipError_t launch_bits(const EntArgs &a, hipStream_t s);
@@ -32,6 +32,9 @@ hipError_t launch_pack(const EntArgs &a, hipStream_t s);
 hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s);
 hipError_t launch_emit(const EntArgs &a, hipStream_t s);
 hipError_t launch_or_words(uint32_t *dst, const uint32_t *src, long long n, hipStream_t s);
+hipError_t launch_gather_regions(uint8_t *dst, long long slot_bytes, int pitch, const uint8_t *src,
+                                 long long src_pitch, const int4 *regions, int n, int max_h,
+                                 hipStream_t s);
 hipError_t launch_mfma_probe(const int4 *A, const int4 *B, int4 *D, hipStream_t s);
 }  // namespace mij
 
@@ -253,6 +256,14 @@ struct mij_batch {
   uint32_t *d_stage = nullptr;      // H2D staging for mij_assemble_words
   size_t stage_words = 0;
   std::vector<unsigned long long> band_words;  // per frame x 3: packed words after mij_band_pack
+  // region batches (mij_batch_set_frame_dims / _gather_regions): per-frame
+  // image size inside the canvas slots; d_frame stages a host frame
+  int2 *d_fdims = nullptr;
+  int4 *d_regions = nullptr;
+  bool use_fdims = false;
+  std::vector<int2> h_fdims;
+  uint8_t *d_frame = nullptr;
+  size_t frame_cap = 0;
   bool keep_coefs = false;  // encode also writes coefficient planes
   bool rgb = false;         // input frames in R, G, B byte order (PPM) instead of B, G, R
   bool split = false;       // true: K1 writes coefficients, a second pass tokenizes;
@@ -278,7 +289,7 @@ static void batch_free(mij_batch *b) {
                   b->d_ehuf, b->d_raw, b->d_tok, b->d_seg_ntok, b->d_seg_bits, b->d_seg_off,
                   b->d_scan_bits, b->d_out_len, b->d_hc, b->d_out, b->d_err, b->d_replays,
                   b->d_dcpred, b->d_bitbase, b->d_stage, b->d_fix, b->d_fix_count, b->d_ffc, b->d_choff,
-                  b->d_pack_state, b->d_pack_ticket};
+                  b->d_pack_state, b->d_pack_ticket, b->d_fdims, b->d_frame, b->d_regions};
   for (void *p : ptrs)
     if (p) hipFree(p);
   for (auto &row : b->evh)
@@ -343,6 +354,9 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
   HIP_TRY(dalloc(&b->d_pack_ticket, 1));
   HIP_TRY(dalloc(&b->d_fix_count, 1));
   HIP_TRY(hipMemsetAsync(b->d_replays, 0, sizeof(unsigned), b->stream));
+  HIP_TRY(dalloc(&b->d_fdims, F));
+  HIP_TRY(dalloc(&b->d_regions, F));
+  b->h_fdims.assign((size_t)F, make_int2(w, h));
   HIP_TRY(dalloc(&b->d_dcpred, F * 4));
   HIP_TRY(dalloc(&b->d_bitbase, F * 4));
   HIP_TRY(hipMemsetAsync(b->d_dcpred, 0, sizeof(int16_t) * F * 4, b->stream));
@@ -426,6 +440,7 @@ static EntArgs ent_args(mij_batch *b, int nframes) {
   a.choff = b->d_choff;
   a.pack_state = b->d_pack_state;
   a.pack_ticket = b->d_pack_ticket;
+  a.fdims = b->use_fdims ? b->d_fdims : nullptr;
   return a;
 }
 
@@ -449,6 +464,7 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int se
   k.fix_list = b->d_fix;
   k.fix_count = b->d_fix_count;
   k.rgb = b->rgb && (mode & 4) == 0;  // pixel-input variants
+  k.fdims = b->use_fdims ? b->d_fdims : nullptr;
   static const int k1_flags = getenv("MIJ_K1_FLAGS") ? atoi(getenv("MIJ_K1_FLAGS")) : 0;
   k.flags = k1_flags;
   const long long ntiles = (long long)nframes * b->g.tiles_per_frame;
@@ -521,6 +537,11 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
 
 static int encode_frames(mij_batch *b, int nframes) {
   HIP_TRY(hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * nframes * 4 * 257, b->stream));
+  // region batches: K1 skips the canvas tiles outside a frame, so their
+  // segments must read as empty
+  if (b->use_fdims && b->rgb) return fail(MIJ_EINVAL, "encode: region batches read B, G, R frames");
+  if (b->use_fdims)
+    HIP_TRY(hipMemsetAsync(b->d_seg_ntok, 0, sizeof(uint32_t) * nframes * b->g.nseg, b->stream));
   HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * nframes, b->stream));
   if (b->timing) HIP_TRY(hipEventRecord(b->ev[0], b->stream));
   if (b->split) {
@@ -556,6 +577,90 @@ extern "C" int mij_batch_set_rgb(mij_batch *b, int on) {
   if (!b) return fail(MIJ_EINVAL, "set_rgb: null batch");
   b->rgb = on != 0;
   return MIJ_OK;
+}
+
+// ---- region batches --------------------------------
+static int check_frame_dims(const mij_batch *b, int w, int h, const char *what, int i) {
+  if (!valid_dims(w, h) || w > b->g.w || h > b->g.h)
+    return fail(MIJ_EINVAL, "%s: frame %d is %dx%d (multiples of 16, at most the batch's %dx%d)", what, i,
+                w, h, b->g.w, b->g.h);
+  return MIJ_OK;
+}
+
+// per-frame sizes, queued on the batch stream (the kernels read them there)
+static int upload_frame_dims(mij_batch *b, const int2 *wh, int n) {
+  for (int i = 0; i < b->cap; i++) b->h_fdims[i] = i < n ? wh[i] : make_int2(b->g.w, b->g.h);
+  HIP_TRY(hipMemcpyAsync(b->d_fdims, b->h_fdims.data(), sizeof(int2) * b->cap, hipMemcpyHostToDevice,
+                         b->stream));
+  // the pageable source is read before the call returns only with a sync
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  b->use_fdims = true;
+  return MIJ_OK;
+}
+
+extern "C" int mij_batch_set_frame_dims(mij_batch *b, const int *wh, int nframes) {
+  if (!b) return fail(MIJ_EINVAL, "set_frame_dims: null batch");
+  HIP_TRY(hipSetDevice(b->dev));
+  if (!wh) {
+    b->use_fdims = false;
+    return MIJ_OK;
+  }
+  if (nframes < 1 || nframes > b->cap) return fail(MIJ_EINVAL, "set_frame_dims: bad frame count");
+  std::vector<int2> v(nframes);
+  for (int i = 0; i < nframes; i++) {
+    if (check_frame_dims(b, wh[2 * i], wh[2 * i + 1], "set_frame_dims", i)) return g_err;
+    v[i] = make_int2(wh[2 * i], wh[2 * i + 1]);
+  }
+  return upload_frame_dims(b, v.data(), nframes);
+}
+
+// regions of one frame in device memory (rows src_pitch bytes apart, frame
+// frame_w x frame_h pixels) into slots 0..n-1, each slot's size set to its
+// region's; one gather launch on the batch stream
+static int gather_regions(mij_batch *b, const uint8_t *d_src, long long src_pitch, int frame_w,
+                          int frame_h, const area_t *regions, int n) {
+  if (!b->own_in) return fail(MIJ_EINVAL, "regions: batch reads external device input");
+  if (n < 1 || n > b->cap || !regions) return fail(MIJ_EINVAL, "regions: bad region count %d", n);
+  std::vector<int4> r(n);
+  std::vector<int2> wh(n);
+  int max_h = 0;
+  for (int i = 0; i < n; i++) {
+    const area_t d = regions[i];
+    if (check_frame_dims(b, d.w, d.h, "regions", i)) return g_err;
+    if (d.x < 0 || d.y < 0 || d.x + d.w > frame_w || d.y + d.h > frame_h)
+      return fail(MIJ_EINVAL, "regions: region %d (%d,%d %dx%d) outside the %dx%d frame", i, d.x, d.y,
+                  d.w, d.h, frame_w, frame_h);
+    r[i] = make_int4(d.x, d.y, d.w, d.h);
+    wh[i] = make_int2(d.w, d.h);
+    max_h = d.h > max_h ? d.h : max_h;
+  }
+  HIP_TRY(hipMemcpyAsync(b->d_regions, r.data(), sizeof(int4) * n, hipMemcpyHostToDevice, b->stream));
+  HIP_TRY(launch_gather_regions(b->d_in, b->in_fs, b->pitch, d_src, src_pitch, b->d_regions, n, max_h,
+                                b->stream));
+  return upload_frame_dims(b, wh.data(), n);  // synchronises (pageable sources)
+}
+
+extern "C" int mij_batch_gather_regions(mij_batch *b, const void *d_frame, long long pitch, int frame_w,
+                                        int frame_h, const area_t *regions, int n) {
+  if (!b || !d_frame || pitch < 3LL * frame_w) return fail(MIJ_EINVAL, "gather_regions: bad args");
+  HIP_TRY(hipSetDevice(b->dev));
+  return gather_regions(b, (const uint8_t *)d_frame, pitch, frame_w, frame_h, regions, n);
+}
+
+extern "C" int mij_batch_upload_regions(mij_batch *b, const uint8_t *bgr, int stride_px, int frame_h,
+                                        const area_t *regions, int n) {
+  if (!b || !bgr || stride_px < 16 || frame_h < 16) return fail(MIJ_EINVAL, "upload_regions: bad args");
+  HIP_TRY(hipSetDevice(b->dev));
+  const size_t bytes = (size_t)stride_px * frame_h * 3;
+  if (bytes > b->frame_cap) {
+    if (b->d_frame) HIP_TRY(hipFree(b->d_frame));
+    b->d_frame = nullptr;
+    b->frame_cap = 0;
+    HIP_TRY(hipMalloc((void **)&b->d_frame, bytes));
+    b->frame_cap = bytes;
+  }
+  HIP_TRY(hipMemcpyAsync(b->d_frame, bgr, bytes, hipMemcpyHostToDevice, b->stream));
+  return gather_regions(b, b->d_frame, 3LL * stride_px, stride_px, frame_h, regions, n);
 }
 
 // ---- asynchronous host transfers for the streaming engine (mij_stream.hip):
@@ -708,14 +813,17 @@ extern "C" int mij_batch_coefs(mij_batch *b, int frame, int16_t *Y, int16_t *Cb,
                                int diffed) {
   if (!b || frame < 0 || frame >= b->cap) return fail(MIJ_EINVAL, "coefs: bad frame");
   HIP_TRY(hipSetDevice(b->dev));
-  const Geom &g = b->g;
-  int16_t *base = b->d_coef + (long long)frame * g.coef_fs;
+  const Geom &g0 = b->g;
+  // the frame's own planes (region batches: its w x h, not the canvas)
+  const FGeom g = frame_geom(g0, b->use_fdims ? b->h_fdims.data() : nullptr, frame);
+  int16_t *base = b->d_coef + (long long)frame * g0.coef_fs;
   int16_t *tmp = nullptr;
   if (diffed) {  // differenced copy, leaving the batch's planes raw
-    HIP_TRY(hipMalloc((void **)&tmp, sizeof(int16_t) * g.coef_fs));
-    HIP_TRY(hipMemcpyAsync(tmp, base, sizeof(int16_t) * g.coef_fs, hipMemcpyDeviceToDevice,
+    HIP_TRY(hipMalloc((void **)&tmp, sizeof(int16_t) * g0.coef_fs));
+    HIP_TRY(hipMemcpyAsync(tmp, base, sizeof(int16_t) * g0.coef_fs, hipMemcpyDeviceToDevice,
                            b->stream));
-    HIP_TRY(launch_dc_diff(tmp, b->d_dc + (long long)frame * g.nblk, g, 1, b->stream));
+    HIP_TRY(launch_dc_diff(tmp, b->d_dc + (long long)frame * g0.nblk, g0, 1,
+                           b->use_fdims ? b->d_fdims + frame : nullptr, b->stream));
     base = tmp;
   }
   HIP_TRY(hipStreamSynchronize(b->stream));
@@ -805,7 +913,7 @@ extern "C" void rgb_to_dct(uint8_t *in, int16_t *Y, int16_t *Cb, int16_t *Cr, ar
   if (!b) return;
   if (upload_region(b, in, g_stride, dims)) return;
   if (run_k1(b, 1, 1)) return;
-  if (launch_dc_diff(b->d_coef, b->d_dc, b->g, 1, b->stream) != hipSuccess) {
+  if (launch_dc_diff(b->d_coef, b->d_dc, b->g, 1, nullptr, b->stream) != hipSuccess) {
     fail(MIJ_EHIP, "dc_diff launch failed");
     return;
   }
@@ -906,6 +1014,52 @@ extern "C" int mij_encode(const uint8_t *bgr, int stride_px, area_t dims, int qu
   if (n > cap) return fail(MIJ_ENOSPC, "mij_encode: need %zu bytes", n);
   if (mij_batch_output(b, 0, out, cap, &n)) return g_err;
   if (out_len) *out_len = n;
+  return MIJ_OK;
+}
+
+// main.c:142-155 in one call: every region of a BGR frame its own JPEG, all
+// regions through one region batch (canvas = the largest region)
+static mij_batch *g_rctx = nullptr;
+
+extern "C" int mij_encode_regions(const uint8_t *bgr, int stride_px, int frame_h, const area_t *regions,
+                                  int n, int quality, uint8_t *out, size_t cap, size_t *lens) {
+  std::lock_guard<std::mutex> l(g_mu);
+  g_err = MIJ_OK;
+  if (!bgr || !regions || n < 1 || !out || !lens || quality < 1 || quality > 100)
+    return fail(MIJ_EINVAL, "mij_encode_regions: bad arguments");
+  int W = 16, H = 16;
+  for (int i = 0; i < n; i++) {
+    if (!valid_dims(regions[i].w, regions[i].h))
+      return fail(MIJ_EINVAL, "mij_encode_regions: region %d is %dx%d", i, regions[i].w, regions[i].h);
+    W = regions[i].w > W ? regions[i].w : W;
+    H = regions[i].h > H ? regions[i].h : H;
+  }
+  if (!g_rctx || g_rctx->g.w < W || g_rctx->g.h < H || g_rctx->cap < n || g_rctx->quality != quality) {
+    const int cw = g_rctx && g_rctx->g.w > W ? g_rctx->g.w : W;
+    const int ch = g_rctx && g_rctx->g.h > H ? g_rctx->g.h : H;
+    const int cn = g_rctx && g_rctx->cap > n ? g_rctx->cap : n;
+    batch_free(g_rctx);
+    g_rctx = mij_batch_create(drop_device(), cw, ch, cn, quality);
+    if (!g_rctx) return g_err;
+  }
+  mij_batch *b = g_rctx;
+  if (mij_batch_upload_regions(b, bgr, stride_px, frame_h, regions, n)) return g_err;
+  if (encode_frames(b, n)) return g_err;
+  std::vector<size_t> len(n);
+  if (mij_batch_lengths(b, len.data(), n)) return g_err;
+  std::vector<int> err(n);
+  HIP_TRY(hipMemcpy(err.data(), b->d_err, sizeof(int) * n, hipMemcpyDeviceToHost));
+  for (int i = 0; i < n; i++)
+    if (err[i]) return fail(MIJ_ETABLE, "mij_encode_regions: region %d: Huffman table construction failed", i);
+  size_t off = 0;
+  for (int i = 0; i < n; i++) {
+    lens[i] = len[i];
+    if (off + len[i] > cap) return fail(MIJ_ENOSPC, "mij_encode_regions: need more than %zu bytes", cap);
+    HIP_TRY(hipMemcpyAsync(out + off, b->d_out + (long long)i * b->g.out_cap, len[i], hipMemcpyDeviceToHost,
+                           b->stream));
+    off += len[i];
+  }
+  HIP_TRY(hipStreamSynchronize(b->stream));
   return MIJ_OK;
 }
 

@@ -62,6 +62,46 @@ struct Geom {
   long long out_cap;        // output bytes per frame
 };
 
+// The image of frame f of a batch.  Buffers are laid out for the batch
+// geometry G (the "canvas"); a region batch (mij_batch_set_frame_dims) holds
+// smaller frames, each w x h at the top-left of its canvas slot: its blocks
+// are numbered in its own raster order (per-frame bw, nY, nC), its tiles and
+// segments keep the canvas numbering (tiles / segments outside the frame are
+// skipped and hold no tokens).  fd == nullptr: every frame is the canvas.
+struct FGeom {
+  int w, h, bw, mw, nY, nC, tiles_x, rows;  // rows = MCU rows = tile rows
+};
+__host__ __device__ inline FGeom frame_geom(const Geom &G, const int2 *fd, int f) {
+  FGeom r;
+  if (!fd) {  // the canvas: the Geom fields themselves (kernel arguments the
+              // compiler can reload instead of keeping them in registers)
+    r.w = G.w;
+    r.h = G.h;
+    r.bw = G.w >> 3;
+    r.mw = G.w >> 4;
+    r.nY = G.nY;
+    r.nC = G.nC;
+    r.tiles_x = G.tiles_x;
+    r.rows = G.h / TILE_H;
+    return r;
+  }
+#ifdef __HIP_DEVICE_COMPILE__
+  // f is wave-uniform wherever this is called: keep the sizes in SGPRs
+  const int w = __builtin_amdgcn_readfirstlane(fd[f].x), h = __builtin_amdgcn_readfirstlane(fd[f].y);
+#else
+  const int w = fd[f].x, h = fd[f].y;
+#endif
+  r.w = w;
+  r.h = h;
+  r.bw = w >> 3;
+  r.mw = w >> 4;
+  r.nY = (w >> 3) * (h >> 3);
+  r.nC = (w >> 4) * (h >> 4);
+  r.tiles_x = (w + TILE_W - 1) / TILE_W;
+  r.rows = h / TILE_H;
+  return r;
+}
+
 // Device-resident constant tables for one quality setting.
 struct Tables {
   int4 mfma_a[12 * 64];   // A fragments: 4 M-tiles x 3 digits x 64 lanes
@@ -95,6 +135,7 @@ struct K1Args {
   unsigned int *fix_count;  // coefficient mode: length of fix_list
   unsigned long long *wtime;  // diagnostics only (MIJ_K1_WTIME): per wave start, end, tiles
   int rgb;                  // input bytes in R, G, B order (PPM) instead of B, G, R
+  const int2 *fdims;        // per-frame image size (region batches), null: the canvas
 };
 // K1 diagnostic switches (timing attribution; outputs are wrong when set)
 constexpr int K1F_NO_LUT = 1, K1F_NO_REPLAY = 2, K1F_NO_COLOUR = 4, K1F_NO_DCT = 8,
@@ -129,6 +170,7 @@ struct EntArgs {
   unsigned long long *pack_state;  // k_pack_lb: per pack group, flag << 62 | bits
   unsigned int *pack_ticket;       // k_pack_lb: next group to claim
   unsigned long long *dbg;         // diagnostics only (MIJ_PACK_TIME, diag build)
+  const int2 *fdims;               // per-frame image size (region batches), null: the canvas
 };
 
 // EMIT_CH chunks of the largest scan buffer (the per-scan stride of EntArgs::ffc)

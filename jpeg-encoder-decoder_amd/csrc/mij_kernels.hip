@@ -232,6 +232,16 @@ __device__ __forceinline__ TilePos tile_pos(const Geom &G, int t) {
   return p;
 }
 
+// region batches: the tile inside its frame's own size (valid_px), and
+// whether it holds any of the frame (the canvas tiles outside are skipped)
+__device__ __forceinline__ TilePos tile_pos_r(const Geom &G, const int2 *fd, int t, bool &ok) {
+  TilePos p = tile_pos(G, t);
+  const FGeom fg = frame_geom(G, fd, p.f);
+  p.valid_px = min(TILE_W, fg.w - p.tx * TILE_W);
+  ok = p.tx < fg.tiles_x && p.ty < fg.rows;
+  return p;
+}
+
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void global_void_t;
 constexpr int TILE_RAW = TILE_W * 3 * TILE_H;  // 6144 B of BGR888 per tile
@@ -593,13 +603,15 @@ constexpr int K1M_COEF_OUT = 1;  // write zigzag coefficient planes
 constexpr int K1M_TOK_OUT = 2;   // write per-segment token streams + histograms
 constexpr int K1M_COEF_IN = 4;   // read coefficient planes (DC differences) instead of pixels
 constexpr int K1M_RGB = 8;       // pixels in RGB order (PPM) instead of BGR (encoder.c:133)
+constexpr int K1M_REGIONS = 16;  // per-frame image sizes inside the canvas (region batches)
+constexpr int k1_base(int mode) { return mode & ~(K1M_RGB | K1M_REGIONS); }
 
 // Waves per workgroup: the coefficient-only variant runs one 12-wave
 // workgroup per CU (3 waves per SIMD: 120 KB of per-wave tile buffers + the
 // shared tables fit the 160 KB LDS, <= 168 VGPRs); the token variants carry
 // per-wave token staging and run 4-wave workgroups, two per CU.
 template <int MODE>
-constexpr bool k1_wide() { return (MODE & ~K1M_RGB) == K1M_COEF_OUT || (MODE & ~K1M_RGB) == K1M_TOK_OUT; }
+constexpr bool k1_wide() { return k1_base(MODE) == K1M_COEF_OUT || k1_base(MODE) == K1M_TOK_OUT; }
 template <int MODE>
 constexpr int k1_waves() { return k1_wide<MODE>() ? 12 : 4; }
 
@@ -611,8 +623,12 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   constexpr int NT = 64 * NW;  // threads per workgroup
   // coefficient variant: FP64 replays are deferred to k_fix_blocks; the
   // token variants replay in place (their tokens are emitted here)
-  constexpr bool DEFER = (MODE & ~K1M_RGB) == K1M_COEF_OUT;
+  constexpr bool DEFER = k1_base(MODE) == K1M_COEF_OUT;
   constexpr bool RGB = MODE & K1M_RGB;
+  // region batches only: the frame sizes (compile-time null otherwise, so
+  // the per-tile geometry folds to the batch's)
+  constexpr bool REG = MODE & K1M_REGIONS;
+  const int2 *const fdims = REG ? a.fdims : nullptr;
   __shared__ __attribute__((aligned(16))) uint8_t s_raw[PIX ? NW : 1][TILE_RAW];
   __shared__ __attribute__((aligned(16))) uint8_t s_tile[PIX ? NW : 1][LDS_WAVE];
   __shared__ __attribute__((aligned(16))) int4 s_A[PIX ? 12 * 64 : 1];
@@ -679,13 +695,28 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   const int f0 = t0 / G.tiles_per_frame;      // a workgroup spans <= 2 frames
   const int tend = min(ntiles, t0 + a.per_wg);
   int t = t0 + wave;
+  // region batches: a tile holds pixels of its frame, or the wave claims the
+  // next one (the canvas tiles outside a frame are skipped)
+  auto skip_outside = [&](int &tt) {
+    bool ok;
+    while (tt < tend && (tile_pos_r(G, fdims, tt, ok), !ok)) {
+      int v = 0;
+      if (lane == 0) v = atomicAdd(&s_next, 1);
+      tt = __builtin_amdgcn_readfirstlane(v);
+    }
+  };
+  auto tpos = [&](int tt) {
+    bool ok;
+    return REG ? tile_pos_r(G, fdims, tt, ok) : tile_pos(G, tt);
+  };
+  if (REG) skip_outside(t);
 #ifdef MIJ_K1_DIAG
   const unsigned long long w_t0 = __builtin_amdgcn_s_memrealtime();
   int w_ntiles = 0;
 #endif
   if (t < tend) {
     uint8_t *raw = s_raw[PIX ? wave : 0];
-    TilePos p = tile_pos(G, t);
+    TilePos p = tpos(t);
     const uint32_t doff = dma_offset(a.pitch, lane);
     if (PIX) issue_tile_dma(a, p, lane, raw, doff);
     // coefficient input: the three N-tiles' 32 B per lane of a tile
@@ -694,14 +725,17 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
       for (int nt = 0; nt < 3; nt++) {
         bool valid;
         long long blk;
+        const FGeom fg = frame_geom(G, fdims, pp.f);  // REG only
+        const int bwf = REG ? fg.bw : bw, mwf = REG ? fg.mw : mw;
+        const int nYf = REG ? fg.nY : G.nY, nCf = REG ? fg.nC : G.nC;
         if (nt < 2) {
           const int bx = pp.tx * 16 + bcol;
-          valid = bx < bw;
-          blk = (long long)(2 * pp.ty + nt) * bw + bx;
+          valid = bx < bwf;
+          blk = (long long)(2 * pp.ty + nt) * bwf + bx;
         } else {
           const int mx = pp.tx * 8 + (bcol & 7);
-          valid = mx < mw;
-          blk = G.nY + (bcol >= 8 ? G.nC : 0) + (long long)pp.ty * mw + mx;
+          valid = mx < mwf;
+          blk = nYf + (bcol >= 8 ? nCf : 0) + (long long)pp.ty * mwf + mx;
         }
         dst[PIX ? 0 : nt][0] = dst[PIX ? 0 : nt][1] = u4v{0, 0, 0, 0};
         if (valid) {
@@ -734,12 +768,14 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
         if (!(kflags & K1F_NO_COLOUR)) colour_stage<RGB>(raw, L, c4, pr, lut, !(kflags & K1F_NO_LUT));
         wave_lds_sync();
         // ---- stream the wave's next tile into the freed raw buffer -----------
+        if (REG) skip_outside(tn);
         if (tn < tend) {
-          pn = tile_pos(G, tn);
+          pn = tpos(tn);
           issue_tile_dma(a, pn, lane, raw, doff);
         }
-      } else if (tn < tend) {
-        pn = tile_pos(G, tn);
+      } else {
+        if (REG) skip_outside(tn);
+        if (tn < tend) pn = tpos(tn);
       }
 
       // ---- 2. DCT on MFMA, one 16-block N-tile at a time ----------------------
@@ -797,14 +833,17 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
       // block (index inside the frame's coefficient space) of this lane's
       // column in N-tile nt; false for columns beyond the frame edge
       auto block_of = [&](const int nt, int &blk) -> bool {
+        const FGeom fg = frame_geom(G, fdims, p.f);  // REG only
+        const int bwf = REG ? fg.bw : bw, mwf = REG ? fg.mw : mw;
+        const int nYf = REG ? fg.nY : G.nY, nCf = REG ? fg.nC : G.nC;
         if (nt < 2) {
           const int bx = p.tx * 16 + bcol;
-          blk = (2 * p.ty + nt) * bw + bx;
-          return bx < bw;
+          blk = (2 * p.ty + nt) * bwf + bx;
+          return bx < bwf;
         }
         const int mx = p.tx * 8 + (bcol & 7);
-        blk = G.nY + (bcol >= 8 ? G.nC : 0) + p.ty * mw + mx;
-        return mx < mw;
+        blk = nYf + (bcol >= 8 ? nCf : 0) + p.ty * mwf + mx;
+        return mx < mwf;
       };
       auto finish = [&](const int nt, int (&o)[16]) {
         const int comp = nt == 2 ? 1 : 0;
@@ -854,7 +893,9 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
           int pred0 = 0;
           const bool first_pred = !PIX && a.seg_dc_inline;
           if (first_pred && valid && g == 0 && (comp == 1 ? (bcol & 7) : bcol) == 0) {
-            const int cstart = comp == 0 ? 0 : (bcol >= 8 ? G.nY + G.nC : G.nY);
+            const FGeom fg = frame_geom(G, fdims, p.f);  // REG only
+            const int nYf = REG ? fg.nY : G.nY, nCf = REG ? fg.nC : G.nC;
+            const int cstart = comp == 0 ? 0 : (bcol >= 8 ? nYf + nCf : nYf);
             pred0 = blk == cstart ? (a.dc_pred ? (int)a.dc_pred[p.f * 4 + (comp == 0 ? 0 : (bcol >= 8 ? 2 : 1))] : 0)
                                   : (int)a.dc[(long long)p.f * G.nblk + blk - 1];
           }
@@ -1047,7 +1088,6 @@ __global__ __launch_bounds__(256) void k_fix_blocks(K1Args a) {
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const Geom G = a.g;
-  const int bw = G.w >> 3, mw = G.w >> 4;
   const unsigned n = *a.fix_count;
   const int x = lane & 7, y = lane >> 3;
   // lane z's output coefficient: zigzag z = frequency (v, u) (encoder.c:38-46)
@@ -1057,14 +1097,16 @@ __global__ __launch_bounds__(256) void k_fix_blocks(K1Args a) {
     const uint32_t id = a.fix_list[e];
     const int f = (int)(id / (uint32_t)G.nblk), blk = (int)(id - (uint32_t)f * (uint32_t)G.nblk);
     const uint8_t *img = a.in + (long long)f * a.in_fs;
+    const FGeom fg = frame_geom(G, a.fdims, f);
+    const int bw = fg.bw, mw = fg.mw;
     int pv, comp;
-    if (blk < G.nY) {  // lane = pixel (x, y) of the block
+    if (blk < fg.nY) {  // lane = pixel (x, y) of the block
       comp = 0;
       const int bx = blk % bw, by = blk / bw;
       pv = y_ref(img + (long long)(8 * by + y) * a.pitch + (8 * bx + x) * 3, ib, ir);
     } else {
       comp = 1;
-      const int c = blk - G.nY, cr = c >= G.nC, m = cr ? c - G.nC : c;
+      const int c = blk - fg.nY, cr = c >= fg.nC, m = cr ? c - fg.nC : c;
       const int mx = m % mw, my = m / mw;
       const uint8_t *q = img + (long long)(16 * my + 2 * y) * a.pitch + (16 * mx + 2 * x) * 3;
       int sum = 0;
@@ -1104,13 +1146,15 @@ __global__ __launch_bounds__(256) void k_fix_blocks(K1Args a) {
 // DC differencing in place (encoder.c:168-177), for the drop-in rgb_to_dct
 // whose caller expects differenced DCs in the planes.
 // ===========================================================================
-__global__ void k_dc_diff(int16_t *coef, const int16_t *dc, Geom G, int nframes) {
+__global__ void k_dc_diff(int16_t *coef, const int16_t *dc, Geom G, int nframes, const int2 *fd) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   long long total = (long long)nframes * G.nblk;
   if (i >= total) return;
   const int f = (int)(i / G.nblk);
   const int j = (int)(i - (long long)f * G.nblk);
-  const bool first = j == 0 || j == G.nY || j == G.nY + G.nC;
+  const FGeom fg = frame_geom(G, fd, f);
+  if (j >= fg.nY + 2 * fg.nC) return;
+  const bool first = j == 0 || j == fg.nY || j == fg.nY + fg.nC;
   const int16_t prev = first ? 0 : dc[i - 1];
   coef[(long long)f * G.coef_fs + (long long)j * 64] = (int16_t)(dc[i] - prev);
 }
@@ -1122,20 +1166,24 @@ __global__ void k_dc_diff(int16_t *coef, const int16_t *dc, Geom G, int nframes)
 //   Cr s in [nsy+nsc, nseg):    likewise
 // so each scan's segments are contiguous and in scan order.
 // ===========================================================================
-__device__ __forceinline__ void seg_info(const Geom &G, int s, int &comp, int &first,
+// (fg: the frame's image; returns false for a canvas segment outside it)
+__device__ __forceinline__ bool seg_info(const Geom &G, const FGeom &fg, int s, int &comp, int &first,
                                          int &cstart, int &local) {
   if (s < G.nsy) {
     comp = 0;
     local = s;
     cstart = 0;
-    first = (s / G.tiles_x) * (G.w >> 3) + (s % G.tiles_x) * 16;
-  } else {
-    const int c = s - G.nsy;
-    comp = 1 + (c >= G.nsc);
-    local = comp == 1 ? c : c - G.nsc;
-    cstart = comp == 1 ? G.nY : G.nY + G.nC;
-    first = cstart + (local / G.tiles_x) * (G.w >> 4) + (local % G.tiles_x) * 8;
+    const int r = s / G.tiles_x, tx = s % G.tiles_x;
+    first = r * fg.bw + tx * 16;
+    return r < 2 * fg.rows && tx < fg.tiles_x;
   }
+  const int c = s - G.nsy;
+  comp = 1 + (c >= G.nsc);
+  local = comp == 1 ? c : c - G.nsc;
+  cstart = comp == 1 ? fg.nY : fg.nY + fg.nC;
+  const int r = local / G.tiles_x, tx = local % G.tiles_x;
+  first = cstart + r * fg.mw + tx * 8;
+  return r < fg.rows && tx < fg.tiles_x;
 }
 
 // ===========================================================================
@@ -1150,9 +1198,8 @@ __global__ __launch_bounds__(256) void k_seg_dc(EntArgs a) {
   const int s = (blockIdx.x - f * per) * 256 + threadIdx.x;
   if (threadIdx.x < 32) (&h[0][0])[threadIdx.x] = 0;
   __syncthreads();
-  if (s < a.g.nseg) {
-    int comp, first, cstart, local;
-    seg_info(a.g, s, comp, first, cstart, local);
+  int comp, first, cstart, local;
+  if (s < a.g.nseg && seg_info(a.g, frame_geom(a.g, a.fdims, f), s, comp, first, cstart, local)) {
     const long long fb = (long long)f * a.g.nblk;
     // a component's first block is predicted from 0 (encoder.c:168-177), or
     // from the previous band's last DC when the frame is split into bands
@@ -1871,7 +1918,8 @@ __global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
       for (int i = 1; i <= 16; i++) out[p++] = (uint8_t)hc[t].code_len_freq[i];
       for (int i = 0; i < n; i++) out[p++] = (uint8_t)hc[t].sym_sorted[i];
     }
-    const int W = a.g.w, H = a.g.h;
+    const FGeom fg = frame_geom(a.g, a.fdims, f);
+    const int W = fg.w, H = fg.h;
     const uint8_t sof[19] = {0xFF, 0xC0, 0x00, 0x11, 0x08, (uint8_t)(H >> 8), (uint8_t)H,
                              (uint8_t)(W >> 8), (uint8_t)W, 0x03, 0x01, 0x22, 0x00,
                              0x02, 0x11, 0x01, 0x03, 0x11, 0x01};
@@ -2011,6 +2059,21 @@ __global__ __launch_bounds__(256) void k_emit_write(EntArgs a) {
   }
 }
 
+// ---- region batches: each region (x, y, w, h) of one frame into its slot ---
+// (the top-left w x h of the slot, rows `pitch` bytes apart), as main.c:142-152
+// hands every region of a frame to rgb_to_dct(raw, .., dims[i]).  Workgroup
+// (row, region) copies one row of the region; rows beyond a region idle.
+__global__ __launch_bounds__(256) void k_gather_regions(uint8_t *dst, long long slot_bytes, int pitch,
+                                                        const uint8_t *src, long long src_pitch,
+                                                        const int4 *regions) {
+  const int4 r = regions[blockIdx.y];  // x, y, w, h
+  const int row = blockIdx.x;
+  if (row >= r.w) return;
+  const uint8_t *s = src + (long long)(r.y + row) * src_pitch + (long long)r.x * 3;
+  uint8_t *d = dst + (long long)blockIdx.y * slot_bytes + (long long)row * pitch;
+  for (int i = threadIdx.x; i < r.z * 3; i += 256) d[i] = s[i];
+}
+
 // ---- band assembly: OR a band's packed words into the frame's scan buffer ----
 __global__ void k_or_words(uint32_t *dst, const uint32_t *src, long long n) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2075,28 +2138,31 @@ hipError_t launch_colour_lut(uint32_t *lut, hipStream_t s) {
   return hipGetLastError();
 }
 // mode: K1M_* bits (see k_mcu_dct)
+template <int MODE>
+static void launch_k1_mode(const K1Args &a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((k_mcu_dct<MODE>), dim3(grid), dim3(64 * k1_waves<MODE>()), 0, s, a);
+}
 hipError_t launch_k1(const K1Args &a, int grid, int mode, hipStream_t s) {
+  if (a.rgb && a.fdims) return hipErrorInvalidValue;  // not instantiated (the API refuses it)
   switch (mode) {
     case K1M_COEF_OUT:
-      if (a.rgb)
-        hipLaunchKernelGGL((k_mcu_dct<K1M_COEF_OUT | K1M_RGB>), dim3(grid), dim3(64 * k1_waves<K1M_COEF_OUT>()), 0, s, a);
-      else
-        hipLaunchKernelGGL((k_mcu_dct<K1M_COEF_OUT>), dim3(grid), dim3(64 * k1_waves<K1M_COEF_OUT>()), 0, s, a);
+      if (a.rgb) launch_k1_mode<K1M_COEF_OUT | K1M_RGB>(a, grid, s);
+      else if (a.fdims) launch_k1_mode<K1M_COEF_OUT | K1M_REGIONS>(a, grid, s);
+      else launch_k1_mode<K1M_COEF_OUT>(a, grid, s);
       break;
     case K1M_TOK_OUT:
-      if (a.rgb)
-        hipLaunchKernelGGL((k_mcu_dct<K1M_TOK_OUT | K1M_RGB>), dim3(grid), dim3(64 * k1_waves<K1M_TOK_OUT>()), 0, s, a);
-      else
-        hipLaunchKernelGGL((k_mcu_dct<K1M_TOK_OUT>), dim3(grid), dim3(64 * k1_waves<K1M_TOK_OUT>()), 0, s, a);
+      if (a.rgb) launch_k1_mode<K1M_TOK_OUT | K1M_RGB>(a, grid, s);
+      else if (a.fdims) launch_k1_mode<K1M_TOK_OUT | K1M_REGIONS>(a, grid, s);
+      else launch_k1_mode<K1M_TOK_OUT>(a, grid, s);
       break;
     case K1M_COEF_OUT | K1M_TOK_OUT:
-      if (a.rgb)
-        hipLaunchKernelGGL((k_mcu_dct<K1M_COEF_OUT | K1M_TOK_OUT | K1M_RGB>), dim3(grid), dim3(256), 0, s, a);
-      else
-        hipLaunchKernelGGL((k_mcu_dct<K1M_COEF_OUT | K1M_TOK_OUT>), dim3(grid), dim3(256), 0, s, a);
+      if (a.rgb) launch_k1_mode<K1M_COEF_OUT | K1M_TOK_OUT | K1M_RGB>(a, grid, s);
+      else if (a.fdims) launch_k1_mode<K1M_COEF_OUT | K1M_TOK_OUT | K1M_REGIONS>(a, grid, s);
+      else launch_k1_mode<K1M_COEF_OUT | K1M_TOK_OUT>(a, grid, s);
       break;
     case K1M_COEF_IN | K1M_TOK_OUT:
-      hipLaunchKernelGGL((k_mcu_dct<K1M_COEF_IN | K1M_TOK_OUT>), dim3(grid), dim3(256), 0, s, a);
+      if (a.fdims) launch_k1_mode<K1M_COEF_IN | K1M_TOK_OUT | K1M_REGIONS>(a, grid, s);
+      else launch_k1_mode<K1M_COEF_IN | K1M_TOK_OUT>(a, grid, s);
       break;
     default: return hipErrorInvalidValue;
   }
@@ -2107,10 +2173,10 @@ hipError_t launch_seg_dc(const EntArgs &a, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t launch_dc_diff(int16_t *coef, const int16_t *dc, const Geom &g, int nframes,
-                          hipStream_t s) {
+                          const int2 *fd, hipStream_t s) {
   long long n = (long long)nframes * g.nblk;
   hipLaunchKernelGGL(k_dc_diff, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, coef, dc, g,
-                     nframes);
+                     nframes, fd);
   return hipGetLastError();
 }
 hipError_t launch_tables(const EntArgs &a, hipStream_t s) {
@@ -2154,6 +2220,13 @@ hipError_t launch_emit(const EntArgs &a, hipStream_t s) {
   hipLaunchKernelGGL(k_emit_count, dim3(a.nframes * 3 * EMIT_SLOTS), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_emit_scan, dim3(a.nframes), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_emit_write, dim3(a.nframes * 3 * EMIT_SLOTS), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_gather_regions(uint8_t *dst, long long slot_bytes, int pitch, const uint8_t *src,
+                                 long long src_pitch, const int4 *regions, int n, int max_h,
+                                 hipStream_t s) {
+  hipLaunchKernelGGL(k_gather_regions, dim3(max_h, n), dim3(256), 0, s, dst, slot_bytes, pitch, src,
+                     src_pitch, regions);
   return hipGetLastError();
 }
 hipError_t launch_mfma_probe(const int4 *A, const int4 *B, int4 *D, hipStream_t s) {

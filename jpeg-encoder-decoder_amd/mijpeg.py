@@ -31,6 +31,8 @@ EXPORTS = [
     "mij_batch_set_rgb", "mij_ppm_header", "mij_ppm_read",
     "mij_stream_create", "mij_stream_destroy", "mij_stream_encode_files",
     "mij_stream_encode_frames", "mij_stream_stats",
+    "mij_batch_set_frame_dims", "mij_batch_gather_regions", "mij_batch_upload_regions",
+    "mij_encode_regions",
 ]
 
 
@@ -131,6 +133,14 @@ def load() -> C.CDLL:
     lib.mij_stream_encode_frames.argtypes = [p, C.POINTER(p), i, C.POINTER(p), C.POINTER(sz),
                                              C.POINTER(sz)]
     lib.mij_stream_stats.argtypes = [p, p, i]
+    try:
+        lib.mij_batch_set_frame_dims.argtypes = [p, p, i]
+        lib.mij_batch_gather_regions.argtypes = [p, p, C.c_longlong, i, i, p, i]
+        lib.mij_batch_upload_regions.argtypes = [p, p, i, i, p, i]
+        lib.mij_encode_regions.argtypes = [p, i, i, p, i, i, p, sz, p]
+    except AttributeError:
+        if not os.environ.get("MIJ_LIB"):  # older builds only in A/B timing runs
+            raise
     _lib = lib
     return lib
 
@@ -194,6 +204,29 @@ def write_jpg(Y, Cb, Cr, region, tables) -> bytes:
     return out[:n].tobytes()
 
 
+def _areas(regions):
+    arr = (Area * len(regions))(*[Area(*map(int, r)) for r in regions])
+    return arr
+
+
+def encode_regions(frame_bgr: np.ndarray, regions, quality: int = 50) -> list:
+    """mij_encode_regions: every (x, y, w, h) region of a BGR frame to its own
+    JPEG in one launch sequence (main.c:142-155)."""
+    lib = load()
+    frame_bgr = np.ascontiguousarray(frame_bgr, np.uint8)
+    H, W = frame_bgr.shape[:2]
+    cap = sum(max_jpg_bytes(r[2], r[3]) for r in regions)
+    out = np.zeros(max(cap, 1), np.uint8)
+    lens = (C.c_size_t * len(regions))()
+    _check(lib.mij_encode_regions(_ptr(frame_bgr), W, H, _areas(regions), len(regions), quality,
+                                  _ptr(out), out.size, lens), "mij_encode_regions")
+    res, off = [], 0
+    for n in lens:
+        res.append(out[off:off + n].tobytes())
+        off += n
+    return res
+
+
 def encode(frame_bgr: np.ndarray, quality: int = 50, region=None) -> bytes:
     """mij_encode: whole path host->host."""
     lib = load()
@@ -218,6 +251,7 @@ class Batch:
         self.lib = load()
         self.w, self.h, self.max_frames = w, h, max_frames
         self.h_ = self.lib.mij_batch_create(device, w, h, max_frames, quality)
+        self.fdims = None  # per-frame (w, h) of a region batch
         if not self.h_:
             raise MijError(f"mij_batch_create failed: "
                            f"{self.lib.mij_strerror(self.lib.mij_last_error()).decode()}")
@@ -241,6 +275,28 @@ class Batch:
     def set_rgb(self, on: bool) -> None:
         """frames in R, G, B byte order (PPM) instead of the encoder's B, G, R"""
         _check(self.lib.mij_batch_set_rgb(self.h_, int(on)), "set_rgb")
+
+    def set_frame_dims(self, dims) -> None:
+        """per-frame (w, h) of a region batch; None restores the batch geometry"""
+        if dims is None:
+            _check(self.lib.mij_batch_set_frame_dims(self.h_, None, 0), "set_frame_dims")
+            self.fdims = None
+            return
+        wh = np.ascontiguousarray(np.asarray(dims, np.int32).reshape(-1, 2))
+        _check(self.lib.mij_batch_set_frame_dims(self.h_, _ptr(wh), wh.shape[0]), "set_frame_dims")
+        self.fdims = [tuple(map(int, d)) for d in wh]
+
+    def upload_regions(self, frame_bgr: np.ndarray, regions) -> None:
+        frame_bgr = np.ascontiguousarray(frame_bgr, np.uint8)
+        H, W = frame_bgr.shape[:2]
+        _check(self.lib.mij_batch_upload_regions(self.h_, _ptr(frame_bgr), W, H, _areas(regions),
+                                                 len(regions)), "upload_regions")
+        self.fdims = [(int(r[2]), int(r[3])) for r in regions]
+
+    def gather_regions(self, dev_ptr: int, pitch: int, frame_w: int, frame_h: int, regions) -> None:
+        _check(self.lib.mij_batch_gather_regions(self.h_, dev_ptr, pitch, frame_w, frame_h,
+                                                 _areas(regions), len(regions)), "gather_regions")
+        self.fdims = [(int(r[2]), int(r[3])) for r in regions]
 
     def upload(self, frames_bgr: np.ndarray, first: int = 0) -> None:
         frames_bgr = np.ascontiguousarray(frames_bgr, np.uint8)
@@ -273,9 +329,10 @@ class Batch:
         return np.array(arr[:], np.int64)
 
     def coefs(self, frame: int, diffed: bool = True):
-        Y = np.zeros(self.w * self.h, np.int16)
-        Cb = np.zeros(self.w * self.h // 4, np.int16)
-        Cr = np.zeros(self.w * self.h // 4, np.int16)
+        w, h = self.fdims[frame] if self.fdims and frame < len(self.fdims) else (self.w, self.h)
+        Y = np.zeros(w * h, np.int16)
+        Cb = np.zeros(w * h // 4, np.int16)
+        Cr = np.zeros(w * h // 4, np.int16)
         _check(self.lib.mij_batch_coefs(self.h_, frame, _ptr(Y), _ptr(Cb), _ptr(Cr),
                                         int(diffed)), "coefs")
         return Y, Cb, Cr
