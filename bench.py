@@ -60,10 +60,14 @@ def parse():
     ap.add_argument("--coef-launches", type=int, default=3,
                     help="extra launches of the coefficient-output K1 variant after the timed "
                          "region, for its own 6 B/px roofline line (0 disables)")
-    ap.add_argument("--workload", choices=["config3", "config4"], default="config3",
+    ap.add_argument("--workload", choices=["config3", "config4", "regions"], default="config3",
                     help="config4: a stream of 7680x4320 frames, each split into MCU-row bands "
                          "over the ranks with the RCCL exchange steps (strong scaling)")
     ap.add_argument("--frames4", type=int, default=8, help="config4 frames per step")
+    ap.add_argument("--regions", type=int, default=100,
+                    help="regions workload: rectangles per frame (main.c's diffDims holds up to 100)")
+    ap.add_argument("--region-frame", default="1920x1080",
+                    help="regions workload: the frame the rectangles are cut from")
     ap.add_argument("--verify", type=int, default=2,
                     help="frames re-checked against the oracle after timing")
     return ap.parse_args()
@@ -150,6 +154,96 @@ def run_config4(args, world, rank, local, dist):
     band.close()
     if full is not None:
         full.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def region_set(W, H, n, seed=7):
+    """n rectangles (x, y, w, h) with w, h multiples of 16 (brain.c:244-261
+    enlargeAdjust makes them so), 16..512 px per side, inside a W x H frame."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        w = 16 * int(rng.integers(1, min(32, W // 16) + 1))
+        h = 16 * int(rng.integers(1, min(32, H // 16) + 1))
+        out.append((int(rng.integers(0, W - w + 1)), int(rng.integers(0, H - h + 1)), w, h))
+    return out
+
+
+def run_regions(args, world, rank, local, dist):
+    """SURVEY §8(f) rank 2, the reference's own workload shape (main.c:142-155):
+    every step encodes --regions rectangles of one device-resident frame, each
+    to its own JFIF, through one region batch (one gather launch + one encode
+    launch sequence).  Frame-parallel over ranks (each rank its own frame)."""
+    import torch
+    W, H = map(int, args.region_frame.split("x"))
+    gpu = 0 if dist is not None and dist.get_backend() != "nccl" else local
+    torch.cuda.set_device(gpu)
+    frame = np.ascontiguousarray(recipes.config3_frame(rank, H, W) if W <= 3840 and H <= 2160
+                                 else recipes.config4_frame(rank, H, W))
+    regions = region_set(W, H, args.regions, 7 + rank)
+    cw, ch = max(r[2] for r in regions), max(r[3] for r in regions)
+    batch = mijpeg.Batch(cw, ch, len(regions), args.quality, device=gpu)
+    dframe = torch.from_numpy(frame).to(f"cuda:{gpu}")
+    torch.cuda.synchronize()
+
+    def step():
+        batch.gather_regions(dframe.data_ptr(), W * 3, W, H, regions)
+        batch.encode(len(regions))
+
+    for _ in range(args.warmup):
+        step()
+    batch.sync()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    batch.sync()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
+    px = sum(r[2] * r[3] for r in regions)
+    el, px_all = sharding.reduce_timing(el, px * args.steps, dist, dist_device(dist, local))
+    verified = 0
+    if args.verify:
+        import oracle as O
+        for i in range(min(len(regions), 4 * args.verify)):
+            if batch.output(i) != O.cref_encode(frame, args.quality, regions[i]):
+                raise SystemExit(f"bench regions: region {i} differs from the oracle")
+            verified += 1
+    res = {
+        "metric": "Mpixels/s encoded (device-resident BGR888 -> JFIF bytes)",
+        "value": round(px_all / el / 1e6, 1), "unit": "Mpixels/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int8",
+        "data": "synthetic: config-3 recipe frame, seeded rectangles",
+        "config": {"workload": f"regions: {len(regions)} rectangles (16..512 px a side, "
+                               f"{px / 1e6:.2f} Mpixels) of one {W}x{H} frame per step, each its own JFIF "
+                               f"(main.c:142-155), one region batch",
+                   "regions": len(regions), "frame": f"{W}x{H}", "region_pixels": px,
+                   "quality": args.quality, "parallelism": f"frame-parallel x{world}"},
+        "regions_per_s": round(len(regions) * args.steps * world / el, 1),
+        "verified_regions": verified,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle as O
+        use_ref = O.ref_available()
+        n, npx, t0 = 0, 0, time.perf_counter()
+        while time.perf_counter() - t0 < args.cpu_seconds or n < len(regions):
+            r = regions[n % len(regions)]
+            (O.ref_stages(frame, r) if use_ref else O.cref_encode(frame, args.quality, r))
+            n += 1
+            npx += r[2] * r[3]
+        el_c = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(npx / el_c / 1e6, 3), "unit": "Mpixels/s", "cores": 1,
+                               "kind": "reference" if use_ref else "port",
+                               "sample": f"{n} region encodes of the same rectangles, {el_c:.1f} s, "
+                                         f"1 thread, main.c's per-region call sequence"}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    batch.close()
     if dist is not None:
         dist.destroy_process_group()
 
@@ -268,6 +362,8 @@ def main():
     world, rank, local, dist, torch = dist_setup(args)
     if args.workload == "config4":
         return run_config4(args, world, rank, local, dist)
+    if args.workload == "regions":
+        return run_regions(args, world, rank, local, dist)
     W, H, F = args.width, args.height, args.frames
     frames = make_frames(args, rank)
     gpu = 0 if dist is not None and dist.get_backend() != "nccl" else local
