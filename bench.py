@@ -60,9 +60,10 @@ def parse():
     ap.add_argument("--coef-launches", type=int, default=3,
                     help="extra launches of the coefficient-output K1 variant after the timed "
                          "region, for its own 6 B/px roofline line (0 disables)")
-    ap.add_argument("--workload", choices=["config3", "config4", "regions"], default="config3",
+    ap.add_argument("--workload", choices=["config3", "config4", "regions", "detect"], default="config3",
                     help="config4: a stream of 7680x4320 frames, each split into MCU-row bands "
                          "over the ranks with the RCCL exchange steps (strong scaling)")
+    ap.add_argument("--detect-frames", type=int, default=8, help="detect: distinct frames cycled")
     ap.add_argument("--frames4", type=int, default=8, help="config4 frames per step")
     ap.add_argument("--regions", type=int, default=100,
                     help="regions workload: rectangles per frame (main.c's diffDims holds up to 100)")
@@ -248,6 +249,130 @@ def run_regions(args, world, rank, local, dist):
         dist.destroy_process_group()
 
 
+def run_detect(args, world, rank, local, dist):
+    """the reference's whole per-frame loop (main.c:136-163)
+    on a device-resident stream of --detect-frames distinct frames of
+    --region-frame size: one detector kernel (4x4 subsample + weighted colour
+    distance vs the stored frame, brain.c:16-45/:184-195) + the host area
+    joining (brain.c:104-233), then every detected area encoded to its own
+    JFIF through one region batch, then store.  Frame-parallel over ranks."""
+    import torch
+    W, H = map(int, args.region_frame.split("x"))
+    gpu = 0 if dist is not None and dist.get_backend() != "nccl" else local
+    torch.cuda.set_device(gpu)
+    nf = args.detect_frames
+    frames = [np.ascontiguousarray(recipes.detect_scene(500 + 97 * rank + i, W, H, "objects")[1])
+              for i in range(nf)]
+    dframes = [torch.from_numpy(f).to(f"cuda:{gpu}") for f in frames]
+    det = mijpeg.Detector(W, H, device=gpu)
+    torch.cuda.synchronize()
+    # one pass to size the region batch (detection is deterministic)
+    plan = []
+    det.subsample(dframes[-1].data_ptr())
+    det.store()
+    for f in dframes:
+        plan.append(det.step(f.data_ptr())[1])
+        det.store()
+    cw = max([a[2] for areas in plan for a in areas] + [16])
+    ch = max([a[3] for areas in plan for a in areas] + [16])
+    batch = mijpeg.Batch(cw, ch, max(max(len(a) for a in plan), 1), args.quality, device=gpu)
+
+    def step(i):
+        f = dframes[i % nf]
+        n, areas = det.step(f.data_ptr())
+        if n:
+            batch.gather_regions(f.data_ptr(), 3 * W, W, H, areas)
+            batch.encode(n)
+        det.store()
+        return areas
+
+    for i in range(args.warmup):
+        step(i)
+    batch.sync()
+    if dist is not None:
+        dist.barrier()
+    nreg = 0
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        nreg += len(step(args.warmup + i))
+    batch.sync()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
+    el, px_all = sharding.reduce_timing(el, W * H * args.steps, dist, dist_device(dist, local))
+    # the detector kernel alone, HIP events on the detector's own stream
+    ds = torch.cuda.ExternalStream(det.stream())
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 50
+    e0.record(ds)
+    for i in range(reps):
+        det.launch(dframes[i % nf].data_ptr())
+    e1.record(ds)
+    e1.synchronize()
+    k_ms = e0.elapsed_time(e1) / reps
+    sw, sh = W // 4, H // 4
+    k_bytes = 3 * W * H + 2 * 4 * sw * sh + 8 * ((sw + 63) // 64) * sh
+    # verification: the last step's areas and a few JFIFs against the oracle
+    import oracle as O
+    last = (args.warmup + args.steps - 1) % nf
+    prev = O.cref_subsample(frames[(last - 1) % nf])
+    want = O.cref_compare(O.cref_subsample(frames[last]), prev, W, H)
+    got_areas = plan[last]
+    if (len(got_areas), got_areas) != (want[0], want[1]):
+        raise SystemExit("bench detect: areas differ from the oracle")
+    verified = 0
+    if args.verify and want[0]:
+        n, areas = want
+        for i in range(min(n, 4 * args.verify)):
+            if batch.output(i) != O.cref_encode(frames[last], args.quality, areas[i]):
+                raise SystemExit(f"bench detect: area {i} differs from the oracle")
+            verified += 1
+    res = {
+        "metric": "Mpixels/s encoded (device-resident BGR888 -> JFIF bytes)",
+        "value": round(px_all / el / 1e6, 1), "unit": "Mpixels/s (frame pixels through detect+encode)",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: tests/recipes.detect_scene moving-object frames",
+        "config": {"workload": f"detect: main.c:136-163 loop on {W}x{H} frames -- detector kernel, "
+                               f"host area joining, every area its own JFIF (one region batch), store",
+                   "frame": f"{W}x{H}", "distinct_frames": nf, "quality": args.quality,
+                   "parallelism": f"frame-parallel x{world}"},
+        "frames_per_s": round(args.steps * world / el, 1),
+        "areas_per_frame": round(nreg / args.steps, 2),
+        "roofline": {"bound": "hbm", "kernel": "k_detect<true> (4x4 subsample + compare + ballot mask)",
+                     "achieved": round(k_bytes / k_ms / 1e6, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(k_bytes / k_ms / 1e6 / HBM_PEAK_GBS, 4), "traffic": None,
+                     "ms_per_launch": round(k_ms, 4), "algorithmic_bytes_per_launch": k_bytes},
+        "verified_areas": verified,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        use_ref = O.ref_brain_available() and O.ref_available()
+        sub_fn = O.ref_subsample if use_ref else O.cref_subsample
+        cmp_fn = O.ref_compare if use_ref else O.cref_compare
+        n, t0 = 0, time.perf_counter()
+        saved = sub_fn(frames[-1])
+        while time.perf_counter() - t0 < args.cpu_seconds or n < 1:
+            f = frames[n % nf]
+            sub = sub_fn(f)
+            cnt, areas = cmp_fn(sub, saved, W, H)
+            for a in areas[:cnt]:
+                (O.ref_stages(f, a) if use_ref else O.cref_encode(f, args.quality, a))
+            saved = sub
+            n += 1
+        el_c = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(n * W * H / el_c / 1e6, 3), "unit": "Mpixels/s", "cores": 1,
+                               "kind": "reference" if use_ref else "port",
+                               "sample": f"{n} frames through brain.c subsample/compare + encoder.c per "
+                                         f"area, {el_c:.1f} s, 1 thread"}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    batch.close()
+    det.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def make_frames(args, rank):
     """Distinct config-3 frames (recipe in tests/recipes.py), rank-offset so
     ranks encode different content."""
@@ -364,6 +489,8 @@ def main():
         return run_config4(args, world, rank, local, dist)
     if args.workload == "regions":
         return run_regions(args, world, rank, local, dist)
+    if args.workload == "detect":
+        return run_detect(args, world, rank, local, dist)
     W, H, F = args.width, args.height, args.frames
     frames = make_frames(args, rank)
     gpu = 0 if dist is not None and dist.get_backend() != "nccl" else local

@@ -265,6 +265,63 @@ int mij_colour_lut(uint32_t *out);
 /* name of the code object target the library was built for ("gfx950") */
 const char *mij_build_target(void);
 
+/* ---- change detector (reference main/brain.c) ------
+ * The reference's per-frame loop (main.c:136-163) subsamples the camera frame
+ * 4x4 (brain.c:16-45), compares it with the stored subsampled frame
+ * (brain.c:104-233: weighted colour distance > 600 per subsampled pixel,
+ * runs of differing pixels joined into at most 100 areas, enlarged to
+ * multiples of 16 in frame pixels) and encodes each area.  Here the
+ * subsample and the per-pixel test run as one HIP kernel over a
+ * device-resident frame that writes one bit per subsampled pixel; the run
+ * joining, which is sequential in the reference and keeps its quirks (see
+ * DESIGN.md), runs on the host over the runs of that bit mask. */
+
+/* include/structs.h:20-22 */
+typedef struct {
+    int beg, end, row, done;
+} pair_t;
+
+typedef struct mij_detector mij_detector;
+/* frame geometry: width and height multiples of 4 (the reference: 320x240);
+ * the stored plane starts as zeros, like main.c:33's static `saved` */
+mij_detector *mij_detector_create(int device, int width, int height);
+void mij_detector_destroy(mij_detector *d);
+/* brain.c:16-45 on a device BGR frame (rows pitch bytes apart, pitch and
+ * pointer 4-byte aligned) into the detector's current plane */
+int mij_detector_subsample(mij_detector *d, const void *d_frame, long long pitch);
+/* brain.c:104-233: current plane vs stored plane -> outs[100], *count */
+int mij_detector_compare(mij_detector *d, area_t outs[100], int *count);
+/* subsample + compare in one kernel launch (main.c:140-143) */
+int mij_detector_step(mij_detector *d, const void *d_frame, long long pitch, area_t outs[100],
+                      int *count);
+/* the step's kernel alone, asynchronous on the detector's stream (the mask
+ * stays on the device; for timing) */
+int mij_detector_launch(mij_detector *d, const void *d_frame, long long pitch);
+/* brain.c:53-60 / main.c:161: stored plane := current plane (device copy) */
+int mij_detector_store(mij_detector *d);
+/* host BGR frame (height rows pitch bytes apart; pitch 0 = 3*width) into the
+ * detector's frame buffer, same pitch; *d_frame receives its device address */
+int mij_detector_upload(mij_detector *d, const uint8_t *bgr, long long pitch, const void **d_frame);
+/* plane 0 = current, 1 = stored, in the reference's layout (R, G, B bytes per
+ * subsampled pixel, (width/4)*(height/4)*3 bytes): read back / set */
+int mij_detector_get_plane(mij_detector *d, int which, uint8_t *rgb);
+int mij_detector_set_plane(mij_detector *d, int which, const uint8_t *rgb);
+/* the kernel's bit mask of the last compare: one row of `words` 64-bit words
+ * per subsampled row (bit x%64 of word x/64 = pixel x differs) */
+int mij_detector_mask(mij_detector *d, unsigned long long *dst, size_t cap_words, int *words);
+void *mij_detector_stream(mij_detector *d);
+
+/* Drop-in entry points of include/brain.h:7-10, on frames of
+ * mij_set_input_stride() x mij_set_frame_height() pixels (define.h:3-4,
+ * 320x240 by default).  subsample writes the PPM copy to f when f is not
+ * NULL (brain.c:22, :29-42).  compare uses differences (2 rows of WIDTH/8
+ * runs, main.c:35) as scratch like the reference.  Errors: mij_last_error. */
+int mij_set_frame_height(int height);
+void subsample(FILE *f, uint8_t *in, uint8_t *out);
+void store(uint8_t *in, uint8_t *saved);
+uint8_t compare(uint8_t *in, uint8_t *saved, area_t *outs, pair_t (*differences)[]);
+void enlargeAdjust(area_t *a);
+
 #ifdef __cplusplus
 }
 #endif

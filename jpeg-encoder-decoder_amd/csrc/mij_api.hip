@@ -868,6 +868,13 @@ static mij_batch *ctx_for(int w, int h, int quality) {
   return g_ctx;
 }
 
+// for the other host translation units (the drop-in detector, mij_detect.hip)
+int mij_drop_stride() {
+  std::lock_guard<std::mutex> l(g_mu);
+  return g_stride;
+}
+int mij_drop_device() { return drop_device(); }
+
 extern "C" int mij_set_input_stride(int stride_px) {
   if (stride_px < 16) return fail(MIJ_EINVAL, "stride %d", stride_px);
   std::lock_guard<std::mutex> l(g_mu);

@@ -14,3 +14,7 @@ void mij_clear_error();
 int mij_batch_upload_async(mij_batch *b, const uint8_t *host, int nframes);
 int mij_batch_lengths_async(mij_batch *b, uint64_t *h_len, int *h_err, int nframes);
 int mij_batch_output_async(mij_batch *b, int frame, uint8_t *dst, size_t n);
+
+// drop-in state shared with the detector's drop-in calls (mij_detect.hip)
+int mij_drop_stride();   // define.h:3 WIDTH, as set by mij_set_input_stride
+int mij_drop_device();   // MIJ_DEVICE or 0

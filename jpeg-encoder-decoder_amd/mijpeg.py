@@ -28,6 +28,11 @@ EXPORTS = [
     "mij_band_analyze", "mij_band_histograms", "mij_band_tables", "mij_band_pack", "mij_band_words",
     "mij_assemble_begin", "mij_assemble_words", "mij_assemble_end",
     "mij_probe_mfma", "mij_colour_lut", "mij_build_target",
+    # change detector (reference include/brain.h:7-10 drop-in + extensions)
+    "subsample", "store", "compare", "enlargeAdjust", "mij_set_frame_height",
+    "mij_detector_create", "mij_detector_destroy", "mij_detector_subsample", "mij_detector_compare",
+    "mij_detector_step", "mij_detector_launch", "mij_detector_store", "mij_detector_upload", "mij_detector_get_plane",
+    "mij_detector_set_plane", "mij_detector_mask", "mij_detector_stream",
     "mij_batch_set_rgb", "mij_ppm_header", "mij_ppm_read",
     "mij_stream_create", "mij_stream_destroy", "mij_stream_encode_files",
     "mij_stream_encode_frames", "mij_stream_stats",
@@ -134,6 +139,29 @@ def load() -> C.CDLL:
                                              C.POINTER(sz)]
     lib.mij_stream_stats.argtypes = [p, p, i]
     try:
+        lib.mij_detector_create.restype = p
+        lib.mij_detector_create.argtypes = [i, i, i]
+        lib.mij_detector_destroy.argtypes = [p]
+        lib.mij_detector_subsample.argtypes = [p, p, C.c_longlong]
+        lib.mij_detector_compare.argtypes = [p, p, C.POINTER(i)]
+        lib.mij_detector_step.argtypes = [p, p, C.c_longlong, p, C.POINTER(i)]
+        lib.mij_detector_store.argtypes = [p]
+        lib.mij_detector_launch.argtypes = [p, p, C.c_longlong]
+        lib.mij_detector_upload.argtypes = [p, p, C.c_longlong, C.POINTER(p)]
+        lib.mij_detector_get_plane.argtypes = [p, i, p]
+        lib.mij_detector_set_plane.argtypes = [p, i, p]
+        lib.mij_detector_mask.argtypes = [p, p, sz, C.POINTER(i)]
+        lib.mij_detector_stream.restype = p
+        lib.mij_detector_stream.argtypes = [p]
+        lib.mij_set_frame_height.argtypes = [i]
+        lib.subsample.restype = None
+        lib.subsample.argtypes = [p, p, p]
+        lib.store.restype = None
+        lib.store.argtypes = [p, p]
+        lib.compare.restype = C.c_uint8
+        lib.compare.argtypes = [p, p, p, p]
+        lib.enlargeAdjust.restype = None
+        lib.enlargeAdjust.argtypes = [p]
         lib.mij_batch_set_frame_dims.argtypes = [p, p, i]
         lib.mij_batch_gather_regions.argtypes = [p, p, C.c_longlong, i, i, p, i]
         lib.mij_batch_upload_regions.argtypes = [p, p, i, i, p, i]
@@ -505,3 +533,134 @@ def colour_lut() -> np.ndarray:
     out = np.zeros(3 * 1024, np.uint32)
     _check(load().mij_colour_lut(_ptr(out)), "colour_lut")
     return out.reshape(3, 1024)
+
+
+# ---- change detector (reference main/brain.c) ------
+
+class Pair(C.Structure):
+    """pair_t, reference include/structs.h:20-22."""
+    _fields_ = [("beg", C.c_int), ("end", C.c_int), ("row", C.c_int), ("done", C.c_int)]
+
+
+def _area_list(outs, n: int) -> list:
+    return [(a.x, a.y, a.w, a.h) for a in outs[:max(0, min(n, 100))]]
+
+
+class Detector:
+    """Device-resident change detector over frames of w x h BGR pixels.
+
+    step(frame) = the reference's subsample + compare (main.c:140-143) in one
+    kernel launch plus the host-side area joining; store() = main.c:161.
+    Returns (count, areas) with the count the reference's compare returns."""
+
+    def __init__(self, w: int, h: int, device: int = 0):
+        self.lib = load()
+        self.w, self.h = w, h
+        self.h_ = self.lib.mij_detector_create(device, w, h)
+        if not self.h_:
+            raise MijError("mij_detector_create failed: "
+                           f"{self.lib.mij_strerror(self.lib.mij_last_error()).decode()}")
+        self._outs = (Area * 100)()
+
+    def close(self) -> None:
+        if self.h_:
+            self.lib.mij_detector_destroy(self.h_)
+            self.h_ = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, frame_bgr: np.ndarray, pitch: int = 0) -> int:
+        """Copies a host frame ((h, w, 3), or (h, pitch) bytes rows) to the
+        detector's frame buffer; returns its device address."""
+        f = np.ascontiguousarray(frame_bgr, np.uint8)
+        if pitch:
+            assert f.shape == (self.h, pitch), f.shape
+        else:
+            assert f.shape == (self.h, self.w, 3), f.shape
+        ptr = C.c_void_p()
+        _check(self.lib.mij_detector_upload(self.h_, _ptr(f), pitch, C.byref(ptr)), "detector_upload")
+        return ptr.value
+
+    def subsample(self, dev_ptr: int, pitch: int | None = None) -> None:
+        _check(self.lib.mij_detector_subsample(self.h_, dev_ptr, pitch or 3 * self.w),
+               "detector_subsample")
+
+    def compare(self):
+        n = C.c_int()
+        _check(self.lib.mij_detector_compare(self.h_, self._outs, C.byref(n)), "detector_compare")
+        return n.value, _area_list(self._outs, n.value)
+
+    def step(self, dev_ptr: int, pitch: int | None = None):
+        n = C.c_int()
+        _check(self.lib.mij_detector_step(self.h_, dev_ptr, pitch or 3 * self.w, self._outs,
+                                          C.byref(n)), "detector_step")
+        return n.value, _area_list(self._outs, n.value)
+
+    def launch(self, dev_ptr: int, pitch: int | None = None) -> None:
+        """The step's kernel alone, asynchronous (timing)."""
+        _check(self.lib.mij_detector_launch(self.h_, dev_ptr, pitch or 3 * self.w), "detector_launch")
+
+    def stream(self) -> int:
+        return int(self.lib.mij_detector_stream(self.h_) or 0)
+
+    def store(self) -> None:
+        _check(self.lib.mij_detector_store(self.h_), "detector_store")
+
+    def plane(self, which: int = 0) -> np.ndarray:
+        out = np.zeros((self.h // 4, self.w // 4, 3), np.uint8)
+        _check(self.lib.mij_detector_get_plane(self.h_, which, _ptr(out)), "detector_get_plane")
+        return out
+
+    def set_plane(self, which: int, rgb: np.ndarray) -> None:
+        rgb = np.ascontiguousarray(rgb, np.uint8)
+        assert rgb.shape == (self.h // 4, self.w // 4, 3), rgb.shape
+        _check(self.lib.mij_detector_set_plane(self.h_, which, _ptr(rgb)), "detector_set_plane")
+
+    def mask(self) -> np.ndarray:
+        """Bit mask of the last compare as a bool array (h/4, w/4)."""
+        words = C.c_int()
+        _check(self.lib.mij_detector_mask(self.h_, None, 0, C.byref(words)), "detector_mask")
+        m = np.zeros((self.h // 4, words.value), np.uint64)
+        _check(self.lib.mij_detector_mask(self.h_, _ptr(m), m.size, C.byref(words)), "detector_mask")
+        bits = np.unpackbits(m.view(np.uint8).reshape(self.h // 4, -1), axis=1, bitorder="little")
+        return bits[:, :self.w // 4].astype(bool)
+
+
+def drop_in_subsample(frame_bgr: np.ndarray) -> np.ndarray:
+    """brain.h:7 subsample() through the drop-in entry point (f = NULL)."""
+    lib = load()
+    f = np.ascontiguousarray(frame_bgr, np.uint8)
+    H, W = f.shape[:2]
+    _check(lib.mij_set_input_stride(W), "set_input_stride")
+    _check(lib.mij_set_frame_height(H), "set_frame_height")
+    out = np.zeros((H // 4, W // 4, 3), np.uint8)
+    lib.subsample(None, _ptr(f), _ptr(out))
+    _check(lib.mij_last_error(), "subsample")
+    return out
+
+
+def drop_in_compare(sub: np.ndarray, saved: np.ndarray, W: int, H: int):
+    """brain.h:9 compare() through the drop-in entry point."""
+    lib = load()
+    _check(lib.mij_set_input_stride(W), "set_input_stride")
+    _check(lib.mij_set_frame_height(H), "set_frame_height")
+    sub = np.ascontiguousarray(sub, np.uint8)
+    saved = np.ascontiguousarray(saved, np.uint8)
+    outs = (Area * 100)()
+    diffs = (Pair * (2 * (W // 8)))()
+    n = lib.compare(_ptr(sub), _ptr(saved), outs, diffs)
+    _check(lib.mij_last_error(), "compare")
+    return int(n), _area_list(outs, int(n))
+
+
+def drop_in_enlarge_adjust(area, W: int, H: int):
+    lib = load()
+    _check(lib.mij_set_input_stride(W), "set_input_stride")
+    _check(lib.mij_set_frame_height(H), "set_frame_height")
+    a = Area(*area)
+    lib.enlargeAdjust(C.byref(a))
+    return (a.x, a.y, a.w, a.h)

@@ -444,3 +444,185 @@ size_t cref_encode(const uint8_t *bgr, int stride_px, cref_area d, int quality,
     free(Y); free(Cb); free(Cr); free(t);
     return n;
 }
+
+/* ======================================================================== */
+/* Change detector: main/brain.c                                            */
+/* ======================================================================== */
+
+/* brain.c:16-45.  Sums of 16 bytes (uint16 in the reference) floored by 16;
+ * the output is R, G, B (R = in[+2] of the BGR input). */
+void cref_subsample(const uint8_t *bgr, int w, int h, uint8_t *sub) {
+    int sw = w / 4, sh = h / 4;
+    for (int sy = 0; sy < sh; sy++)
+        for (int sx = 0; sx < sw; sx++)
+            for (int c = 0; c < 3; c++) {
+                unsigned acc = 0;
+                for (int r = 0; r < 4; r++)
+                    for (int k = 0; k < 4; k++)
+                        acc += bgr[3 * ((size_t)(4 * sy + r) * w + 4 * sx + k) + (2 - c)];
+                sub[3 * ((size_t)sy * sw + sx) + c] = (uint8_t)(acc / 16);
+            }
+}
+
+/* brain.c:184-195: the weighted colour distance is evaluated in FP64 in the
+ * reference; every intermediate is an exact dyadic rational there
+ * (d^2 * (2 + cR/256) with cR = (a+b)/2), so the integer form below is the
+ * same value: floor(d^2 (1024+s) / 512), 4 d^2, floor(d^2 (1534-s) / 512),
+ * s = a_R + b_R.  The deltas go through uint32 (two's complement squares). */
+static int cref_pixel_differs(const uint8_t *a, const uint8_t *b) {
+    uint32_t s = (uint32_t)a[0] + b[0];
+    uint32_t dr = (uint32_t)((int)a[0] - (int)b[0]);
+    uint32_t dg = (uint32_t)((int)a[1] - (int)b[1]);
+    uint32_t db = (uint32_t)((int)a[2] - (int)b[2]);
+    dr *= dr; dg *= dg; db *= db;
+    uint32_t t = (uint32_t)(((uint64_t)dr * (1024 + s)) >> 9) + 4 * dg +
+                 (uint32_t)(((uint64_t)db * (1534 - s)) >> 9);
+    return t > 600;
+}
+
+static int cref_invalid(const cref_area *a) { return a->x < 0 || a->y < 0 || a->w < 0 || a->h < 0; }
+
+/* brain.c:86-102 (areas as x0, y0, x1, y1 during the scan) */
+static void cref_sum_areas(cref_area *a, cref_area b) {
+    if (cref_invalid(a) && cref_invalid(&b)) {
+        a->x = a->y = a->w = a->h = -1;
+    } else if (cref_invalid(a)) {
+        *a = b;
+    } else if (!cref_invalid(&b)) {
+        if (b.x < a->x) a->x = b.x;
+        if (b.y < a->y) a->y = b.y;
+        if (b.w > a->w) a->w = b.w;
+        if (b.h > a->h) a->h = b.h;
+    }
+}
+
+/* brain.c:64-74 */
+static int cref_overlap(cref_area a, cref_area b) {
+    return !(a.x > b.w + 1 || a.w + 1 < b.x) && !(a.y > b.h + 1 || a.h + 1 < b.y);
+}
+static int cref_overlap2(cref_area a, cref_area b) {
+    return !(a.x > b.x + b.w + 2 || a.x + a.w + 2 < b.x) &&
+           !(a.y > b.y + b.h + 2 || a.y + a.h + 2 < b.y);
+}
+
+/* brain.c:240-261 */
+void cref_enlarge_adjust(cref_area *a, int w, int h) {
+    a->w = (a->w - a->x + 1) * 4;
+    a->h = (a->h - a->y + 1) * 4;
+    a->x *= 4;
+    a->y *= 4;
+    a->x -= (16 - a->w % 16) / 2;
+    a->y -= (16 - a->h % 16) / 2;
+    if (a->w % 16) a->w += 16 - a->w % 16;
+    if (a->h % 16) a->h += 16 - a->h % 16;
+    if (a->w > w) a->w = w;
+    if (a->h > h) a->h = h;
+    if (a->x + a->w > w) a->x -= a->x + a->w - w;
+    if (a->y + a->h > h) a->y -= a->y + a->h - h;
+    if (a->x < 0) a->x = 0;
+    if (a->y < 0) a->y = 0;
+}
+
+/* brain.c:104-233.  Runs of differing pixels are collected per sub-row into
+ * one of two alternating lists; when a sub-row starts, the runs of the row
+ * before it are joined to the runs of the row before that (8-adjacency)
+ * into areas.  Kept as the reference has it: a run still open at the end of
+ * a row is dropped, the last row is never joined, the 100-area overflow
+ * compaction leaves run labels stale, and sumAreas after enlargeAdjust takes
+ * the larger width/height rather than the union. */
+int cref_compare(const uint8_t *sub, const uint8_t *saved, int w, int h, cref_area outs[100]) {
+    int sw = w / 4, sh = h / 4, cap = w / 8;
+    cref_run *lists = malloc(sizeof(cref_run) * 2 * (size_t)cap);
+    cref_run *L[2] = {lists, lists + cap};
+    int n = 0, cur = 0, ncur = 0, nprev = 0, open = 0;
+    for (int i = 0; i < 100; i++) outs[i].x = outs[i].y = outs[i].w = outs[i].h = -1;
+    for (int i = 0; i < 2 * cap; i++) lists[i].beg = lists[i].end = lists[i].row = lists[i].done = -1;
+    for (int y = 0; y < sh; y++) {
+        /* :124-181 join the finished row's runs (L[cur]) to L[!cur] */
+        cref_run *rk = L[cur], *rz = L[!cur];
+        for (int k = 0; k < ncur; k++) {
+            int joined = 0;
+            for (int z = 0; z < nprev; z++) {
+                if (rk[k].end < rz[z].beg - 1 || rk[k].beg > rz[z].end + 1) continue;
+                joined = 1;
+                if (rk[k].done >= 0) {
+                    int lo = rz[z].done < rk[k].done ? rz[z].done : rk[k].done;
+                    int hi = rz[z].done < rk[k].done ? rk[k].done : rz[z].done;
+                    if (lo == hi) continue;
+                    cref_sum_areas(&outs[lo], outs[hi]);
+                    n--;
+                    if (hi < n) outs[hi] = outs[n];
+                    rk[k].done = rz[z].done = lo;
+                    for (int a = 0; a < k; a++) {
+                        if (rk[a].done == hi) rk[a].done = lo;
+                        if (rk[a].done == n) rk[a].done = hi;
+                    }
+                    for (int a = z + 1; a < nprev; a++) {
+                        if (rz[a].done == hi) rz[a].done = lo;
+                        if (rz[a].done == n) rz[a].done = hi;
+                    }
+                } else {
+                    rk[k].done = rz[z].done;
+                    cref_area seg = {rk[k].beg, rk[k].row, rk[k].end, rk[k].row};
+                    cref_sum_areas(&outs[rz[z].done], seg);
+                }
+            }
+            if (!joined) {
+                if (n > 99) { /* :156-168 */
+                    for (int i = 0; i < n; i++)
+                        for (int j = i + 1; j < n; j++)
+                            if (cref_overlap(outs[i], outs[j])) {
+                                cref_sum_areas(&outs[i], outs[j]);
+                                n--;
+                                outs[j] = outs[n];
+                            }
+                    if (n > 99) { free(lists); return n; }
+                }
+                rk[k].done = n;
+                cref_area seg = {rk[k].beg, rk[k].row, rk[k].end, rk[k].row};
+                outs[n++] = seg;
+            }
+        }
+        cur = !cur;
+        open = 0;
+        nprev = ncur;
+        ncur = 0;
+        /* :184-210 scan row y into L[cur] */
+        for (int x = 0; x < sw; x++) {
+            size_t o = 3 * ((size_t)y * sw + x);
+            if (cref_pixel_differs(sub + o, saved + o)) {
+                if (!open) {
+                    open = 1;
+                    L[cur][ncur].beg = x;
+                    L[cur][ncur].row = y;
+                    L[cur][ncur].done = -1;
+                }
+                L[cur][ncur].end = x;
+            } else if (open) {
+                open = 0;
+                ncur++;
+            }
+        }
+    }
+    free(lists);
+    /* :212-232 */
+    for (int i = 0; i < n; i++) cref_enlarge_adjust(&outs[i], w, h);
+    for (int i = 0; i < n; i++)
+        for (int j = i + 1; j < n; j++)
+            if (cref_overlap2(outs[i], outs[j])) {
+                cref_sum_areas(&outs[i], outs[j]);
+                n--;
+                outs[j] = outs[n];
+                j--;
+            }
+    for (int i = 0; i < n;) {
+        if (outs[i].w < 32 && outs[i].h < 24) {
+            n--;
+            if (i < n) outs[i] = outs[n];
+            outs[n].x = outs[n].y = outs[n].w = outs[n].h = -1;
+        } else {
+            i++;
+        }
+    }
+    return n;
+}

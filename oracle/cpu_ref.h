@@ -68,6 +68,22 @@ void cref_cos_bits(int64_t out[64]);
 /* Number of worst-case bytes a frame of w*h pixels can need. */
 size_t cref_max_jpg_bytes(int w, int h);
 
+/* ---- change detector (main/brain.c) ------------------------------------ */
+
+typedef struct { int beg, end, row, done; } cref_run;   /* structs.h:20-22 pair_t */
+
+/* brain.c:16-45: 4x4 box average of a w x h BGR frame (stride w) into a
+ * (w/4) x (h/4) RGB plane (sub[3i] = R average). */
+void cref_subsample(const uint8_t *bgr, int w, int h, uint8_t *sub);
+
+/* brain.c:104-233 (+64-102, 240-261): compares two (w/4) x (h/4) RGB planes
+ * and writes up to 100 areas into outs (100 entries); returns the count the
+ * reference returns (its uint8_t). */
+int cref_compare(const uint8_t *sub, const uint8_t *saved, int w, int h, cref_area outs[100]);
+
+/* brain.c:240-261 for a w x h frame. */
+void cref_enlarge_adjust(cref_area *a, int w, int h);
+
 #ifdef __cplusplus
 }
 #endif

@@ -20,6 +20,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CREF_SO = os.path.join(HERE, "libcref.so")
 REF_SO = os.path.join(HERE, "_ref", "libref_encoder.so")
 REF_QUALITY = os.path.join(HERE, "_ref", "ref_quality")
+REF_BRAIN_SO = os.path.join(HERE, "_ref", "libref_brain.so")
 
 
 class Huff(C.Structure):
@@ -71,6 +72,10 @@ def cref() -> C.CDLL:
         lib.cref_cos_bits.argtypes = [p]
         lib.cref_max_jpg_bytes.restype = C.c_size_t
         lib.cref_max_jpg_bytes.argtypes = [C.c_int, C.c_int]
+        lib.cref_subsample.argtypes = [p, C.c_int, C.c_int, p]
+        lib.cref_compare.restype = C.c_int
+        lib.cref_compare.argtypes = [p, p, C.c_int, C.c_int, p]
+        lib.cref_enlarge_adjust.argtypes = [p, C.c_int, C.c_int]
         _cref = lib
     return _cref
 
@@ -93,6 +98,74 @@ def ref() -> C.CDLL:
         lib.ref_huff_size.restype = C.c_size_t
         _ref = lib
     return _ref
+
+
+_ref_brain = None
+
+
+def ref_brain_available() -> bool:
+    return os.path.exists(REF_BRAIN_SO)
+
+
+def ref_brain() -> C.CDLL:
+    """The unmodified reference main/brain.c (oracle/_ref/libref_brain.so)."""
+    global _ref_brain
+    if _ref_brain is None:
+        lib = C.CDLL(REF_BRAIN_SO)
+        p = C.c_void_p
+        lib.ref_subsample.restype = C.c_int
+        lib.ref_subsample.argtypes = [p, C.c_int, C.c_int, p]
+        lib.ref_compare.restype = C.c_int
+        lib.ref_compare.argtypes = [p, p, C.c_int, C.c_int, p]
+        lib.ref_enlarge_adjust.argtypes = [p, C.c_int, C.c_int]
+        _ref_brain = lib
+    return _ref_brain
+
+
+def _areas(outs, n):
+    return [(a.x, a.y, a.w, a.h) for a in outs[:max(0, min(n, 100))]]
+
+
+def cref_subsample(bgr: np.ndarray) -> np.ndarray:
+    """brain.c:16-45 restated: (H/4, W/4, 3) RGB plane of a BGR frame."""
+    bgr = np.ascontiguousarray(bgr, dtype=np.uint8)
+    H, W = bgr.shape[:2]
+    sub = np.zeros((H // 4, W // 4, 3), np.uint8)
+    cref().cref_subsample(_ptr(bgr), W, H, _ptr(sub))
+    return sub
+
+
+def cref_compare(sub: np.ndarray, saved: np.ndarray, W: int, H: int):
+    """brain.c:104-233 restated: (count, [areas]) for two subsampled planes."""
+    sub = np.ascontiguousarray(sub, dtype=np.uint8)
+    saved = np.ascontiguousarray(saved, dtype=np.uint8)
+    outs = (Area * 100)()
+    n = cref().cref_compare(_ptr(sub), _ptr(saved), W, H, outs)
+    return n, _areas(outs, n)
+
+
+def cref_area_adjust(area, W: int, H: int):
+    """brain.c:240-261 restated."""
+    a = Area(*area)
+    cref().cref_enlarge_adjust(C.byref(a), W, H)
+    return (a.x, a.y, a.w, a.h)
+
+
+def ref_subsample(bgr: np.ndarray) -> np.ndarray:
+    bgr = np.ascontiguousarray(bgr, dtype=np.uint8)
+    H, W = bgr.shape[:2]
+    sub = np.zeros((H // 4, W // 4, 3), np.uint8)
+    if ref_brain().ref_subsample(_ptr(bgr), W, H, _ptr(sub)):
+        raise OSError("ref_subsample failed")
+    return sub
+
+
+def ref_compare(sub: np.ndarray, saved: np.ndarray, W: int, H: int):
+    sub = np.ascontiguousarray(sub, dtype=np.uint8)
+    saved = np.ascontiguousarray(saved, dtype=np.uint8)
+    outs = (Area * 100)()
+    n = ref_brain().ref_compare(_ptr(sub), _ptr(saved), W, H, outs)
+    return n, _areas(outs, n)
 
 
 def _ptr(a: np.ndarray) -> int:

@@ -118,3 +118,53 @@ ADVERSARIAL = {
     "noise": noise,
     "near_gray": near_gray,
 }
+
+
+def detect_scene(seed: int, w: int = 320, h: int = 240, kind: str = "objects"):
+    """(stored, current) BGR frame pair for the change detector (brain.c).
+
+    kinds: "objects" -- a smooth background with a few solid/noisy rectangles
+    pasted into the current frame; "many" -- hundreds of small patches (the
+    100-area overflow path of brain.c:156-168); "noise" -- the whole current
+    frame perturbed by +-30; "same" -- identical frames; "edge" -- patches
+    touching the right and bottom edges (runs left open at a row end);
+    "grid" -- a regular grid of small separated patches (> 100 areas)."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:h, 0:w]
+    base = np.stack([(xx * 255 // max(w - 1, 1)), (yy * 255 // max(h - 1, 1)),
+                     ((xx + yy) * 127 // max(w + h - 2, 1))], axis=-1).astype(np.uint8)
+    base = np.clip(base.astype(int) + rng.integers(-3, 4, base.shape), 0, 255).astype(np.uint8)
+    cur = base.copy()
+    if kind == "same":
+        return base, cur
+    if kind == "noise":
+        cur = np.clip(cur.astype(int) + rng.integers(-30, 31, cur.shape), 0, 255).astype(np.uint8)
+        return base, cur
+    if kind == "grid":  # separated 8x8 patches every 24 px: > 100 areas
+        for y in range(8, h - 16, 24):
+            for x in range(8, w - 16, 24):
+                cur[y:y + 8, x:x + 8] = rng.integers(0, 256, 3)
+        return base, cur
+    n = {"objects": int(rng.integers(1, 12)), "many": 400, "edge": 6}[kind]
+    big = {"objects": 0.12, "many": 0.03, "edge": 0.3}[kind]
+    for _ in range(n):
+        rw = int(rng.integers(2, max(3, int(w * big) + 3)))
+        rh = int(rng.integers(2, max(3, int(h * big) + 3)))
+        if kind == "edge":
+            x, y = (w - rw, int(rng.integers(0, h - rh))) if rng.random() < 0.5 else \
+                   (int(rng.integers(0, w - rw)), h - rh)
+        else:
+            x, y = int(rng.integers(0, w - rw)), int(rng.integers(0, h - rh))
+        if rng.random() < 0.6:
+            cur[y:y + rh, x:x + rw] = rng.integers(0, 256, 3)
+        else:
+            cur[y:y + rh, x:x + rw] = rng.integers(0, 256, (rh, rw, 3))
+    return base, cur
+
+
+# (seed, w, h, kind) of the committed detector fixtures (tests/golden/detect.json)
+DETECT_CASES = [(s, 320, 240, "objects") for s in range(12)] + \
+    [(100 + s, 320, 240, k) for s, k in enumerate(["many", "many", "noise", "same", "edge", "edge"])] + \
+    [(200, 64, 64, "objects"), (201, 640, 480, "objects"), (202, 1920, 1080, "objects"),
+     (203, 1920, 1080, "many"), (204, 3840, 2160, "objects"), (205, 336, 208, "edge"),
+     (206, 320, 240, "grid"), (207, 640, 480, "grid"), (208, 1280, 720, "noise")]
