@@ -60,7 +60,7 @@ def parse():
     ap.add_argument("--coef-launches", type=int, default=3,
                     help="extra launches of the coefficient-output K1 variant after the timed "
                          "region, for its own 6 B/px roofline line (0 disables)")
-    ap.add_argument("--workload", choices=["config3", "config4", "regions", "detect"], default="config3",
+    ap.add_argument("--workload", choices=["config3", "config4", "regions", "detect", "decode"], default="config3",
                     help="config4: a stream of 7680x4320 frames, each split into MCU-row bands "
                          "over the ranks with the RCCL exchange steps (strong scaling)")
     ap.add_argument("--detect-frames", type=int, default=8, help="detect: distinct frames cycled")
@@ -373,6 +373,61 @@ def run_detect(args, world, rank, local, dist):
         dist.destroy_process_group()
 
 
+def run_decode(args, world, rank, local, dist):
+    """SURVEY §8(f) rank 4, the round-trip verifier: --frames JFIF streams of
+    the config-3 frames (encoded by this library) decoded back to coefficient
+    planes per step (host parse + H2D of the streams + the GPU entropy decode,
+    one lane per scan).  Verified against the encoder's kept coefficients."""
+    import torch
+    gpu = 0 if dist is not None and dist.get_backend() != "nccl" else local
+    torch.cuda.set_device(gpu)
+    W, H, F = args.width, args.height, args.frames
+    frames = make_frames(args, rank)
+    enc = mijpeg.Batch(W, H, F, args.quality, device=gpu, keep_coefs=True)
+    host = np.stack([frames[i % len(frames)] for i in range(F)])
+    enc.upload(host)
+    enc.encode(F)
+    streams = [enc.output(i) for i in range(F)]
+    dec = mijpeg.Decoder(W, H, F, device=gpu)
+
+    for _ in range(args.warmup):
+        dec.decode(streams)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dec.decode(streams)
+    el = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
+    el, px_all = sharding.reduce_timing(el, W * H * F * args.steps, dist, dist_device(dist, local))
+    verified = 0
+    for i in range(min(F, args.verify)):
+        for g, w in zip(dec.coefs(i), enc.coefs(i, diffed=True)):
+            if not (g == w).all():
+                raise SystemExit(f"bench decode: frame {i} coefficients differ from the encoder's")
+        verified += 1
+    res = {
+        "metric": "Mpixels/s decoded (JFIF -> coefficient planes, round-trip verifier)",
+        "value": round(px_all / el / 1e6, 1), "unit": "Mpixels/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int16",
+        "data": "synthetic: config-3 frames encoded by this library",
+        "config": {"workload": f"decode: {F} x {W}x{H} JFIF streams per step (host parse + H2D + "
+                               f"GPU entropy decode)", "frames": F, "width": W, "height": H,
+                   "stream_MB": round(sum(len(s) for s in streams) / 1e6, 2),
+                   "parallelism": f"frame-parallel x{world}"},
+        "verified_frames": verified,
+    }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    dec.close()
+    enc.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def make_frames(args, rank):
     """Distinct config-3 frames (recipe in tests/recipes.py), rank-offset so
     ranks encode different content."""
@@ -491,6 +546,8 @@ def main():
         return run_regions(args, world, rank, local, dist)
     if args.workload == "detect":
         return run_detect(args, world, rank, local, dist)
+    if args.workload == "decode":
+        return run_decode(args, world, rank, local, dist)
     W, H, F = args.width, args.height, args.frames
     frames = make_frames(args, rank)
     gpu = 0 if dist is not None and dist.get_backend() != "nccl" else local

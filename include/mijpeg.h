@@ -83,7 +83,8 @@ enum {
     MIJ_ETABLE = 5,     /* Huffman construction outside the reference's
                            defined behaviour (code length >= 32 etc.) */
     MIJ_EPPM = 6,       /* PPM rejected by the rules of utils/original.c:294-365 */
-    MIJ_EIO = 7         /* file could not be opened, read or written */
+    MIJ_EIO = 7,        /* file could not be opened, read or written */
+    MIJ_EJPEG = 8       /* decoder: stream outside the supported JFIF subset or corrupt */
 };
 int mij_last_error(void);
 const char *mij_strerror(int code);
@@ -310,6 +311,26 @@ int mij_detector_set_plane(mij_detector *d, int which, const uint8_t *rgb);
  * per subsampled row (bit x%64 of word x/64 = pixel x differs) */
 int mij_detector_mask(mij_detector *d, unsigned long long *dst, size_t cap_words, int *words);
 void *mij_detector_stream(mij_detector *d);
+
+/* ---- round-trip verifier ---------------------------
+ * The reference has no decoder.  mij_decoder turns baseline JFIF streams of
+ * the shape encoder.c:549-644 writes (8-bit, Y 2x2 + Cb + Cr 1x1, three
+ * one-component scans, no restarts) back into the encoder's coefficient
+ * layout: per component, blocks in raster order, 64 zigzag-ordered
+ * quantized coefficients, DC as the coded difference (= rgb_to_dct's
+ * output), so encode -> decode can be checked bit-exactly at any size.
+ * Entropy decoding runs on the GPU, one lane per scan of the batch. */
+typedef struct mij_decoder mij_decoder;
+mij_decoder *mij_decoder_create(int device, int max_w, int max_h, int max_frames);
+void mij_decoder_destroy(mij_decoder *d);
+/* n host streams; synchronous; MIJ_EJPEG names the stream on failure */
+int mij_decoder_decode(mij_decoder *d, const uint8_t *const *jpgs, const size_t *lens, int n);
+/* frame size and the two DQT tables (zigzag order) of stream `frame` */
+int mij_decoder_info(mij_decoder *d, int frame, int *w, int *h, uint8_t dqt[128]);
+/* Y[w*h], Cb[w*h/4], Cr[w*h/4] of stream `frame` (host copies) */
+int mij_decoder_coefs(mij_decoder *d, int frame, int16_t *Y, int16_t *Cb, int16_t *Cr);
+/* device address of stream `frame`'s planes (Y, then Cb, then Cr) */
+void *mij_decoder_device_coefs(mij_decoder *d, int frame);
 
 /* Drop-in entry points of include/brain.h:7-10, on frames of
  * mij_set_input_stride() x mij_set_frame_height() pixels (define.h:3-4,

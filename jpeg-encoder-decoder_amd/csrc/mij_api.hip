@@ -88,6 +88,7 @@ extern "C" const char *mij_strerror(int code) {
     case MIJ_ETABLE: return "Huffman table outside the reference's defined behaviour";
     case MIJ_EPPM: return "PPM rejected (utils/original.c read_ppm rules)";
     case MIJ_EIO: return "file I/O error";
+    case MIJ_EJPEG: return "JPEG stream rejected (not a baseline 4:2:0 three-scan JFIF, or corrupt)";
   }
   return "unknown error";
 }

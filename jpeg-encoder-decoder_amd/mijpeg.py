@@ -30,6 +30,8 @@ EXPORTS = [
     "mij_probe_mfma", "mij_colour_lut", "mij_build_target",
     # change detector (reference include/brain.h:7-10 drop-in + extensions)
     "subsample", "store", "compare", "enlargeAdjust", "mij_set_frame_height",
+    "mij_decoder_create", "mij_decoder_destroy", "mij_decoder_decode", "mij_decoder_info",
+    "mij_decoder_coefs", "mij_decoder_device_coefs",
     "mij_detector_create", "mij_detector_destroy", "mij_detector_subsample", "mij_detector_compare",
     "mij_detector_step", "mij_detector_launch", "mij_detector_store", "mij_detector_upload", "mij_detector_get_plane",
     "mij_detector_set_plane", "mij_detector_mask", "mij_detector_stream",
@@ -154,6 +156,14 @@ def load() -> C.CDLL:
         lib.mij_detector_stream.restype = p
         lib.mij_detector_stream.argtypes = [p]
         lib.mij_set_frame_height.argtypes = [i]
+        lib.mij_decoder_create.restype = p
+        lib.mij_decoder_create.argtypes = [i, i, i, i]
+        lib.mij_decoder_destroy.argtypes = [p]
+        lib.mij_decoder_decode.argtypes = [p, C.POINTER(p), C.POINTER(sz), i]
+        lib.mij_decoder_info.argtypes = [p, i, C.POINTER(i), C.POINTER(i), p]
+        lib.mij_decoder_coefs.argtypes = [p, i, p, p, p]
+        lib.mij_decoder_device_coefs.restype = p
+        lib.mij_decoder_device_coefs.argtypes = [p, i]
         lib.subsample.restype = None
         lib.subsample.argtypes = [p, p, p]
         lib.store.restype = None
@@ -664,3 +674,49 @@ def drop_in_enlarge_adjust(area, W: int, H: int):
     a = Area(*area)
     lib.enlargeAdjust(C.byref(a))
     return (a.x, a.y, a.w, a.h)
+
+
+# ---- round-trip verifier ---------------------------
+
+class Decoder:
+    """Baseline JFIF streams (the shape encoder.c:549-644 writes) -> the
+    encoder's coefficient planes, entropy-decoded on the GPU."""
+
+    def __init__(self, max_w: int, max_h: int, max_frames: int, device: int = 0):
+        self.lib = load()
+        self.h_ = self.lib.mij_decoder_create(device, max_w, max_h, max_frames)
+        if not self.h_:
+            raise MijError("mij_decoder_create failed: "
+                           f"{self.lib.mij_strerror(self.lib.mij_last_error()).decode()}")
+
+    def close(self) -> None:
+        if self.h_:
+            self.lib.mij_decoder_destroy(self.h_)
+            self.h_ = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def decode(self, streams) -> None:
+        n = len(streams)
+        bufs = [np.frombuffer(s, np.uint8) for s in streams]
+        ptrs = (C.c_void_p * n)(*[_ptr(b) for b in bufs])
+        lens = (C.c_size_t * n)(*[len(s) for s in streams])
+        _check(self.lib.mij_decoder_decode(self.h_, ptrs, lens, n), "decoder_decode")
+
+    def info(self, frame: int):
+        w, h = C.c_int(), C.c_int()
+        dqt = np.zeros(128, np.uint8)
+        _check(self.lib.mij_decoder_info(self.h_, frame, C.byref(w), C.byref(h), _ptr(dqt)), "decoder_info")
+        return w.value, h.value, dqt
+
+    def coefs(self, frame: int):
+        w, h, _ = self.info(frame)
+        Y = np.zeros(w * h, np.int16)
+        Cb = np.zeros(w * h // 4, np.int16)
+        Cr = np.zeros(w * h // 4, np.int16)
+        _check(self.lib.mij_decoder_coefs(self.h_, frame, _ptr(Y), _ptr(Cb), _ptr(Cr)), "decoder_coefs")
+        return Y, Cb, Cr

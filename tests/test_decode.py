@@ -1,0 +1,136 @@
+"""Round-trip verifier: the reference has no
+decoder (its output was checked with libjpeg only).  mij_decoder entropy-
+decodes the JFIF streams of encoder.c:549-644's shape on the GPU back into
+the encoder's coefficient planes (zigzag order, DC as the coded difference),
+so decode(jpg) must equal rgb_to_dct(frame) bit for bit:
+
+* on the committed reference fixtures: the reference's own coefficient
+  dumps (tests/golden/sample_64x64.coefs.npz, manifest coef_sha256);
+* at full size (config 3, 3840x2160) as a size-independent property:
+  decode(GPU encode(x)) == the GPU encoder's kept coefficient planes.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import mijpeg
+import oracle as O
+import recipes
+from test_oracle import case_input
+
+
+def sha(a) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def test_decoder_validates_before_device_use():
+    lib = mijpeg.load()
+    assert not lib.mij_decoder_create(0, 24, 16, 1)
+    assert lib.mij_last_error() == 1
+
+
+@pytest.mark.gpu
+def test_decode_reference_golden_64x64():
+    jpg = open(f"{recipes.GOLDEN}/sample_64x64.jpg", "rb").read()
+    z = np.load(f"{recipes.GOLDEN}/sample_64x64.coefs.npz")
+    d = mijpeg.Decoder(64, 64, 1)
+    try:
+        d.decode([jpg])
+        w, h, dqt = d.info(0)
+        assert (w, h) == (64, 64)
+        Y, Cb, Cr = d.coefs(0)
+        assert (Y == z["Y"]).all() and (Cb == z["Cb"]).all() and (Cr == z["Cr"]).all()
+    finally:
+        d.close()
+
+
+@pytest.mark.gpu
+def test_decode_manifest_cases(manifest):
+    """Every small golden case: decode(oracle jpg whose sha the reference
+    pinned) has the reference's coefficient sha256 (the oracle's planes for
+    cases whose manifest entry holds only the jpg sha)."""
+    cases = [(k, e) for k, e in sorted(manifest.items())
+             if e["frame"][0] * e["frame"][1] <= 1920 * 1280 and e["quality"] == 50]
+    streams, want = [], []
+    for name, ent in cases:
+        bgr = case_input(name, ent)
+        region = tuple(ent["region"])
+        Y, Cb, Cr, _, jpg = O.cref_stages(bgr, 50, region)
+        assert sha(jpg) == ent["jpg_sha256"], name
+        streams.append(jpg)
+        # the reference's coefficient dump where the manifest holds one
+        want.append(ent.get("coef_sha256", [sha(Y), sha(Cb), sha(Cr)]))
+    mw = max(e["region"][2] for _, e in cases)
+    mh = max(e["region"][3] for _, e in cases)
+    d = mijpeg.Decoder(mw, mh, len(streams))
+    try:
+        d.decode(streams)
+        for i, (name, _) in enumerate(cases):
+            Y, Cb, Cr = d.coefs(i)
+            assert [sha(Y), sha(Cb), sha(Cr)] == want[i], name
+    finally:
+        d.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("quality", [50, 75, 90, 100, 10])
+def test_decode_quality_sweep_and_long_codes(quality):
+    """Q sweep (original.c:504-509) on natural and uniform-noise content (the
+    noise needs AC codes longer than the 9-bit lookahead)."""
+    frames = [recipes.noise(), recipes.gradients(), recipes.checkerboards(64, 128)]
+    streams, want = [], []
+    for f in frames:
+        Y, Cb, Cr, _, jpg = O.cref_stages(f, quality)
+        streams.append(jpg)
+        want.append((Y, Cb, Cr))
+    d = mijpeg.Decoder(256, 128, len(frames))
+    try:
+        d.decode(streams)
+        lq, cq = O.quality_tables(quality)
+        for i in range(len(frames)):
+            got = d.coefs(i)
+            for g, w in zip(got, want[i]):
+                assert (g == w).all()
+        _, _, dqt = d.info(0)
+        assert dqt.size == 128
+    finally:
+        d.close()
+
+
+@pytest.mark.gpu
+def test_round_trip_config3_full_size():
+    """decode(GPU encode) == the GPU encoder's own coefficients, 3840x2160."""
+    frames = np.stack([recipes.config3_frame(0), recipes.config3_uniform(1)])
+    b = mijpeg.Batch(3840, 2160, 2, 50, keep_coefs=True)
+    d = mijpeg.Decoder(3840, 2160, 2)
+    try:
+        b.upload(frames)
+        b.encode(2)
+        streams = [b.output(i) for i in range(2)]
+        d.decode(streams)
+        for i in range(2):
+            for g, w in zip(d.coefs(i), b.coefs(i, diffed=True)):
+                assert (g == w).all()
+    finally:
+        b.close()
+        d.close()
+
+
+@pytest.mark.gpu
+def test_corrupt_streams_rejected():
+    jpg = bytearray(open(f"{recipes.GOLDEN}/sample_64x64.jpg", "rb").read())
+    d = mijpeg.Decoder(64, 64, 1)
+    try:
+        with pytest.raises(mijpeg.MijError):
+            d.decode([bytes(jpg[:200])])           # cut inside the headers
+        bad = bytes(jpg[:330]) + bytes(jpg[-2:])   # first scan cut short
+        with pytest.raises(mijpeg.MijError):
+            d.decode([bad])
+        prog = bytearray(jpg)
+        prog[293 + 1] = 0xC2                       # SOF2: progressive
+        with pytest.raises(mijpeg.MijError):
+            d.decode([bytes(prog)])
+        d.decode([bytes(jpg)])                     # and still usable afterwards
+    finally:
+        d.close()
