@@ -414,11 +414,12 @@ def run_decode(args, world, rank, local, dist):
         "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "int16",
         "data": "synthetic: config-3 frames encoded by this library",
-        "config": {"workload": f"decode: {F} x {W}x{H} JFIF streams per step (host parse + H2D + "
-                               f"GPU entropy decode)", "frames": F, "width": W, "height": H,
+        "config": {"workload": f"decode: {F} x {W}x{H} JFIF streams per step (host parse + "
+                               f"unstuffing + H2D + GPU chunk-parallel entropy decode)", "frames": F, "width": W, "height": H,
                    "stream_MB": round(sum(len(s) for s in streams) / 1e6, 2),
                    "parallelism": f"frame-parallel x{world}"},
         "verified_frames": verified,
+        "sync_passes": dec.passes(),
     }
     if rank == 0:
         print(json.dumps(res), flush=True)

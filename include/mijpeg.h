@@ -319,7 +319,8 @@ void *mij_detector_stream(mij_detector *d);
  * layout: per component, blocks in raster order, 64 zigzag-ordered
  * quantized coefficients, DC as the coded difference (= rgb_to_dct's
  * output), so encode -> decode can be checked bit-exactly at any size.
- * Entropy decoding runs on the GPU, one lane per scan of the batch. */
+ * Entropy decoding runs on the GPU, one lane per 2048-bit chunk of every
+ * scan, the chunks' entry states found by self-synchronisation. */
 typedef struct mij_decoder mij_decoder;
 mij_decoder *mij_decoder_create(int device, int max_w, int max_h, int max_frames);
 void mij_decoder_destroy(mij_decoder *d);
@@ -329,6 +330,8 @@ int mij_decoder_decode(mij_decoder *d, const uint8_t *const *jpgs, const size_t 
 int mij_decoder_info(mij_decoder *d, int frame, int *w, int *h, uint8_t dqt[128]);
 /* Y[w*h], Cb[w*h/4], Cr[w*h/4] of stream `frame` (host copies) */
 int mij_decoder_coefs(mij_decoder *d, int frame, int16_t *Y, int16_t *Cb, int16_t *Cr);
+/* self-synchronisation passes the last decode needed */
+int mij_decoder_passes(mij_decoder *d);
 /* device address of stream `frame`'s planes (Y, then Cb, then Cr) */
 void *mij_decoder_device_coefs(mij_decoder *d, int frame);
 

@@ -11,12 +11,16 @@
 // rgb_to_dct(x) at any size.
 //
 // Host: marker parsing (SOI, APP0, DQT, DHT, SOF0, SOS, EOI), canonical
-// Huffman tables with a 9-bit lookahead.  Device: one lane per (frame,
-// scan) decodes its scan sequentially: a 64-bit bit buffer refilled a byte
-// at a time with the 0xFF 0x00 unstuffing inline, table lookups from the
-// L1/L2-resident per-frame tables, coefficients written block by block.
-// Entropy decoding of one scan is sequential by construction; the batch
-// gives the parallelism (3 lanes per frame).
+// Huffman tables with a 9-bit lookahead, and the scans copied unstuffed
+// into one pinned staging blob.  Device: every scan is cut into 2048-bit
+// chunks, one lane per chunk.  Entropy decoding is sequential by
+// construction, so the chunks' entry states (bit position, coefficient
+// index) are found by self-synchronisation: each chunk first decodes from
+// its own first bit as if a block began there, then repeatedly from the
+// exit state of its predecessor until no entry changes (2-3 passes).  A
+// per-scan prefix sum of the blocks each chunk starts gives every chunk its
+// output block, and a final pass writes the nonzero coefficients into the
+// zeroed planes.
 #include <hip/hip_runtime.h>
 #include <string.h>
 
@@ -44,113 +48,238 @@ struct DecTab {
 };
 
 struct DecJob {
-  long long data, end;  // scan bytes [data, end) in the stream blob
-  long long out;        // first int16 of the component's plane
+  long long data;   // byte offset of the UNSTUFFED scan in the blob (8-aligned)
+  long long nbits;  // its length in bits (the pad bits included)
+  long long out;    // first int16 of the component's plane
   int nblocks;
-  int dc, ac;           // table indices
-  int frame;
+  int dc, ac;       // table indices
+  int chunk0, nchunks;  // global ids of the scan's chunks
 };
 
-struct BitReader {
-  const uint8_t *p;
-  long long pos, end;
-  unsigned long long acc;
-  int n;
-  int fed0;  // zero bytes fed past the scan's end
-  __device__ void fill() {
-    while (n <= 56) {
-      uint32_t b = 0;
-      if (pos < end) {
-        b = p[pos++];
-        if (b == 0xFF) pos++;  // stuffed 0x00 (B.1.1.5)
+// chunk c of a scan covers bits [c*CHUNK, (c+1)*CHUNK): a symbol belongs to
+// the chunk its first bit lies in
+constexpr int CHUNK = 2048;
+
+// MSB-first bit window over an unstuffed, 8-byte aligned, zero-padded scan
+struct Bits {
+  const unsigned long long *w;
+  long long cw = -2;  // index of the word pair held (none yet)
+  unsigned long long hi = 0, lo = 0;
+  __device__ unsigned long long window(long long pos) {
+    const long long i = pos >> 6;
+    if (i != cw) {
+      if (i == cw + 1) {
+        hi = lo;
+        lo = __builtin_bswap64(w[i + 1]);
       } else {
-        fed0++;
+        hi = __builtin_bswap64(w[i]);
+        lo = __builtin_bswap64(w[i + 1]);
       }
-      acc |= (unsigned long long)b << (56 - n);
-      n += 8;
+      cw = i;
     }
-  }
-  __device__ uint32_t peek(int k) const { return (uint32_t)(acc >> (64 - k)); }
-  __device__ void skip(int k) {
-    acc <<= k;
-    n -= k;
+    const int sh = pos & 63;
+    return sh ? (hi << sh) | (lo >> (64 - sh)) : hi;
   }
 };
 
-__device__ __forceinline__ int decode_sym(BitReader &br, const DecTab &t) {
-  br.fill();
-  const uint32_t e = t.look[br.peek(LOOK)];
+// one symbol (+ its magnitude bits) at pos; returns bits consumed, or 0 on
+// an invalid code.  F.2.2.3 DECODE with a LOOK-bit table, F.2.2.1 EXTEND
+__device__ __forceinline__ int decode_one(Bits &br, long long pos, const DecTab &t, int &sym, int &val) {
+  const unsigned long long win = br.window(pos);
+  int len;
+  const uint32_t e = t.look[win >> (64 - LOOK)];
   if (e) {
-    br.skip(e >> 8);
-    return e & 255;
-  }
-  for (int l = LOOK + 1; l <= 16; l++) {
-    const int32_t code = (int32_t)br.peek(l);
-    if (code <= t.maxcode[l]) {
-      br.skip(l);
-      return t.val[t.valoff[l] + code];
-    }
-  }
-  return -1;
-}
-
-// F.2.2.1 EXTEND: s magnitude bits; the encoder's negative form is ~|v|
-// (encoder.c:442-444)
-__device__ __forceinline__ int receive_extend(BitReader &br, int s) {
-  if (!s) return 0;
-  br.fill();
-  const int v = (int)br.peek(s);
-  br.skip(s);
-  return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v;
-}
-
-__global__ __launch_bounds__(64) void k_decode_scans(const uint8_t *__restrict__ blob,
-                                                     const DecJob *__restrict__ jobs, int njobs,
-                                                     const DecTab *__restrict__ tabs,
-                                                     int16_t *__restrict__ coefs,
-                                                     int *__restrict__ status) {
-  const int j = blockIdx.x * 64 + threadIdx.x;
-  if (j >= njobs) return;
-  const DecJob job = jobs[j];
-  const DecTab &dc = tabs[job.dc];
-  const DecTab &ac = tabs[job.ac];
-  BitReader br{blob, job.data, job.end, 0ULL, 0, 0};
-  int16_t *out = coefs + job.out;
-  int err = 0;
-  for (int b = 0; b < job.nblocks && !err; b++) {
-    int16_t *blk = out + 64LL * b;
-    int4 *o = (int4 *)blk;
-#pragma unroll
-    for (int q = 0; q < 8; q++) o[q] = int4{0, 0, 0, 0};
-    const int s = decode_sym(br, dc);
-    if (s < 0 || s > 15) {
-      err = 1;
-      break;
-    }
-    blk[0] = (int16_t)receive_extend(br, s);
-    for (int k = 1; k < 64;) {
-      const int rs = decode_sym(br, ac);
-      if (rs < 0) {
-        err = 2;
+    len = e >> 8;
+    sym = e & 255;
+  } else {
+    len = 0;
+    for (int l = LOOK + 1; l <= 16; l++) {
+      const int32_t code = (int32_t)(win >> (64 - l));
+      if (code <= t.maxcode[l]) {
+        len = l;
+        sym = t.val[t.valoff[l] + code];
         break;
       }
-      const int r = rs >> 4, sz = rs & 15;
-      if (!sz) {
-        if (r != 15) break;  // EOB
-        k += 16;             // ZRL
-        continue;
-      }
-      k += r;
-      if (k > 63) {
-        err = 3;
+    }
+    if (!len) return 0;
+  }
+  const int s = sym & 15;
+  if (s) {
+    // magnitude bits follow the code; the window holds >= 64 - 16 bits
+    const int v = (int)((win << len) >> (64 - s));
+    val = v < (1 << (s - 1)) ? v - (1 << s) + 1 : v;  // negatives are ~|v| (encoder.c:442-444)
+  } else {
+    val = 0;
+  }
+  return len + s;
+}
+
+// Decodes from (pos, k) until pos reaches `stop` or `blocks_left` blocks
+// have ended.  k = next coefficient index (0 = a DC symbol is next).
+// Returns the number of blocks started; pos/k are the state after the last
+// symbol.  WRITE: coefficients go to out[64*blk + zigzag index] (nonzeros
+// only; the planes are zeroed first).  *bad = invalid code met.
+template <bool WRITE>
+__device__ int decode_span(Bits &br, long long &pos, int &k, long long stop, const DecTab &dc,
+                           const DecTab &ac, int16_t *out, long long blk, long long blocks_left,
+                           bool *bad) {
+  int started = 0;
+  *bad = false;
+  while (pos < stop) {
+    int sym, val;
+    if (k == 0) {
+      if (blocks_left <= 0) break;
+      const int n = decode_one(br, pos, dc, sym, val);
+      if (!n || sym > 15) {
+        *bad = true;
         break;
       }
-      blk[k++] = (int16_t)receive_extend(br, sz);
+      pos += n;
+      if (WRITE && val) out[64 * blk] = (int16_t)val;
+      started++;
+      k = 1;
+    } else {
+      const int n = decode_one(br, pos, ac, sym, val);
+      if (!n) {
+        *bad = true;
+        break;
+      }
+      pos += n;
+      const int r = sym >> 4;
+      if (sym & 15) {
+        k += r;
+        if (k > 63) {
+          *bad = true;
+          break;
+        }
+        if (WRITE) out[64 * blk + k] = (int16_t)val;
+        k++;
+      } else if (r == 15) {
+        k += 16;  // ZRL
+      } else {
+        k = 64;   // EOB
+      }
+    }
+    if (k >= 64) {
+      k = 0;
+      blk++;
+      blocks_left--;
     }
   }
-  // bits consumed past the scan's bytes: truncated or corrupt stream
-  if (!err && 8 * br.fed0 > br.n) err = 4;
-  status[j] = err;
+  return started;
+}
+
+__device__ __forceinline__ int job_of(const DecJob *jobs, int njobs, int c) {
+  int lo = 0, hi = njobs - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].chunk0 <= c) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// Self-synchronising pass (Weissenberger & Schmidt, ICPP 2018): chunk c
+// decodes from its entry state to its end.  First pass: every chunk starts
+// at its first bit as if a block began there (exact for chunk 0 of a
+// scan).  Later passes: the entry of chunk c is the exit of chunk c-1 from
+// the previous pass; a chunk whose entry did not change keeps its result.
+// Huffman streams resynchronise within a few symbols, so 2-3 passes settle.
+struct SyncArgs {
+  const uint8_t *blob;
+  const DecJob *jobs;
+  int njobs, nchunks;
+  const DecTab *tabs;
+  long long *entry_pos, *exit_in, *exit_out;  // pos * 64 + k packed
+  int *nblk;
+  int *changed;
+  int first;
+};
+
+__device__ __forceinline__ long long pack_state(long long pos, int k) { return pos * 64 + k; }
+
+__global__ __launch_bounds__(256) void k_dec_sync(SyncArgs a) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= a.nchunks) return;
+  const DecJob &job = a.jobs[job_of(a.jobs, a.njobs, c)];
+  const int lc = c - job.chunk0;
+  long long entry;
+  if (a.first || lc == 0) {
+    entry = pack_state((long long)lc * CHUNK, 0);
+    if (!a.first) {
+      a.exit_out[c] = a.exit_in[c];
+      return;
+    }
+  } else {
+    entry = a.exit_in[c - 1];
+    if (entry < 0) entry = pack_state((long long)lc * CHUNK, 0);  // predecessor met a bad code
+    if (entry == a.entry_pos[c]) {
+      a.exit_out[c] = a.exit_in[c];
+      return;
+    }
+    *a.changed = 1;
+  }
+  a.entry_pos[c] = entry;
+  Bits br{(const unsigned long long *)(a.blob + job.data)};
+  long long pos = entry >> 6;
+  int k = (int)(entry & 63);
+  const long long stop = min((long long)(lc + 1) * CHUNK, job.nbits);
+  bool bad;
+  const int n = decode_span<false>(br, pos, k, stop, a.tabs[job.dc], a.tabs[job.ac], nullptr, 0,
+                                   (long long)job.nblocks, &bad);
+  a.nblk[c] = n;
+  a.exit_out[c] = bad ? -1 : pack_state(pos, k);
+}
+
+// per scan: exclusive scan of the chunks' block counts (one workgroup per
+// scan, sequential over 256-chunk tiles) and the total check
+__global__ __launch_bounds__(256) void k_dec_scan(const DecJob *jobs, const int *nblk, long long *base,
+                                                  int *status) {
+  __shared__ long long part[256];
+  const DecJob job = jobs[blockIdx.x];
+  long long carry = 0;
+  for (int t0 = 0; t0 < job.nchunks; t0 += 256) {
+    const int t = t0 + threadIdx.x;
+    const long long v = t < job.nchunks ? nblk[job.chunk0 + t] : 0;
+    part[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+      const long long add = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+      __syncthreads();
+      part[threadIdx.x] += add;
+      __syncthreads();
+    }
+    if (t < job.nchunks) base[job.chunk0 + t] = carry + part[threadIdx.x] - v;
+    const long long tot = part[255];
+    __syncthreads();
+    carry += tot;
+  }
+  // a chunk that decodes the last block may go on through the pad bits
+  // (and count garbage blocks there); fewer blocks than the frame needs is
+  // a truncated stream
+  if (threadIdx.x == 0) status[blockIdx.x] = carry >= job.nblocks ? 0 : 5;
+}
+
+// final pass: every chunk decodes from its settled entry and writes
+__global__ __launch_bounds__(256) void k_dec_write(SyncArgs a, const long long *base, int16_t *coefs,
+                                                   int *status) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= a.nchunks) return;
+  const int j = job_of(a.jobs, a.njobs, c);
+  const DecJob &job = a.jobs[j];
+  const int lc = c - job.chunk0;
+  const long long entry = a.entry_pos[c];
+  long long pos = entry >> 6;
+  int k = (int)(entry & 63);
+  // the block in progress at the entry was started by an earlier chunk
+  const long long blk = base[c] - (k ? 1 : 0);
+  if (blk >= job.nblocks) return;  // pad bits after the last block
+  Bits br{(const unsigned long long *)(a.blob + job.data)};
+  const long long stop = min((long long)(lc + 1) * CHUNK, job.nbits);
+  bool bad;
+  decode_span<true>(br, pos, k, stop, a.tabs[job.dc], a.tabs[job.ac], coefs + job.out, blk,
+                    job.nblocks - blk, &bad);
+  if (bad) atomicMax(&status[j], 6);
 }
 
 }  // namespace mij
@@ -297,6 +426,10 @@ struct mij_decoder {
   mij::DecTab *d_tabs = nullptr;
   mij::DecJob *d_jobs = nullptr;
   int *d_status = nullptr;
+  int *d_changed = nullptr;
+  long long *d_entry = nullptr, *d_exit[2] = {nullptr, nullptr}, *d_base = nullptr;
+  int *d_nblk = nullptr;
+  int chunk_cap = 0, job_cap = 1 << 30, last_passes = 0;
   std::vector<Parsed> parsed;
   long long plane_px = 0;  // max_w * max_h: Y plane; Cb/Cr a quarter each
   int n = 0;
@@ -311,6 +444,12 @@ static void decoder_free(mij_decoder *d) {
   hipFree(d->d_tabs);
   hipFree(d->d_jobs);
   hipFree(d->d_status);
+  hipFree(d->d_changed);
+  hipFree(d->d_entry);
+  hipFree(d->d_exit[0]);
+  hipFree(d->d_exit[1]);
+  hipFree(d->d_nblk);
+  hipFree(d->d_base);
   if (d->h_blob) hipHostFree(d->h_blob);
   if (d->stream) hipStreamDestroy(d->stream);
   delete d;
@@ -340,6 +479,7 @@ extern "C" mij_decoder *mij_decoder_create(int device, int max_w, int max_h, int
     HIP_TRY(hipMalloc((void **)&d->d_tabs, (size_t)max_frames * 4 * sizeof(mij::DecTab)));
     HIP_TRY(hipMalloc((void **)&d->d_jobs, (size_t)max_frames * 3 * sizeof(mij::DecJob)));
     HIP_TRY(hipMalloc((void **)&d->d_status, (size_t)max_frames * 3 * sizeof(int)));
+    HIP_TRY(hipMalloc((void **)&d->d_changed, sizeof(int)));
     return MIJ_OK;
   };
   if (init()) {
@@ -367,6 +507,41 @@ static int decoder_stage(mij_decoder *d, size_t total) {
 
 // Parses n streams, stages them in one device blob and decodes every scan.
 // Synchronous; the coefficients stay on the device (mij_decoder_coefs).
+// Unstuffed copy of scan bytes [b, e) of stream s into dst; returns bytes
+static size_t unstuff(uint8_t *dst, const uint8_t *s, size_t b, size_t e) {
+  size_t o = 0;
+  while (b < e) {
+    const uint8_t *f = (const uint8_t *)memchr(s + b, 0xFF, e - b);
+    const size_t stop = f ? (size_t)(f - s) + 1 : e;  // through the 0xFF
+    memcpy(dst + o, s + b, stop - b);
+    o += stop - b;
+    b = stop;
+    if (f && b < e && s[b] == 0x00) b++;  // stuffed zero (B.1.1.5)
+  }
+  return o;
+}
+
+static int decoder_buffers(mij_decoder *d, int nchunks, int njobs) {
+  if (nchunks <= d->chunk_cap && njobs <= d->job_cap) return MIJ_OK;
+  hipFree(d->d_entry);
+  hipFree(d->d_exit[0]);
+  hipFree(d->d_exit[1]);
+  hipFree(d->d_nblk);
+  hipFree(d->d_base);
+  d->chunk_cap = 0;
+  const size_t n = (size_t)nchunks + nchunks / 4 + 1024;
+  HIP_TRY(hipMalloc((void **)&d->d_entry, n * sizeof(long long)));
+  HIP_TRY(hipMalloc((void **)&d->d_exit[0], n * sizeof(long long)));
+  HIP_TRY(hipMalloc((void **)&d->d_exit[1], n * sizeof(long long)));
+  HIP_TRY(hipMalloc((void **)&d->d_nblk, n * sizeof(int)));
+  HIP_TRY(hipMalloc((void **)&d->d_base, n * sizeof(long long)));
+  d->chunk_cap = (int)n;
+  return MIJ_OK;
+}
+
+// Parses n streams, stages their unstuffed scans in one device blob and
+// decodes every scan chunk-parallel.  Synchronous; the coefficients stay on
+// the device (mij_decoder_coefs).
 extern "C" int mij_decoder_decode(mij_decoder *d, const uint8_t *const *jpgs, const size_t *lens, int n) {
   mij_clear_error();
   if (!d || !jpgs || !lens || n < 1 || n > d->cap) return mij_fail(MIJ_EINVAL, "decoder_decode: bad args");
@@ -379,41 +554,71 @@ extern "C" int mij_decoder_decode(mij_decoder *d, const uint8_t *const *jpgs, co
     const Parsed &P = d->parsed[f];
     if (P.w > d->max_w || P.h > d->max_h)
       return mij_fail(MIJ_EINVAL, "stream %d: %dx%d exceeds the decoder's %dx%d", f, P.w, P.h, d->max_w, d->max_h);
-    total += lens[f];
+    total += lens[f] + 3 * 24;
   }
   if (int rc = decoder_stage(d, total)) return rc;
   std::vector<mij::DecTab> tabs(4 * (size_t)n);
   std::vector<mij::DecJob> jobs(3 * (size_t)n);
   size_t off = 0;
+  int nchunks = 0;
   const long long fs = d->plane_px * 3 / 2;  // int16 per frame slot
   for (int f = 0; f < n; f++) {
     const Parsed &P = d->parsed[f];
-    memcpy(d->h_blob + off, jpgs[f], lens[f]);
     for (int t = 0; t < 4; t++) tabs[4 * f + t] = P.tab[t];
     const long long ny = (long long)P.w * P.h;
     const long long base[3] = {f * fs, f * fs + ny, f * fs + ny + ny / 4};
     for (int k = 0; k < 3; k++) {
       const auto &sc = P.scan[k];
+      const size_t len = unstuff(d->h_blob + off, jpgs[f], (size_t)sc.data, (size_t)sc.end);
+      memset(d->h_blob + off + len, 0, 24 - (len & 7) % 8);
       mij::DecJob &j = jobs[3 * f + k];
-      j.data = (long long)off + sc.data;
-      j.end = (long long)off + sc.end;
+      j.data = (long long)off;
+      j.nbits = 8LL * (long long)len;
       j.out = base[sc.comp];
       j.nblocks = (int)(sc.comp ? ny / 256 : ny / 64);
       j.dc = 4 * f + 2 * sc.td;
       j.ac = 4 * f + 2 * sc.ta + 1;
-      j.frame = f;
+      j.chunk0 = nchunks;
+      j.nchunks = (int)((j.nbits + mij::CHUNK - 1) / mij::CHUNK);
+      if (!j.nchunks) j.nchunks = 1;
+      nchunks += j.nchunks;
+      off = (off + len + 16 + 7) & ~(size_t)7;  // >= 16 zero bytes after each scan
     }
-    off += lens[f];
   }
   d->n = n;
-  HIP_TRY(hipMemcpyAsync(d->d_blob, d->h_blob, total, hipMemcpyHostToDevice, d->stream));
+  const int nj = 3 * n;
+  if (int rc = decoder_buffers(d, nchunks, nj)) return rc;
+  HIP_TRY(hipMemcpyAsync(d->d_blob, d->h_blob, off, hipMemcpyHostToDevice, d->stream));
   HIP_TRY(hipMemcpyAsync(d->d_tabs, tabs.data(), tabs.size() * sizeof(mij::DecTab), hipMemcpyHostToDevice,
                          d->stream));
   HIP_TRY(hipMemcpyAsync(d->d_jobs, jobs.data(), jobs.size() * sizeof(mij::DecJob), hipMemcpyHostToDevice,
                          d->stream));
-  const int nj = 3 * n;
-  hipLaunchKernelGGL(mij::k_decode_scans, dim3((nj + 63) / 64), dim3(64), 0, d->stream, d->d_blob, d->d_jobs,
-                     nj, d->d_tabs, d->d_coef, d->d_status);
+  HIP_TRY(hipMemsetAsync(d->d_coef, 0, (size_t)n * fs * sizeof(int16_t), d->stream));
+  HIP_TRY(hipMemsetAsync(d->d_status, 0, nj * sizeof(int), d->stream));
+  mij::SyncArgs a{d->d_blob, d->d_jobs, nj, nchunks, d->d_tabs, d->d_entry, d->d_exit[1], d->d_exit[0],
+                  d->d_nblk, d->d_changed, 1};
+  const dim3 grid((nchunks + 255) / 256);
+  hipLaunchKernelGGL(mij::k_dec_sync, grid, dim3(256), 0, d->stream, a);
+  HIP_TRY(hipGetLastError());
+  int cur = 0, passes = 1;
+  for (;; passes++) {
+    if (passes > 64) return mij_fail(MIJ_EJPEG, "decoder: chunk states did not settle");
+    HIP_TRY(hipMemsetAsync(d->d_changed, 0, sizeof(int), d->stream));
+    a.first = 0;
+    a.exit_in = d->d_exit[cur];
+    a.exit_out = d->d_exit[!cur];
+    hipLaunchKernelGGL(mij::k_dec_sync, grid, dim3(256), 0, d->stream, a);
+    HIP_TRY(hipGetLastError());
+    cur = !cur;
+    int changed = 0;
+    HIP_TRY(hipMemcpyAsync(&changed, d->d_changed, sizeof(int), hipMemcpyDeviceToHost, d->stream));
+    HIP_TRY(hipStreamSynchronize(d->stream));
+    if (!changed) break;
+  }
+  d->last_passes = passes;
+  hipLaunchKernelGGL(mij::k_dec_scan, dim3(nj), dim3(256), 0, d->stream, d->d_jobs, d->d_nblk, d->d_base,
+                     d->d_status);
+  hipLaunchKernelGGL(mij::k_dec_write, grid, dim3(256), 0, d->stream, a, d->d_base, d->d_coef, d->d_status);
   HIP_TRY(hipGetLastError());
   std::vector<int> st(nj);
   HIP_TRY(hipMemcpyAsync(st.data(), d->d_status, nj * sizeof(int), hipMemcpyDeviceToHost, d->stream));
@@ -422,6 +627,8 @@ extern "C" int mij_decoder_decode(mij_decoder *d, const uint8_t *const *jpgs, co
     if (st[j]) return mij_fail(MIJ_EJPEG, "stream %d scan %d: corrupt entropy data (%d)", j / 3, j % 3, st[j]);
   return MIJ_OK;
 }
+
+extern "C" int mij_decoder_passes(mij_decoder *d) { return d ? d->last_passes : -1; }
 
 extern "C" int mij_decoder_info(mij_decoder *d, int frame, int *w, int *h, uint8_t dqt[128]) {
   mij_clear_error();

@@ -31,7 +31,7 @@ EXPORTS = [
     # change detector (reference include/brain.h:7-10 drop-in + extensions)
     "subsample", "store", "compare", "enlargeAdjust", "mij_set_frame_height",
     "mij_decoder_create", "mij_decoder_destroy", "mij_decoder_decode", "mij_decoder_info",
-    "mij_decoder_coefs", "mij_decoder_device_coefs",
+    "mij_decoder_coefs", "mij_decoder_device_coefs", "mij_decoder_passes",
     "mij_detector_create", "mij_detector_destroy", "mij_detector_subsample", "mij_detector_compare",
     "mij_detector_step", "mij_detector_launch", "mij_detector_store", "mij_detector_upload", "mij_detector_get_plane",
     "mij_detector_set_plane", "mij_detector_mask", "mij_detector_stream",
@@ -164,6 +164,7 @@ def load() -> C.CDLL:
         lib.mij_decoder_coefs.argtypes = [p, i, p, p, p]
         lib.mij_decoder_device_coefs.restype = p
         lib.mij_decoder_device_coefs.argtypes = [p, i]
+        lib.mij_decoder_passes.argtypes = [p]
         lib.subsample.restype = None
         lib.subsample.argtypes = [p, p, p]
         lib.store.restype = None
@@ -706,6 +707,9 @@ class Decoder:
         ptrs = (C.c_void_p * n)(*[_ptr(b) for b in bufs])
         lens = (C.c_size_t * n)(*[len(s) for s in streams])
         _check(self.lib.mij_decoder_decode(self.h_, ptrs, lens, n), "decoder_decode")
+
+    def passes(self) -> int:
+        return int(self.lib.mij_decoder_passes(self.h_))
 
     def info(self, frame: int):
         w, h = C.c_int(), C.c_int()
