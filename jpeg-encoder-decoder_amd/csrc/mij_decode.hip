@@ -24,6 +24,9 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <algorithm>
+#include <atomic>
+#include <thread>
 #include <vector>
 
 #include "mij_host.h"
@@ -547,43 +550,65 @@ extern "C" int mij_decoder_decode(mij_decoder *d, const uint8_t *const *jpgs, co
   if (!d || !jpgs || !lens || n < 1 || n > d->cap) return mij_fail(MIJ_EINVAL, "decoder_decode: bad args");
   HIP_TRY(hipSetDevice(d->dev));
   d->parsed.assign(n, Parsed());
-  size_t total = 0;
-  for (int f = 0; f < n; f++) {
+  // host work per stream in parallel: parse (finds the scan ends), then
+  // unstuff each scan into its slot (sized by the raw length, an upper bound)
+  const int nth = std::max(1, std::min(n, (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()))));
+  auto parallel = [&](auto &&fn) {
+    std::atomic<int> next{0};
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nth; t++)
+      pool.emplace_back([&] { for (int f; (f = next++) < n;) fn(f); });
+    for (int f; (f = next++) < n;) fn(f);
+    for (auto &th : pool) th.join();
+  };
+  std::vector<int> prc(n, MIJ_OK);
+  for (int f = 0; f < n; f++)
     if (!jpgs[f]) return mij_fail(MIJ_EINVAL, "decoder_decode: stream %d is NULL", f);
-    if (int rc = parse(jpgs[f], lens[f], d->parsed[f], f)) return rc;
+  parallel([&](int f) { prc[f] = parse(jpgs[f], lens[f], d->parsed[f], f); });
+  for (int f = 0; f < n; f++) {
+    if (prc[f]) return mij_fail(prc[f], "decoder_decode: stream %d rejected", f);
     const Parsed &P = d->parsed[f];
     if (P.w > d->max_w || P.h > d->max_h)
       return mij_fail(MIJ_EINVAL, "stream %d: %dx%d exceeds the decoder's %dx%d", f, P.w, P.h, d->max_w, d->max_h);
-    total += lens[f] + 3 * 24;
   }
-  if (int rc = decoder_stage(d, total)) return rc;
+  // slots: raw scan length + >= 16 zero bytes, 8-aligned
+  std::vector<size_t> slot(3 * (size_t)n);
+  size_t off = 0;
+  for (int f = 0; f < n; f++)
+    for (int k = 0; k < 3; k++) {
+      slot[3 * f + k] = off;
+      const auto &sc = d->parsed[f].scan[k];
+      off = (off + (size_t)(sc.end - sc.data) + 16 + 7) & ~(size_t)7;
+    }
+  if (int rc = decoder_stage(d, off)) return rc;
   std::vector<mij::DecTab> tabs(4 * (size_t)n);
   std::vector<mij::DecJob> jobs(3 * (size_t)n);
-  size_t off = 0;
-  int nchunks = 0;
   const long long fs = d->plane_px * 3 / 2;  // int16 per frame slot
-  for (int f = 0; f < n; f++) {
+  parallel([&](int f) {
     const Parsed &P = d->parsed[f];
     for (int t = 0; t < 4; t++) tabs[4 * f + t] = P.tab[t];
     const long long ny = (long long)P.w * P.h;
     const long long base[3] = {f * fs, f * fs + ny, f * fs + ny + ny / 4};
     for (int k = 0; k < 3; k++) {
       const auto &sc = P.scan[k];
-      const size_t len = unstuff(d->h_blob + off, jpgs[f], (size_t)sc.data, (size_t)sc.end);
-      memset(d->h_blob + off + len, 0, 24 - (len & 7) % 8);
+      const size_t at = slot[3 * f + k];
+      const size_t len = unstuff(d->h_blob + at, jpgs[f], (size_t)sc.data, (size_t)sc.end);
+      const size_t next = (at + (size_t)(sc.end - sc.data) + 16 + 7) & ~(size_t)7;
+      memset(d->h_blob + at + len, 0, next - at - len);
       mij::DecJob &j = jobs[3 * f + k];
-      j.data = (long long)off;
+      j.data = (long long)at;
       j.nbits = 8LL * (long long)len;
       j.out = base[sc.comp];
       j.nblocks = (int)(sc.comp ? ny / 256 : ny / 64);
       j.dc = 4 * f + 2 * sc.td;
       j.ac = 4 * f + 2 * sc.ta + 1;
-      j.chunk0 = nchunks;
-      j.nchunks = (int)((j.nbits + mij::CHUNK - 1) / mij::CHUNK);
-      if (!j.nchunks) j.nchunks = 1;
-      nchunks += j.nchunks;
-      off = (off + len + 16 + 7) & ~(size_t)7;  // >= 16 zero bytes after each scan
     }
+  });
+  int nchunks = 0;
+  for (auto &j : jobs) {
+    j.chunk0 = nchunks;
+    j.nchunks = std::max(1, (int)((j.nbits + mij::CHUNK - 1) / mij::CHUNK));
+    nchunks += j.nchunks;
   }
   d->n = n;
   const int nj = 3 * n;
