@@ -346,6 +346,19 @@ def run_detect(args, world, rank, local, dist):
                      "ms_per_launch": round(k_ms, 4), "algorithmic_bytes_per_launch": k_bytes},
         "verified_areas": verified,
     }
+    # PMC-measured HBM bytes of the same kernel on the same workload
+    # (scripts/profile.sh detect -> profiles/rNN/detect/traffic.json)
+    import glob
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "detect", "traffic.json")), reverse=True):
+        d = json.load(open(path))
+        if d.get("config", {}).get("frame") != f"{W}x{H}":
+            continue
+        for name, v in d.get("kernels", {}).items():
+            if "k_detect<true>" in name:
+                res["roofline"]["traffic"] = v["hbm_bytes"]
+                res["roofline"]["traffic_source"] = (f"{os.path.relpath(path, REPO)} (rocprofv3 PMC "
+                                                     f"FETCH_SIZE x2 + WRITE_SIZE, same workload)")
+        break
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         use_ref = O.ref_brain_available() and O.ref_available()
         sub_fn = O.ref_subsample if use_ref else O.cref_subsample
