@@ -263,9 +263,15 @@ __global__ __launch_bounds__(256) void k_dec_scan(const DecJob *jobs, const int 
   if (threadIdx.x == 0) status[blockIdx.x] = carry >= job.nblocks ? 0 : 5;
 }
 
-// final pass: every chunk decodes from its settled entry and writes
+// final pass: every chunk decodes from its settled entry and writes.  A
+// lane assembles each block in its own LDS slot (128 B) and stores it whole
+// (8 x 16 B, zeros included: no memset of the planes).  A block split
+// between two chunks is stored in halves with 2-byte stores: the lane that
+// started it writes positions [first, k_exit), the next lane [k_entry, 64)
+// -- the settled states make k_exit == k_entry.
 __global__ __launch_bounds__(256) void k_dec_write(SyncArgs a, const long long *base, int16_t *coefs,
                                                    int *status) {
+  __shared__ int4 slot[256][8];
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= a.nchunks) return;
   const int j = job_of(a.jobs, a.njobs, c);
@@ -275,13 +281,65 @@ __global__ __launch_bounds__(256) void k_dec_write(SyncArgs a, const long long *
   long long pos = entry >> 6;
   int k = (int)(entry & 63);
   // the block in progress at the entry was started by an earlier chunk
-  const long long blk = base[c] - (k ? 1 : 0);
+  long long blk = base[c] - (k ? 1 : 0);
   if (blk >= job.nblocks) return;  // pad bits after the last block
   Bits br{(const unsigned long long *)(a.blob + job.data)};
   const long long stop = min((long long)(lc + 1) * CHUNK, job.nbits);
-  bool bad;
-  decode_span<true>(br, pos, k, stop, a.tabs[job.dc], a.tabs[job.ac], coefs + job.out, blk,
-                    job.nblocks - blk, &bad);
+  const DecTab &dc = a.tabs[job.dc], &ac = a.tabs[job.ac];
+  int4 *sl = slot[threadIdx.x];
+  int16_t *b16 = (int16_t *)sl;
+  int16_t *out = coefs + job.out;
+#pragma unroll
+  for (int q = 0; q < 8; q++) sl[q] = int4{0, 0, 0, 0};
+  int first = k;
+  bool bad = false;
+  while (pos < stop && blk < job.nblocks) {
+    int sym, val;
+    const int n = decode_one(br, pos, k ? ac : dc, sym, val);
+    if (!n) {
+      bad = true;
+      break;
+    }
+    pos += n;
+    if (k == 0) {
+      if (sym > 15) {
+        bad = true;
+        break;
+      }
+      b16[0] = (int16_t)val;
+      k = 1;
+    } else {
+      const int r = sym >> 4;
+      if (sym & 15) {
+        k += r;
+        if (k > 63) {
+          bad = true;
+          break;
+        }
+        b16[k++] = (int16_t)val;
+      } else {
+        k = r == 15 ? k + 16 : 64;  // ZRL / EOB
+      }
+    }
+    if (k >= 64) {  // block complete: store it, clear the slot
+      int16_t *o = out + 64 * blk;
+      if (first == 0) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) ((int4 *)o)[q] = sl[q];
+      } else {
+        for (int t = first; t < 64; t++) o[t] = b16[t];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; q++) sl[q] = int4{0, 0, 0, 0};
+      first = 0;
+      k = 0;
+      blk++;
+    }
+  }
+  if (!bad && k && blk < job.nblocks) {  // block continues in the next chunk
+    int16_t *o = out + 64 * blk;
+    for (int t = first; t < k; t++) o[t] = b16[t];
+  }
   if (bad) atomicMax(&status[j], 6);
 }
 
@@ -618,7 +676,6 @@ extern "C" int mij_decoder_decode(mij_decoder *d, const uint8_t *const *jpgs, co
                          d->stream));
   HIP_TRY(hipMemcpyAsync(d->d_jobs, jobs.data(), jobs.size() * sizeof(mij::DecJob), hipMemcpyHostToDevice,
                          d->stream));
-  HIP_TRY(hipMemsetAsync(d->d_coef, 0, (size_t)n * fs * sizeof(int16_t), d->stream));
   HIP_TRY(hipMemsetAsync(d->d_status, 0, nj * sizeof(int), d->stream));
   mij::SyncArgs a{d->d_blob, d->d_jobs, nj, nchunks, d->d_tabs, d->d_entry, d->d_exit[1], d->d_exit[0],
                   d->d_nblk, d->d_changed, 1};
