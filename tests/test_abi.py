@@ -73,3 +73,43 @@ def test_c_host_builds():
     pkg = os.path.dirname(mijpeg.LIB_PATH)
     subprocess.check_call(["make", "-s", "-C", pkg, "host/encode_ppm"])
     assert os.access(os.path.join(pkg, "host", "encode_ppm"), os.X_OK)
+
+
+MAIN_LOOP_C = r"""
+/* main.c:25-37 buffers and :136-163 loop body, as the reference writes them,
+ * compiled against mijpeg.h in place of brain.h / encoder.h / structs.h */
+#include "mijpeg.h"
+#define WIDTH 320
+#define HEIGHT 240
+#define PIX_LEN WIDTH*HEIGHT
+static uint8_t raw[3*PIX_LEN], sub[3*PIX_LEN/16], saved[3*PIX_LEN/16], jpg[3*PIX_LEN];
+static int16_t ordered_dct_Y[PIX_LEN], ordered_dct_Cb[PIX_LEN/4], ordered_dct_Cr[PIX_LEN/4];
+static area_t diffDims[100];
+static pair_t differences[2][WIDTH/8];
+static huff_code Luma[2], Chroma[2];
+int main(void) {
+  subsample(NULL, raw, sub);
+  store(sub, saved);
+  int different = compare(sub, saved, diffDims, differences);
+  for (int i = 0; i < different; i++) {
+    enlargeAdjust(&diffDims[i]);
+    rgb_to_dct(raw, ordered_dct_Y, ordered_dct_Cb, ordered_dct_Cr, diffDims[i]);
+    init_huffman(ordered_dct_Y, ordered_dct_Cb, ordered_dct_Cr, diffDims[i], Luma, Chroma);
+    FILE *f = fopen("/dev/null", "w");
+    (void)write_jpg(f, jpg, ordered_dct_Y, ordered_dct_Cb, ordered_dct_Cr, diffDims[i], Luma, Chroma);
+    fclose(f);
+  }
+  return 0;
+}
+"""
+
+
+def test_reference_main_loop_compiles_and_links(tmp_path):
+    """The reference's caller (brain.h + encoder.h calls with its own buffer
+    types, main.c:25-37/136-163) compiles warning-free against mijpeg.h and
+    links against libmijpeg.so (nothing is run: no GPU here)."""
+    src = tmp_path / "main_loop.c"
+    src.write_text(MAIN_LOOP_C)
+    pkg = os.path.dirname(mijpeg.LIB_PATH)
+    subprocess.check_call(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(REPO, "include"),
+                           str(src), "-L", pkg, "-lmijpeg", "-o", str(tmp_path / "main_loop")])
