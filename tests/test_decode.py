@@ -134,3 +134,35 @@ def test_corrupt_streams_rejected():
         d.decode([bytes(jpg)])                     # and still usable afterwards
     finally:
         d.close()
+
+
+@pytest.mark.gpu
+def test_round_trip_region_batch_and_config4():
+    """Streams of different sizes in one decode: the JFIFs of a region batch
+    (per-region SOF0 sizes) and one 7680x4320 config-4 frame."""
+    frame = np.ascontiguousarray(recipes.config3_frame(3, 1080, 1920))
+    regions = [(0, 0, 16, 16), (32, 48, 320, 240), (1904 - 512, 1064 - 256, 512, 256),
+               (7, 5, 1008, 64), (600, 400, 48, 1024 - 400 + 16)]
+    regions = [r for r in regions if r[0] + r[2] <= 1920 and r[1] + r[3] <= 1080]
+    cw, ch = max(r[2] for r in regions), max(r[3] for r in regions)
+    b = mijpeg.Batch(cw, ch, len(regions), 50, keep_coefs=True)
+    big = np.ascontiguousarray(recipes.config4_frame(0))
+    b4 = mijpeg.Batch(7680, 4320, 1, 50, keep_coefs=True)
+    d = mijpeg.Decoder(7680, 4320, len(regions) + 1)
+    try:
+        b.upload_regions(frame, regions)
+        b.encode(len(regions))
+        b4.upload(big[None])
+        b4.encode(1)
+        streams = [b.output(i) for i in range(len(regions))] + [b4.output(0)]
+        d.decode(streams)
+        for i, r in enumerate(regions):
+            assert d.info(i)[:2] == (r[2], r[3])
+            for g, w in zip(d.coefs(i), b.coefs(i, diffed=True)):
+                assert (g == w).all(), r
+        for g, w in zip(d.coefs(len(regions)), b4.coefs(0, diffed=True)):
+            assert (g == w).all()
+    finally:
+        b.close()
+        b4.close()
+        d.close()

@@ -202,3 +202,21 @@ def test_enlarge_adjust_drop_in():
     for a in [(0, 0, 0, 0), (5, 7, 20, 9), (70, 50, 79, 59), (0, 0, 79, 59), (78, 1, 79, 3)]:
         want = O.cref_area_adjust(a, 320, 240)
         assert mijpeg.drop_in_enlarge_adjust(a, 320, 240) == want
+
+
+@pytest.mark.gpu
+def test_detector_config4_frame():
+    """7680x4320 (config 4 size) against the oracle: planes, mask, areas."""
+    W, H = 7680, 4320
+    stored, cur = recipes.detect_scene(400, W, H, "objects")
+    d = mijpeg.Detector(W, H)
+    try:
+        d.subsample(d.upload(stored))
+        d.store()
+        got = d.step(d.upload(cur))
+        s0, s1 = O.cref_subsample(stored), O.cref_subsample(cur)
+        assert (d.plane(0) == s1).all() and (d.plane(1) == s0).all()
+        assert (d.mask() == numpy_mask(s1, s0)).all()
+        assert got == O.cref_compare(s1, s0, W, H)
+    finally:
+        d.close()
