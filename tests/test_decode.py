@@ -166,3 +166,18 @@ def test_round_trip_region_batch_and_config4():
         b.close()
         b4.close()
         d.close()
+
+
+@pytest.mark.gpu
+def test_decode_badly_synchronising_stream():
+    """Q=100 uniform noise: blocks of ~1000 bits, longer than a chunk, so
+    chunks rarely self-synchronise -- many passes, still bit-exact."""
+    f = np.random.default_rng(5).integers(0, 256, (256, 512, 3), dtype=np.uint8)
+    Y, Cb, Cr, _, jpg = O.cref_stages(f, 100)
+    d = mijpeg.Decoder(512, 256, 1)
+    try:
+        d.decode([jpg])
+        for g, w in zip(d.coefs(0), (Y, Cb, Cr)):
+            assert (g == w).all()
+    finally:
+        d.close()
