@@ -12,7 +12,7 @@
 //
 // Host: marker parsing (SOI, APP0, DQT, DHT, SOF0, SOS, EOI), canonical
 // Huffman tables with a 9-bit lookahead, and the scans copied unstuffed
-// into one pinned staging blob.  Device: every scan is cut into 2048-bit
+// into one pinned staging blob.  Device: every scan is cut into 512-bit
 // chunks, one lane per chunk.  Entropy decoding is sequential by
 // construction, so the chunks' entry states (bit position, coefficient
 // index) are found by self-synchronisation: each chunk first decodes from
