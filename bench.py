@@ -69,8 +69,10 @@ def parse():
                     help="regions workload: rectangles per frame (main.c's diffDims holds up to 100)")
     ap.add_argument("--region-frame", default="1920x1080",
                     help="regions workload: the frame the rectangles are cut from")
-    ap.add_argument("--verify", type=int, default=2,
-                    help="frames re-checked against the oracle after timing")
+    ap.add_argument("--verify", type=int, default=-1,
+                    help="frames re-checked against the oracle after timing (-1: every frame "
+                         "of the batch; config3 checks each distinct content with the oracle and "
+                         "the reference-build sha256 of tests/golden, then every slot's bytes)")
     return ap.parse_args()
 
 
@@ -140,7 +142,7 @@ def run_config4(args, world, rank, local, dist):
         "value": round(px / el / 1e6, 1), "unit": "Mpixels/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "int8",
+        "scaling": "strong", "vs_baseline": None, "dtype": "int8-MFMA exact + fp64 replay (bit-exact)",
         "data": f"synthetic: SURVEY §8(d) config-4 recipe, {distinct} distinct frames",
         "config": {"workload": f"config 4: {n} frames of {W}x{H} per step, each split into {world} "
                                f"MCU-row bands (one per rank) with DC/histogram/bit-offset "
@@ -218,7 +220,7 @@ def run_regions(args, world, rank, local, dist):
         "value": round(px_all / el / 1e6, 1), "unit": "Mpixels/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "int8",
+        "scaling": "weak", "vs_baseline": None, "dtype": "int8-MFMA exact + fp64 replay (bit-exact)",
         "data": "synthetic: config-3 recipe frame, seeded rectangles",
         "config": {"workload": f"regions: {len(regions)} rectangles (16..512 px a side, "
                                f"{px / 1e6:.2f} Mpixels) of one {W}x{H} frame per step, each its own JFIF "
@@ -457,6 +459,49 @@ def make_frames(args, rank):
     return out
 
 
+def verify_batch(batch, frames, F, args, rank):
+    """(slots verified, distinct contents pinned to the reference sha256)."""
+    import hashlib
+    import oracle as O
+    gold = {}
+    path = os.path.join(REPO, "tests", "golden", "manifest.json")
+    if os.path.exists(path):
+        gold = json.load(open(path))["cases"]
+    n = F if args.verify < 0 else min(args.verify, F)
+    want, pinned = {}, 0
+    for c in range(min(len(frames), n)):
+        want[c] = O.cref_encode(frames[c], args.quality)
+        key = f"config3_frame{rank * args.distinct + c}"
+        g = gold.get(key)
+        if (g and g["quality"] == args.quality and (args.width, args.height) == (3840, 2160)
+                and g["frame"] == [args.width, args.height]):
+            if hashlib.sha256(want[c]).hexdigest() != g["jpg_sha256"]:
+                raise SystemExit(f"bench: oracle bytes of {key} differ from the reference golden")
+            pinned += 1
+    for i in range(n):
+        if batch.output(i) != want[i % len(frames)]:
+            raise SystemExit(f"bench: frame {i} differs from the oracle")
+    return n, pinned
+
+
+def util_counters(kernel_sym):
+    """VALU / MFMA utilisation of `kernel_sym` from the newest profiles/rNN/util.json
+    (scripts/pmc_util.sh + scripts/util.py: rocprofv3 PMC passes of this bench's
+    default workload).  mfma_util = matrix-pipe busy cycles / (1024 SIMDs x
+    cycles) -- 1.0 is the dense i8 peak at the clock held; valu_util = VALU
+    issue slots used (2 cycles per wave64 instruction) / available."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "util.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        for name, v in d.get("kernels", {}).items():
+            if kernel_sym in name:
+                return v, os.path.relpath(path, REPO)
+    return None, None
+
+
 # rocprofv3 symbol of each K1 variant (for the PMC traffic lookup)
 K1_SYMBOL = {"k_mcu_dct<COEF_OUT>": "k_mcu_dct<1>", "k_mcu_dct<TOK_OUT>": "k_mcu_dct<2>",
              "k_mcu_dct<COEF_IN|TOK_OUT>": "k_mcu_dct<6>"}
@@ -597,14 +642,12 @@ def main():
     if args.mode == "dct":
         stage_avg = {"k1_colour_dct_quant": k1_ms}
 
-    # correctness spot check after timing (not timed): frames vs the oracle
-    verified = 0
+    # correctness after timing (not timed): every distinct content against
+    # the oracle and, where tests/golden holds it, the reference build's
+    # sha256; then every slot of the batch against its content's bytes
+    verified, pinned = 0, 0
     if args.verify and args.mode == "encode" and not os.environ.get("MIJ_K1_FLAGS"):
-        import oracle as O
-        for i in range(min(args.verify, F)):
-            if batch.output(i) != O.cref_encode(frames[i % len(frames)], args.quality):
-                raise SystemExit(f"bench: frame {i} differs from the oracle")
-            verified += 1
+        verified, pinned = verify_batch(batch, frames, F, args, rank)
 
     # the coefficient-output K1 variant (BASELINE.json north_star's "fused
     # DCT+quant kernel" at 6 B/px) is not on the default (fused) path: a few
@@ -652,7 +695,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int8",
+        "dtype": "int8-MFMA exact + fp64 replay (bit-exact)",
         "data": f"synthetic: SURVEY §8(d) config-3 recipe, {args.distinct} distinct frames "
                 f"cycled over the batch",
         "config": {"workload": f"config 3: {F} x {W}x{H} BGR888 frames per GPU, 4:2:0, "
@@ -670,6 +713,7 @@ def main():
                     for k, v in kernels.items()},
         "stages_ms": stage_avg,
         "verified_frames": verified,
+        "verified_contents_pinned_to_reference_sha": pinned,
         # blocks re-encoded in FP64 by k_fix_blocks (split pipeline) or coefficients
         # replayed in place (fused pipeline), per frame
         "fp64_fixups_per_frame": round(replays / (F * (args.warmup + args.steps)), 2),
@@ -683,6 +727,22 @@ def main():
             "frac": round(cb / (coef_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "ms_per_launch": round(coef_ms, 4), "algorithmic_bytes_per_launch": int(cb),
             "launches": args.coef_launches}
+        u1, usrc1 = util_counters("k_mcu_dct<1>")
+        if u1 is not None:
+            res["roofline_k1_coefficient_variant"].update(
+                mfma_util=u1.get("mfma_util"), valu_util=u1.get("valu_util"), util_source=usrc1)
+    u, usrc = util_counters(K1_SYMBOL.get(dom, dom))
+    if u is not None:
+        res["roofline"]["mfma_util"] = u.get("mfma_util")
+        res["roofline"]["valu_util"] = u.get("valu_util")
+        res["roofline"]["util_source"] = (f"{usrc} (rocprofv3 PMC: SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU, "
+                                          f"GRBM_GUI_ACTIVE; same workload)")
+        if u.get("SQ_INSTS_MFMA"):
+            # v_mfma_i32_16x16x64_i8: 16*16*64 MACs = 32768 int8 ops each;
+            # dense i8 peak 5 POP/s (MI355X_MICROARCH.md, 2x bf16's 2.5 PF)
+            tops = u["SQ_INSTS_MFMA"] * 32768 / (dom_ms * 1e-3) / 1e12
+            res["roofline"]["mfma_i8_TOPs"] = round(tops, 1)
+            res["roofline"]["mfma_frac_of_i8_peak"] = round(tops / 5000.0, 4)
     traffic, src = pmc_traffic(dom, res["config"])
     if traffic is not None:
         res["roofline"]["traffic"] = traffic

@@ -173,7 +173,9 @@ void *mij_batch_stream(mij_batch *b);
  * slot.  Each region gets its own tables and JFIF (SOF0 = w_i x h_i); the
  * bytes are those of the three drop-in calls on that region. */
 /* per-frame sizes of the next encodes (multiples of 16, at most the batch
- * geometry); wh = {w0, h0, w1, h1, ...}; NULL restores the batch geometry */
+ * geometry); wh = {w0, h0, w1, h1, ...}; NULL restores the batch geometry.
+ * A full-frame mij_batch_upload / mij_batch_set_input also restores it: call
+ * this after uploading when the uploaded frames are smaller than the canvas. */
 int mij_batch_set_frame_dims(mij_batch *b, const int *wh, int nframes);
 /* regions of a device-resident BGR frame (rows pitch bytes apart) into
  * slots 0..n-1 (one gather launch) and their sizes as the frame dims */

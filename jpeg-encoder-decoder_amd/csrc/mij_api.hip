@@ -394,6 +394,7 @@ extern "C" int mij_batch_upload(mij_batch *b, const uint8_t *bgr, int first, int
     return fail(MIJ_EINVAL, "upload: bad args");
   if (!b->own_in) return fail(MIJ_EINVAL, "upload: batch reads external device input");
   HIP_TRY(hipSetDevice(b->dev));
+  b->use_fdims = false;  // full frames: the batch geometry again (set_frame_dims after, if wanted)
   HIP_TRY(hipMemcpyAsync(b->d_in + (long long)first * b->in_fs, bgr, (size_t)nframes * b->in_fs,
                          hipMemcpyHostToDevice, b->stream));
   HIP_TRY(hipStreamSynchronize(b->stream));
@@ -409,6 +410,7 @@ extern "C" int mij_batch_set_input(mij_batch *b, const void *d_bgr, long long fr
   HIP_TRY(hipSetDevice(b->dev));
   if (b->own_in && b->d_in) HIP_TRY(hipFree(b->d_in));
   b->own_in = false;
+  b->use_fdims = false;  // full frames: the batch geometry again
   b->d_in = (uint8_t *)d_bgr;
   b->in_fs = frame_stride;
   b->pitch = pitch;
@@ -670,6 +672,7 @@ int mij_batch_upload_async(mij_batch *b, const uint8_t *host, int nframes) {
   if (!b || !host || nframes < 1 || nframes > b->cap || !b->own_in)
     return fail(MIJ_EINVAL, "upload_async: bad args");
   HIP_TRY(hipSetDevice(b->dev));
+  b->use_fdims = false;
   HIP_TRY(hipMemcpyAsync(b->d_in, host, (size_t)nframes * b->in_fs, hipMemcpyHostToDevice, b->stream));
   return MIJ_OK;
 }

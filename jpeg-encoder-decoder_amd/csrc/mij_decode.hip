@@ -365,6 +365,7 @@ struct Parsed {
     long long data, end;
   } scan[3];
   int nscans = 0;
+  int comp_seen = 0;  // components that already have a scan (bit c)
 };
 
 int be16(const uint8_t *p) { return (p[0] << 8) | p[1]; }
@@ -444,6 +445,10 @@ int parse(const uint8_t *s, size_t n, Parsed &P, int frame) {
       sc.td = q[2] >> 4;
       sc.ta = q[2] & 15;
       if (sc.comp < 0 || sc.comp > 2 || sc.td > 1 || sc.ta > 1) BAD("stream %d: SOS component", frame);
+      // each component exactly once: a repeated scan would leave another
+      // component's plane unwritten (it keeps the previous call's values)
+      if (P.comp_seen & (1 << sc.comp)) BAD("stream %d: SOS repeats component %d", frame, sc.comp + 1);
+      P.comp_seen |= 1 << sc.comp;
       size_t e = i + 2 + len;
       sc.data = (long long)e;
       // entropy data ends at the next marker: a 0xFF followed by neither
@@ -588,11 +593,13 @@ static size_t unstuff(uint8_t *dst, const uint8_t *s, size_t b, size_t e) {
 
 static int decoder_buffers(mij_decoder *d, int nchunks, int njobs) {
   if (nchunks <= d->chunk_cap && njobs <= d->job_cap) return MIJ_OK;
-  hipFree(d->d_entry);
-  hipFree(d->d_exit[0]);
-  hipFree(d->d_exit[1]);
-  hipFree(d->d_nblk);
-  hipFree(d->d_base);
+  // null each pointer once freed: a failed hipMalloc below must not leave
+  // one dangling for the next call or decoder_free to free again
+  for (void **p : {(void **)&d->d_entry, (void **)&d->d_exit[0], (void **)&d->d_exit[1], (void **)&d->d_nblk,
+                   (void **)&d->d_base}) {
+    hipFree(*p);
+    *p = nullptr;
+  }
   d->chunk_cap = 0;
   const size_t n = (size_t)nchunks + nchunks / 4 + 1024;
   HIP_TRY(hipMalloc((void **)&d->d_entry, n * sizeof(long long)));
@@ -611,6 +618,7 @@ extern "C" int mij_decoder_decode(mij_decoder *d, const uint8_t *const *jpgs, co
   mij_clear_error();
   if (!d || !jpgs || !lens || n < 1 || n > d->cap) return mij_fail(MIJ_EINVAL, "decoder_decode: bad args");
   HIP_TRY(hipSetDevice(d->dev));
+  d->n = 0;  // set to n only once every stream decoded cleanly
   d->parsed.assign(n, Parsed());
   // host work per stream in parallel: parse (finds the scan ends), then
   // unstuff each scan into its slot (sized by the raw length, an upper bound)
@@ -673,7 +681,6 @@ extern "C" int mij_decoder_decode(mij_decoder *d, const uint8_t *const *jpgs, co
     nchunks += j.nchunks;
     max_chunks = std::max(max_chunks, j.nchunks);
   }
-  d->n = n;
   const int nj = 3 * n;
   if (int rc = decoder_buffers(d, nchunks, nj)) return rc;
   HIP_TRY(hipMemcpyAsync(d->d_blob, d->h_blob, off, hipMemcpyHostToDevice, d->stream));
@@ -715,6 +722,7 @@ extern "C" int mij_decoder_decode(mij_decoder *d, const uint8_t *const *jpgs, co
   HIP_TRY(hipStreamSynchronize(d->stream));
   for (int j = 0; j < nj; j++)
     if (st[j]) return mij_fail(MIJ_EJPEG, "stream %d scan %d: corrupt entropy data (%d)", j / 3, j % 3, st[j]);
+  d->n = n;
   return MIJ_OK;
 }
 

@@ -341,9 +341,11 @@ class Batch:
         frames_bgr = np.ascontiguousarray(frames_bgr, np.uint8)
         n = frames_bgr.shape[0] if frames_bgr.ndim == 4 else 1
         _check(self.lib.mij_batch_upload(self.h_, _ptr(frames_bgr), first, n), "upload")
+        self.fdims = None  # full frames: the library restored the batch geometry
 
     def set_input(self, dev_ptr: int, frame_stride: int, pitch: int) -> None:
         _check(self.lib.mij_batch_set_input(self.h_, dev_ptr, frame_stride, pitch), "set_input")
+        self.fdims = None
 
     def encode(self, n: int) -> None:
         _check(self.lib.mij_batch_encode(self.h_, n), "encode")

@@ -128,6 +128,18 @@ def main() -> None:
         C[k]["input"] = f"recipes.config3_frame({f})"
     C["config3_uniform0"] = case_q50("config3_uniform0", recipes.config3_uniform(0))
     C["config3_uniform0"]["input"] = "recipes.config3_uniform(0)"
+    # the rest of bench.py's 16 distinct config-3 contents (rank 0): every
+    # slot of the timed 256-frame batch is checked against these
+    for f in range(2, 16):
+        k = f"config3_frame{f}"
+        C[k] = case_q50(k, recipes.config3_frame(f))
+        C[k]["input"] = f"recipes.config3_frame({f})"
+
+    print("config 4 frames (7680x4320)")
+    for f in (0, 1):
+        k = f"config4_frame{f}"
+        C[k] = case_q50(k, recipes.config4_frame(f))
+        C[k]["input"] = f"recipes.config4_frame({f})"
 
     print("quality sweep via original.c set_quality")
     with tempfile.TemporaryDirectory() as d:

@@ -1,20 +1,14 @@
 #!/bin/bash
-# scripts/gpu_check.sh -- one GPU session: smoke, parity tests, a short bench.
-# Every GPU step has its own time limit; a crash/abort/timeout stops the script.
-set -u
+# scripts/gpu_check.sh -- GPU parity suite, then the default bench line
+# (every slot verified) and smoke(); stops at the first failing step.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-step() {  # step <name> <seconds> <cmd...>; ok for exit 0/1 (test failures)
-  local name=$1 secs=$2; shift 2
-  echo "== $name"
-  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
-  local rc=$?
-  echo "== $name rc=$rc"; tail -n 15 "gpurun_out/$name.log"
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
-}
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step pytest_gpu 900 python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS:-}
-if [ "${BENCH:-1}" = 1 ]; then
-  step bench 600 python bench.py ${BENCH_ARGS:---steps 5 --warmup 2}
-fi
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+tail -3 gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/pytest_gpu.log | head -20; exit $rc; }
+[ -n "${NO_BENCH:-}" ] && exit 0
+timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1 || { tail -5 gpurun_out/bench.log; exit 1; }
+tail -1 gpurun_out/bench.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -5 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log

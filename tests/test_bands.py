@@ -78,6 +78,31 @@ def test_bands_config4_shape_two_bands():
     b.close()
 
 
+def _sha(b: bytes) -> str:
+    import hashlib
+    return hashlib.sha256(b).hexdigest()
+
+
+@pytest.mark.parametrize("f", [0, 1])
+def test_config4_frames_match_reference_goldens(f, manifest):
+    """SURVEY §8(d) config 4 at full size: the 7680x4320 frames encoded whole
+    and in 2, 4 and 8 MCU-row bands give the reference's bytes (sha256 of the
+    reference build's output, tests/golden/manifest.json, oracle/gen_golden.py)."""
+    import mijpeg
+    import recipes
+    want = manifest[f"config4_frame{f}"]
+    frame = recipes.config4_frame(f)[None]
+    b = mijpeg.Batch(7680, 4320, 1)
+    b.upload(frame)
+    b.encode(1)
+    got = b.output(0)
+    b.close()
+    assert (len(got), _sha(got)) == (want["jpg_len"], want["jpg_sha256"])
+    for world in (2, 4, 8):
+        got = encode_banded_local(frame, world)[0]
+        assert (len(got), _sha(got)) == (want["jpg_len"], want["jpg_sha256"]), f"{world} bands"
+
+
 def _free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
