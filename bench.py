@@ -478,9 +478,9 @@ def verify_batch(batch, frames, F, args, rank):
             if hashlib.sha256(want[c]).hexdigest() != g["jpg_sha256"]:
                 raise SystemExit(f"bench: oracle bytes of {key} differ from the reference golden")
             pinned += 1
-    for i in range(n):
-        if batch.output(i) != want[i % len(frames)]:
-            raise SystemExit(f"bench: frame {i} differs from the oracle")
+    bad = [i for i in range(n) if batch.output(i) != want[i % len(frames)]]
+    if bad:
+        raise SystemExit(f"bench: {len(bad)} frames differ from the oracle: {bad[:16]}")
     return n, pinned
 
 

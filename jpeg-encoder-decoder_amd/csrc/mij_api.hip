@@ -265,6 +265,9 @@ struct mij_batch {
   std::vector<int2> h_fdims;
   uint8_t *d_frame = nullptr;
   size_t frame_cap = 0;
+  // k_pack_lb needs all-zero scan buffers; k_emit_write leaves them so, the
+  // band paths (k_scan + k_pack, no emit) do not
+  bool raw_dirty = false;
   bool keep_coefs = false;  // encode also writes coefficient planes
   bool rgb = false;         // input frames in R, G, B byte order (PPM) instead of B, G, R
   bool split = false;       // true: K1 writes coefficients, a second pass tokenizes;
@@ -342,6 +345,7 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
   HIP_TRY(dalloc(&b->d_seg_bits, F * g.nseg));
   HIP_TRY(dalloc(&b->d_seg_off, F * g.nseg));
   HIP_TRY(dalloc(&b->d_raw, F * g.raw_fs));
+  HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * F * g.raw_fs, b->stream));
   HIP_TRY(dalloc(&b->d_scan_bits, F * 3));
   HIP_TRY(dalloc(&b->d_out_len, F));
   HIP_TRY(dalloc(&b->d_hc, F * 4));
@@ -531,7 +535,37 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   if (!tables_given) HIP_TRY(launch_tables(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[5], b->stream));
   // segment bits, scan offsets and packing in one look-back pass
+  if (b->raw_dirty) {
+    HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->cap * b->g.raw_fs, b->stream));
+    b->raw_dirty = false;
+  }
+  // diagnostics (MIJ_PACK_TIME with the diag build): per-group phase times of k_pack_lb
+  static const bool ptime = getenv("MIJ_PACK_TIME") != nullptr;
+  const long long ngroups = (long long)nframes * ((b->g.nsy + PACK_SEGS - 1) / PACK_SEGS +
+                                                  2 * ((b->g.nsc + PACK_SEGS - 1) / PACK_SEGS));
+  if (ptime) {
+    HIP_TRY(hipMalloc(&a.dbg, sizeof(unsigned long long) * 4 * ngroups));
+    HIP_TRY(hipMemsetAsync(a.dbg, 0, sizeof(unsigned long long) * 4 * ngroups, b->stream));
+  }
   HIP_TRY(launch_pack_lb(a, b->stream));
+  if (ptime) {
+    std::vector<unsigned long long> h(4 * ngroups);
+    HIP_TRY(hipMemcpyAsync(h.data(), a.dbg, sizeof(unsigned long long) * 4 * ngroups, hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    HIP_TRY(hipFree(a.dbg));
+    a.dbg = nullptr;
+    double ph[3] = {0};
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (long long g = 0; g < ngroups; g++) {
+      const unsigned long long *r = &h[4 * g];
+      for (int k = 0; k < 3; k++) ph[k] += (double)(r[k + 1] - r[k]);
+      t0 = std::min(t0, r[0]);
+      t1 = std::max(t1, r[3]);
+    }
+    // s_memrealtime ticks at 100 MHz
+    fprintf(stderr, "pack groups %lld: span %.1f us, per group: ticket+bits %.2f us, look-back %.2f us, pack %.2f us\n",
+            ngroups, (t1 - t0) / 100.0, ph[0] / ngroups / 100.0, ph[1] / ngroups / 100.0, ph[2] / ngroups / 100.0);
+  }
   if (t) HIP_TRY(hipEventRecord(b->ev[6], b->stream));
   HIP_TRY(launch_emit(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[7], b->stream));
@@ -1161,6 +1195,7 @@ extern "C" int mij_band_pack(mij_batch *b, int n, const unsigned long long *bit_
   HIP_TRY(hipMemcpyAsync(b->d_bitbase, base.data(), sizeof(uint32_t) * n * 4, hipMemcpyHostToDevice,
                          b->stream));
   EntArgs a = ent_args(b, n);
+  b->raw_dirty = true;  // the band words stay in the scan buffers (no emit)
   HIP_TRY(launch_scan(a, b->stream));
   HIP_TRY(launch_pack(a, b->stream));
   std::vector<unsigned long long> tot((size_t)n * 3);

@@ -612,8 +612,13 @@ constexpr int k1_base(int mode) { return mode & ~(K1M_RGB | K1M_REGIONS); }
 // per-wave token staging and run 4-wave workgroups, two per CU.
 template <int MODE>
 constexpr bool k1_wide() { return k1_base(MODE) == K1M_COEF_OUT || k1_base(MODE) == K1M_TOK_OUT; }
+#ifndef MIJ_K1_TOK_WAVES
+#define MIJ_K1_TOK_WAVES 12
+#endif
 template <int MODE>
-constexpr int k1_waves() { return k1_wide<MODE>() ? 12 : 4; }
+constexpr int k1_waves() {
+  return k1_base(MODE) == K1M_TOK_OUT ? MIJ_K1_TOK_WAVES : (k1_wide<MODE>() ? 12 : 4);
+}
 
 template <int MODE>
 __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) void k_mcu_dct(K1Args a) {
@@ -638,7 +643,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   // colour-exception bitmaps: in LDS for the coefficient variant; the wide
   // token variant reads them from global memory (rare path, L1/L2 hits) to
   // fit its token staging into the 160 KB
-  constexpr bool LUT_LDS = PIX && !(TOK && NW == 12);
+  constexpr bool LUT_LDS = PIX && !(TOK && NW >= 8);
   __shared__ uint32_t s_lut[LUT_LDS ? 3 * LUT_WORDS : 1];
   __shared__ double s_cos[64];
   __shared__ int s_qint[2][64];
@@ -1635,12 +1640,24 @@ __global__ __launch_bounds__(256) void k_pack(EntArgs a) {
 // ticket keeps groups claimed in scan order), sums its segments' token bits,
 // and finds the group's start bit by decoupled look-back over the groups
 // before it in the same scan (per group: aggregate, then inclusive prefix,
-// published in one 64-bit word).  The shared edge words: a group zeroes its
-// last word before it publishes its prefix (the next group ORs into that
-// word only after reading the prefix) and ORs both of its edge words;
-// interior words are stored plainly.  Then it packs as k_pack does.
+// published in one 64-bit word).  Then it packs as k_pack does: 16 lanes (a
+// DPP row) per segment place their tokens by a row scan of token bits and OR
+// the pieces into an LDS window.
+//
+// The scan buffers are all-zero when this kernel starts (k_emit_write zeroes
+// every word it consumes; the host clears them after the band paths), so a
+// group ORs its first and last word, which it may share with a neighbour
+// group, and stores its interior words plainly: no ordering between groups
+// beyond the prefix itself.  (Measured against this two-read form: staging a
+// group's tokens in LDS to read them once ran 1.72 ms instead of 1.31 ms per
+// config-3 step -- the 48 KB staging cut residency from 8 to 3 groups per CU,
+// and the kernel is latency-bound.)
 // ===========================================================================
 constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1;
+#ifndef MIJ_LB_DEPTH
+#define MIJ_LB_DEPTH 12
+#endif
+constexpr int LB_DEPTH = MIJ_LB_DEPTH;  // token loads in flight per lane
 
 __global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
   __shared__ uint32_t buf[PACK_WORDS];
@@ -1650,6 +1667,13 @@ __global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
   __shared__ int s_ticket;
   const Geom &G = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef MIJ_K1_DIAG
+  unsigned long long tstamp[4];
+#define LB_STAMP(k) tstamp[k] = __builtin_amdgcn_s_memrealtime()
+#else
+#define LB_STAMP(k)
+#endif
+  LB_STAMP(0);
   if (tid == 0) s_ticket = (int)atomicAdd(a.pack_ticket, 1u);
   __syncthreads();
   const int gid = s_ticket;  // groups in (frame, scan, q) order
@@ -1670,36 +1694,37 @@ __global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
   const int gscan0 = gid - q;  // ticket of the scan's first group
   const int chroma = comp != 0;
   const int s0 = q * PACK_SEGS, s1 = min(ns, s0 + PACK_SEGS), nsg = s1 - s0;
-  const long long fs0 = (long long)f * G.nseg + sbase;
+  const long long fs0 = (long long)f * G.nseg + sbase + s0;  // the group's first segment
   for (int i = tid; i < 512; i += 256) tab[i >> 8][i & 255] = a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + i];
   __syncthreads();
   const uint32_t zac = tab[1][0xF0];
-  const int Lz = (int)(zac >> 16);
+  const uint32_t Lz = zac >> 16;
   // ---- 1. bits of each segment (16 lanes per segment) --------------------
   const int sub = tid & 15, row = tid >> 4;
   for (int sl = row; sl < nsg; sl += 16) {
-    const long long fs = fs0 + s0 + sl;
+    const long long fs = fs0 + sl;
     const int n = min((int)a.seg_ntok[fs], SEG_TOK);
     const uint32_t *tk = a.tok + fs * SEG_TOK;
     uint32_t b = 0;
-    for (int i0 = 0; i0 < n; i0 += 64) {
-      uint32_t t[4];
+    for (int i0 = 0; i0 < n; i0 += 16 * LB_DEPTH) {
+      uint32_t t[LB_DEPTH];
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
+      for (int u = 0; u < LB_DEPTH; u++) {
         const int i = i0 + 16 * u + sub;
         t[u] = i < n ? tk[i] : 0u;
       }
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
+      for (int u = 0; u < LB_DEPTH; u++) {  // encoder.c:434-460, ZRLs :490-494
         const uint32_t tk4 = t[u], sym = tk4 & 255u;
         if (i0 + 16 * u + sub < n)
-          b += (tab[(tk4 & TOK_AC) ? 1 : 0][sym] >> 16) + (sym & 15u) + ((tk4 >> 8) & 3u) * (uint32_t)Lz;
+          b += (tab[(tk4 & TOK_AC) ? 1 : 0][sym] >> 16) + (sym & 15u) + ((tk4 >> 8) & 3u) * Lz;
       }
     }
     b = row_scan16(b);
     if (sub == 15) s_bits[sl] = b;
   }
   __syncthreads();
+  LB_STAMP(1);
   // ---- 2. offsets inside the group, group total, look-back -----------------
   if (wave == 0) {
     const uint32_t v = lane < nsg ? s_bits[lane] : 0u;
@@ -1732,26 +1757,13 @@ __global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
       }
     }
     if (lane == 0) {
-      // zero the group's last word before the next group may OR into it; the
-      // first word of a scan is zeroed by its first group; a last word that is
-      // also the first word of a group starting mid-word belongs to the
-      // previous group, which zeroed it
-      const unsigned long long wf = prefix >> 5, wl = (prefix + T - 1) >> 5;
-      uint32_t *raw = a.raw + (long long)f * G.raw_fs +
-                      (comp == 0 ? 0 : G.raw_words[0] + (comp == 2 ? G.raw_words[1] : 0));
-      const bool ok = T > 0 && wl + 1 < (unsigned long long)G.raw_words[comp];
-      // (atomics: the per-XCD L2s are not coherent, so a plain store could be
-      // written back over the next group's OR; the state words need no fence,
-      // they carry their own data, relaxed at agent scope = coherent sc1 access)
-      if (ok && q == 0) atomicAnd(&raw[wf], 0u);
-      if (ok && (wl != wf || (prefix & 31) == 0)) atomicAnd(&raw[wl], 0u);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_store(&st[gid], LB_INC | (prefix + T), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (q == nq - 1) a.scan_bits[f * 3 + comp] = prefix + T;
       s_prefix = prefix;
     }
   }
   __syncthreads();
+  LB_STAMP(2);
   // ---- 3. pack the group's tokens (as k_pack) -------------------------------
   const unsigned long long gbase = s_prefix;
   const uint32_t bit0 = (uint32_t)(gbase & 31);
@@ -1769,32 +1781,31 @@ __global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
     for (uint32_t i = tid; i < wn; i += 256) buf[i] = 0;
     __syncthreads();
     for (int sl = row; sl < nsg; sl += 16) {
-      const long long fs = fs0 + s0 + sl;
+      const long long fs = fs0 + sl;
       const uint32_t sb = bit0 + s_off[sl];
       if (sb >= hi_bit || sb + s_bits[sl] <= lo_bit) continue;  // row-uniform
       const int n = min((int)a.seg_ntok[fs], SEG_TOK);
       const uint32_t *tk = a.tok + fs * SEG_TOK;
       uint32_t pos0 = sb;
-      uint32_t tq[4];  // tokens of the next 64, loaded ahead (latency-bound loop)
+      uint32_t tq[LB_DEPTH];  // tokens of the next 16 * LB_DEPTH, loaded ahead (latency-bound loop)
 #pragma unroll
-      for (int u = 0; u < 4; u++) tq[u] = 16 * u + sub < n ? tk[16 * u + sub] : 0u;
+      for (int u = 0; u < LB_DEPTH; u++) tq[u] = 16 * u + sub < n ? tk[16 * u + sub] : 0u;
       for (int i0 = 0; i0 < n; i0 += 16) {
         const int i = i0 + sub;
         const uint32_t t = tq[0];
-        tq[0] = tq[1];
-        tq[1] = tq[2];
-        tq[2] = tq[3];
-        tq[3] = i + 64 < n ? tk[i + 64] : 0u;
+#pragma unroll
+        for (int u = 0; u + 1 < LB_DEPTH; u++) tq[u] = tq[u + 1];
+        tq[LB_DEPTH - 1] = i + 16 * LB_DEPTH < n ? tk[i + 16 * LB_DEPTH] : 0u;
         const uint32_t sym = t & 255u, cls = sym & 15u;
         const uint32_t e = i < n ? tab[(t & TOK_AC) ? 1 : 0][sym] : 0u;
         const uint32_t nz = (t >> 8) & 3u;
         const uint32_t L = (e >> 16) + cls;
-        const uint32_t nb = i < n ? L + nz * (uint32_t)Lz : 0u;
+        const uint32_t nb = i < n ? L + nz * Lz : 0u;
         const uint32_t x = row_scan16(nb);
         uint32_t pos = pos0 + x - nb;
         if (nb && pos < hi_bit && pos + nb > lo_bit) {
           for (uint32_t k = nz; k; k--) {  // encoder.c:490-494 ZRL
-            put_bits_window(buf, pos, lo_bit, hi_bit, zac & 0xFFFFu, Lz);
+            put_bits_window(buf, pos, lo_bit, hi_bit, zac & 0xFFFFu, (int)Lz);
             pos += Lz;
           }
           if (L) put_bits_window(buf, pos, lo_bit, hi_bit, ((e & 0xFFFFu) << cls) | (t >> 16), (int)L);
@@ -1803,16 +1814,20 @@ __global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
       }
     }
     __syncthreads();
-    // the first word is shared with the previous group only when the group
-    // starts mid-word (then that group zeroed it); the last word was zeroed
-    // before the prefix was published
+    // the edge words may be shared with the neighbouring groups: OR (onto zero)
     for (uint32_t i = tid; i < wn; i += 256) {
       const uint32_t wi = w0 + i;
-      if ((wi == 0 && bit0) || wi == nw - 1) atomicOr(&raw[wi], buf[i]);
+      if (wi == 0 || wi == nw - 1) atomicOr(&raw[wi], buf[i]);
       else raw[wi] = buf[i];
     }
     __syncthreads();
   }
+#ifdef MIJ_K1_DIAG
+  LB_STAMP(3);
+  if (a.dbg && tid == 0)
+    for (int k = 0; k < 4; k++) a.dbg[(long long)gid * 4 + k] = tstamp[k];
+#endif
+#undef LB_STAMP
 }
 
 // ===========================================================================
@@ -1982,11 +1997,20 @@ __global__ __launch_bounds__(256) void k_emit_write(EntArgs a) {
   const int slot = blockIdx.x % EMIT_SLOTS, fc = blockIdx.x / EMIT_SLOTS;
   const int f = fc / 3, comp = fc - f * 3;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (!emit_frame_ok(a, f)) return;
+  // every scan-buffer word read here is zeroed after use: k_pack_lb needs
+  // all-zero buffers (a failed frame's buffers are cleared whole)
+  uint32_t *raw = (uint32_t *)scan_raw(a, f, comp);
+  if (!emit_frame_ok(a, f)) {
+    for (long long i = (long long)slot * 256 + tid; i < a.g.raw_words[comp]; i += EMIT_SLOTS * 256) raw[i] = 0;
+    return;
+  }
   uint8_t *out = a.out + (long long)f * a.g.out_cap;
   const long long nchmax = emit_chunks(a.g);
-  const unsigned long long nbytes = a.scan_bits[f * 3 + comp] >> 3;
-  const uint32_t *raw = scan_raw(a, f, comp);
+  const unsigned long long nbits = a.scan_bits[f * 3 + comp], nbytes = nbits >> 3;
+  if (slot == 0 && tid < 2) {  // words past the last whole byte (the pad byte's bits)
+    const unsigned long long w = ((nbytes + 3) >> 2) + tid;
+    if (w < ((nbits + 31) >> 5)) raw[w] = 0;
+  }
   const long long nch = (long long)((nbytes + EMIT_CH - 1) / EMIT_CH);
   const uint32_t *cnt = a.ffc + (long long)fc * nchmax;
   const uint32_t *offs = a.choff + (long long)fc * nchmax;
@@ -2012,6 +2036,9 @@ __global__ __launch_bounds__(256) void k_emit_write(EntArgs a) {
     }
 #pragma unroll
     for (int k = 0; k < WPW / 64; k++) wcnt += lims[k] ? ff_bytes(wds[k], lims[k]) : 0;
+#pragma unroll
+    for (int k = 0; k < WPW / 64; k++)
+      if (lims[k]) raw[(wb0 + 4ull * (64 * k + lane)) >> 2] = 0u;
     for (int off = 32; off; off >>= 1) wcnt += __shfl_xor(wcnt, off);
     if (lane == 0) red[wave] = wcnt;
     __syncthreads();

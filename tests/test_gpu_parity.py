@@ -279,3 +279,24 @@ def test_fused_pipeline_keep_coefs_golden(manifest):
     Y, Cb, Cr = b.coefs(0, diffed=True)
     assert [sha(Y), sha(Cb), sha(Cr)] == ent["coef_sha256"]
     b.close()
+
+
+@pytest.mark.parametrize("q", [50, 100])
+def test_pack_staged_and_unstaged_groups_in_one_scan(q):
+    """k_pack_lb stages a pack group's tokens in LDS when they fit and packs
+    from HBM otherwise: noise rows (thousands of tokens per group at high Q)
+    next to natural rows and flat rows in one scan, so both kinds of groups
+    and the seams between them land in the same bitstream."""
+    rng = np.random.default_rng(q)
+    W, H = 1920, 96
+    nat = ppm.rgb_to_bgr(np.tile(recipes.sample("sample_640x640"), (1, 3, 1))[:32, :W])
+    img = np.concatenate([rng.integers(0, 256, (32, W, 3), dtype=np.uint8), nat,
+                          np.full((32, W, 3), 77, np.uint8)])
+    b = mijpeg.Batch(W, H, 2, q)
+    frames = np.stack([img, img[::-1].copy()])
+    b.upload(frames)
+    b.encode(2)
+    for i in range(2):
+        got, ref = b.output(i), O.cref_encode(frames[i], q)
+        assert got == ref, f"frame {i} q{q}: first diff {first_diff(got, ref)}"
+    b.close()
