@@ -137,6 +137,8 @@ static Geom make_geom(int w, int h) {
   g.raw_words[2] = g.raw_words[1];
   g.raw_fs = g.raw_words[0] + g.raw_words[1] + g.raw_words[2];
   g.out_cap = round_up((long long)g.nblk * 434 + 4096, 256);
+  div_magic((uint32_t)g.tiles_per_frame, g.tpf_m, g.tpf_s);
+  div_magic((uint32_t)g.tiles_x, g.tx_m, g.tx_s);
   return g;
 }
 

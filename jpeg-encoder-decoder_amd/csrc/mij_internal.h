@@ -6,6 +6,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "mij_divmagic.h"
+
 namespace mij {
 
 // ---- tiling of the fused colour+DCT kernel (K1) ---------------------------
@@ -60,7 +62,12 @@ struct Geom {
   long long raw_words[3];   // raw bit-buffer capacity per component (words)
   long long raw_fs;         // words per frame
   long long out_cap;        // output bytes per frame
+  // n / tiles_per_frame and n / tiles_x for 0 <= n < 2^31 as
+  // (umulhi(n, m) + n) >> s (K1's per-tile position on the scalar unit)
+  uint32_t tpf_m, tpf_s, tx_m, tx_s;
 };
+
+
 
 // The image of frame f of a batch.  Buffers are laid out for the batch
 // geometry G (the "canvas"); a region batch (mij_batch_set_frame_dims) holds

@@ -224,9 +224,9 @@ struct TilePos {
 
 __device__ __forceinline__ TilePos tile_pos(const Geom &G, int t) {
   TilePos p;
-  p.f = t / G.tiles_per_frame;
+  p.f = (int)div_by((uint32_t)t, G.tpf_m, G.tpf_s);
   const int rem = t - p.f * G.tiles_per_frame;
-  p.ty = rem / G.tiles_x;
+  p.ty = (int)div_by((uint32_t)rem, G.tx_m, G.tx_s);
   p.tx = rem - p.ty * G.tiles_x;
   p.valid_px = min(TILE_W, G.w - p.tx * TILE_W);
   return p;
@@ -249,17 +249,31 @@ constexpr int TILE_RAW = TILE_W * 3 * TILE_H;  // 6144 B of BGR888 per tile
 // Streams a tile's 16 rows x 384 B into LDS with global_load_lds_dwordx4 (no
 // VGPRs for the data): instruction k moves rows 2k and 2k+1 = LDS bytes
 // [768k, 768k + 768); lane i < 48 moves the 16 B at row 2k + i / 24, column
-// 16 * (i % 24).  The lane offset is the same for every k (the 2k rows go
-// into the SGPR base), so a full tile costs no VALU and one VGPR.
+// 16 * (i % 24).  The per-lane offsets of the eight instructions are fixed
+// for the kernel (DmaOff, eight VGPRs); per tile only the frame/tile base
+// (one SGPR pair) and the LDS base (m0 = base + 768k) change, so the issue
+// needs no VALU and three SGPRs.
 constexpr int DMA_K = TILE_H / 2;
-__device__ __forceinline__ uint32_t dma_offset(int pitch, int lane) {
+struct DmaOff {
+  uint32_t v[DMA_K];
+};
+__device__ __forceinline__ DmaOff dma_offsets(int pitch, int lane) {
   const int l = lane < 48 ? lane : 0;
-  return (uint32_t)((l / 24) * pitch + (l % 24) * 16);
+  const uint32_t o = (uint32_t)((l / 24) * pitch + (l % 24) * 16);
+  DmaOff d;
+#pragma unroll
+  for (int k = 0; k < DMA_K; k++) d.v[k] = o + (uint32_t)(2 * k * pitch);
+  return d;
 }
 __device__ __forceinline__ void issue_tile_dma(const K1Args &a, const TilePos &p, int lane, uint8_t *raw,
-                                               uint32_t off) {
-  const uint8_t *src = a.in + (long long)p.f * a.in_fs + (long long)(p.ty * TILE_H) * a.pitch +
-                       p.tx * TILE_W * 3;
+                                               const DmaOff &off) {
+  const uint64_t srcv = (uint64_t)(uintptr_t)(a.in + (long long)p.f * a.in_fs +
+                                              (long long)(p.ty * TILE_H) * a.pitch + p.tx * TILE_W * 3);
+  // (wave-uniform; readfirstlane keeps it in SGPRs for the "s" operand)
+  // (readfirstlane returns int: widen through uint32_t, never sign-extend)
+  const uint32_t src_hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(srcv >> 32));
+  const uint32_t src_lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)srcv);
+  const uint8_t *src = (const uint8_t *)(uintptr_t)(((uint64_t)src_hi << 32) | (uint64_t)src_lo);
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t *)raw);
   // right frame edge: only the valid columns
   const bool on = lane < 48 && (p.valid_px == TILE_W || (lane % 24) * 16 < p.valid_px * 3);
@@ -268,14 +282,22 @@ __device__ __forceinline__ void issue_tile_dma(const K1Args &a, const TilePos &p
   // stores; K1 waits for the DMA itself (dma_wait) before its first store,
   // when the DMA has long landed
   if (on) {
-#pragma unroll
-    for (int k = 0; k < DMA_K; k++)
-      asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1 nt"
-                   :
-                   : "v"(off), "s"(src + (long long)(2 * k) * a.pitch), "s"(lds0 + 768 * k)
-                   : "memory", "m0");
+    asm volatile(
+        "s_mov_b32 m0, %8\n\tglobal_load_lds_dwordx4 %0, %9 nt\n\t"
+        "s_add_u32 m0, %8, 768\n\tglobal_load_lds_dwordx4 %1, %9 nt\n\t"
+        "s_add_u32 m0, %8, 1536\n\tglobal_load_lds_dwordx4 %2, %9 nt\n\t"
+        "s_add_u32 m0, %8, 2304\n\tglobal_load_lds_dwordx4 %3, %9 nt\n\t"
+        "s_add_u32 m0, %8, 3072\n\tglobal_load_lds_dwordx4 %4, %9 nt\n\t"
+        "s_add_u32 m0, %8, 3840\n\tglobal_load_lds_dwordx4 %5, %9 nt\n\t"
+        "s_add_u32 m0, %8, 4608\n\tglobal_load_lds_dwordx4 %6, %9 nt\n\t"
+        "s_add_u32 m0, %8, 5376\n\tglobal_load_lds_dwordx4 %7, %9 nt"
+        :
+        : "v"(off.v[0]), "v"(off.v[1]), "v"(off.v[2]), "v"(off.v[3]), "v"(off.v[4]), "v"(off.v[5]),
+          "v"(off.v[6]), "v"(off.v[7]), "s"(lds0), "s"(src)
+        : "memory", "m0", "scc");  // s_add_u32 writes SCC
   }
 }
+static_assert(DMA_K == 8 && TILE_W * 3 * 2 == 768, "issue_tile_dma: 8 instructions of 2 rows x 384 B");
 
 // all of this wave's outstanding vector-memory operations (the tile DMA above
 // included) have completed; VMEM operations retire in issue order
@@ -693,7 +715,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   const int g = lane >> 4, bcol = lane & 15;
   const int c4 = lane & 31, pr = lane >> 5;
   const int q_dc[2] = {T->qint[0][0], T->qint[1][0]};
-  const Geom G = a.g;
+  const Geom &G = a.g;
   const int bw = G.w >> 3, mw = G.w >> 4;
   const int ntiles = a.nframes * G.tiles_per_frame;
   const int t0 = (int)blockIdx.x * a.per_wg;  // per_wg <= tiles_per_frame:
@@ -722,7 +744,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   if (t < tend) {
     uint8_t *raw = s_raw[PIX ? wave : 0];
     TilePos p = tpos(t);
-    const uint32_t doff = dma_offset(a.pitch, lane);
+    const DmaOff doff = dma_offsets(a.pitch, lane);
     if (PIX) issue_tile_dma(a, p, lane, raw, doff);
     // coefficient input: the three N-tiles' 32 B per lane of a tile
     auto load_coefs = [&](const TilePos &pp, u4v (&dst)[PIX ? 1 : 3][2]) {

@@ -7,7 +7,7 @@ cd "$(dirname "$0")/../jpeg-encoder-decoder_amd"
 make -s csrc/mij_api.o csrc/mij_stream.o csrc/mij_detect.o csrc/mij_decode.o
 mkdir -p ../ab
 H="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I../include -Icsrc -w"
-/opt/rocm/bin/hipcc $H $2 -c csrc/mij_kernels.hip -o ../ab/k_$1.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o ../ab/libmijpeg_$1.so ../ab/k_$1.o \
+/opt/rocm/bin/hipcc $H $2 -c csrc/mij_kernels.hip -o /tmp/ab_k_$1.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o ../ab/libmijpeg_$1.so /tmp/ab_k_$1.o \
     csrc/mij_api.o csrc/mij_stream.o csrc/mij_detect.o csrc/mij_decode.o
 echo "ab/libmijpeg_$1.so"

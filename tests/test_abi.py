@@ -113,3 +113,15 @@ def test_reference_main_loop_compiles_and_links(tmp_path):
     pkg = os.path.dirname(mijpeg.LIB_PATH)
     subprocess.check_call(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(REPO, "include"),
                            str(src), "-L", pkg, "-lmijpeg", "-o", str(tmp_path / "main_loop")])
+
+
+def test_division_magic(tmp_path):
+    """K1 computes (frame, tile row, tile column) of a tile index with a
+    multiply-high by a host-built magic number (mij_divmagic.h): checked
+    against integer division over every divisor < 4096 and 2000 random ones."""
+    exe = str(tmp_path / "div_check")
+    subprocess.check_call(["g++", "-O2", "-I" + os.path.join(REPO, "jpeg-encoder-decoder_amd", "csrc"),
+                           "-o", exe, os.path.join(REPO, "tests", "div_check.cpp")])
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert out.stdout.startswith("ok")
