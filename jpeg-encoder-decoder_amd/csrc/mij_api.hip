@@ -241,7 +241,7 @@ struct mij_batch {
   int pitch = 0;
   int16_t *d_coef = nullptr, *d_dc = nullptr;
   uint32_t *d_hist = nullptr, *d_ehuf = nullptr, *d_raw = nullptr;
-  uint32_t *d_tok = nullptr, *d_seg_ntok = nullptr, *d_seg_bits = nullptr;
+  uint32_t *d_tok = nullptr, *d_tok0 = nullptr, *d_seg_ntok = nullptr, *d_seg_bits = nullptr;
   uint64_t *d_seg_off = nullptr, *d_scan_bits = nullptr, *d_out_len = nullptr;
   HuffCode *d_hc = nullptr;
   uint8_t *d_out = nullptr;
@@ -292,7 +292,7 @@ static void batch_free(mij_batch *b) {
   hipSetDevice(b->dev);
   if (b->stream) hipStreamSynchronize(b->stream);
   void *ptrs[] = {b->d_tab, b->own_in ? b->d_in : nullptr, b->d_coef, b->d_dc, b->d_hist,
-                  b->d_ehuf, b->d_raw, b->d_tok, b->d_seg_ntok, b->d_seg_bits, b->d_seg_off,
+                  b->d_ehuf, b->d_raw, b->d_tok, b->d_tok0, b->d_seg_ntok, b->d_seg_bits, b->d_seg_off,
                   b->d_scan_bits, b->d_out_len, b->d_hc, b->d_out, b->d_err, b->d_replays,
                   b->d_dcpred, b->d_bitbase, b->d_stage, b->d_fix, b->d_fix_count, b->d_ffc, b->d_choff,
                   b->d_pack_state, b->d_pack_ticket, b->d_fdims, b->d_frame, b->d_regions};
@@ -343,6 +343,7 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
   HIP_TRY(dalloc(&b->d_hist, F * 4 * 257));
   HIP_TRY(dalloc(&b->d_ehuf, F * 4 * 256));
   HIP_TRY(dalloc(&b->d_tok, F * g.nseg * SEG_TOK));
+  HIP_TRY(dalloc(&b->d_tok0, F * g.nseg));
   HIP_TRY(dalloc(&b->d_seg_ntok, F * g.nseg));
   HIP_TRY(dalloc(&b->d_seg_bits, F * g.nseg));
   HIP_TRY(dalloc(&b->d_seg_off, F * g.nseg));
@@ -433,6 +434,7 @@ static EntArgs ent_args(mij_batch *b, int nframes) {
   a.hist = b->d_hist;
   a.ehuf = b->d_ehuf;
   a.tok = b->d_tok;
+  a.tok0 = b->d_tok0;
   a.seg_ntok = b->d_seg_ntok;
   a.seg_bits = b->d_seg_bits;
   a.seg_off = b->d_seg_off;
@@ -468,6 +470,7 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int se
   k.tab = b->d_tab;
   k.replays = b->d_replays;
   k.tok = b->d_tok;
+  k.tok0 = b->d_tok0;
   k.seg_ntok = b->d_seg_ntok;
   k.hist = b->d_hist;
   k.fix_list = b->d_fix;
@@ -532,7 +535,11 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int se
 static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given) {
   EntArgs a = ent_args(b, nframes);
   const bool t = b->timing;
-  if (dc_fix) HIP_TRY(launch_seg_dc(a, b->stream));
+  // segment-first DC tokens: inside k_tables (its DC-table waves), or on
+  // their own when the caller's tables are given
+  static const int segdc_dbg = getenv("MIJ_SEGDC_DBG") ? atoi(getenv("MIJ_SEGDC_DBG")) : 0;  // diag build
+  a.seg_dc = dc_fix && !tables_given ? 1 | segdc_dbg : 0;
+  if (dc_fix && tables_given) HIP_TRY(launch_seg_dc(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[4], b->stream));
   if (!tables_given) HIP_TRY(launch_tables(a, b->stream));
   if (t) HIP_TRY(hipEventRecord(b->ev[5], b->stream));

@@ -135,7 +135,8 @@ struct K1Args {
   int dc_diffed;            // coefficient input holds DC differences (drop-in)
   int seg_dc_inline;        // coefficient input: first DC of each segment from the raw DCs
   const int16_t *dc_pred;   // coefficient input, inline: DC predictor per frame [4] (null: 0)
-  uint32_t *tok;            // token mode: per segment SEG_TOK tokens
+  uint32_t *tok;            // token mode: per segment SEG_TOK tokens (token 0 in tok0)
+  uint32_t *tok0;           // token mode: per segment its first token (the first block's DC)
   uint32_t *seg_ntok;       // token mode: tokens per segment
   uint32_t *hist;           // token mode: per frame [4][257] histograms
   uint32_t *fix_list;       // coefficient mode: blocks (frame * nblk + blk) for k_fix_blocks
@@ -158,7 +159,8 @@ struct EntArgs {
   const int16_t *dc;        // raw DC per block (K1)
   uint32_t *hist;           // per frame [4][257]
   const uint32_t *ehuf;     // per frame [4][256] = len << 16 | code
-  uint32_t *tok;            // per segment SEG_TOK tokens
+  uint32_t *tok;            // per segment SEG_TOK tokens (token 0 in tok0)
+  uint32_t *tok0;           // per segment its first token
   const uint32_t *seg_ntok; // per segment token count
   uint32_t *seg_bits;       // per segment bits
   uint64_t *seg_off;        // per segment bit offset inside its scan
@@ -178,6 +180,7 @@ struct EntArgs {
   unsigned int *pack_ticket;       // k_pack_lb: next group to claim
   unsigned long long *dbg;         // diagnostics only (MIJ_PACK_TIME, diag build)
   const int2 *fdims;               // per-frame image size (region batches), null: the canvas
+  int seg_dc;                      // k_tables: compute the segment-first DC tokens first (k_seg_dc)
 };
 
 // EMIT_CH chunks of the largest scan buffer (the per-scan stride of EntArgs::ffc)

@@ -538,7 +538,7 @@ constexpr uint32_t TOK_AC = 1u << 10;
 __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g, int bcol,
                                             bool valid, bool chroma, bool dc_diffed,
                                             bool first_pred, int pred0,
-                                            uint32_t *segtok, uint32_t *segcnt, uint32_t *hDC,
+                                            uint32_t *segtok, uint32_t *tok0, uint32_t *segcnt, uint32_t *hDC,
                                             uint32_t *hAC, int16_t (*st)[16], int kflags = 0) {
   u4v c0, c1;
 #pragma unroll
@@ -588,7 +588,11 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
       if (dc_diffed || pos != 0 || first_pred) {
         const int diff = dc_diffed ? dc0 : dc0 - (pos != 0 ? prev : pred0);  // :168-177
         const int cls = mag_class(diff);
-        segtok[base] = (uint32_t)cls | (mag_bits(diff, cls) << 16);
+        // a segment's first token lives in the dense tok0 array (one word per
+        // segment: written there it is a whole-line store, not a lone word)
+        const uint32_t tk = (uint32_t)cls | (mag_bits(diff, cls) << 16);
+        if (pos == 0) *tok0 = tk;
+        else segtok[base] = tk;
         atomicAdd(&hDC[cls], 1u);
       }
       if (eob) segtok[base + n - 1] = TOK_AC;
@@ -927,7 +931,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
                                   : (int)a.dc[(long long)p.f * G.nblk + blk - 1];
           }
           emit_tokens(o, lane, g, bcol, valid, comp == 1, !PIX && a.dc_diffed, first_pred, pred0,
-                      a.tok + fs * SEG_TOK,
+                      a.tok + fs * SEG_TOK, a.tok0 + fs,
                       a.seg_ntok + fs, s_hdc[TOK ? slot : 0][comp][bcol & (HREP - 1)],
                       s_hac[TOK ? slot : 0][comp][bcol & (HREP - 1)],
                       s_st[TOK ? wave : 0], kflags);
@@ -1200,7 +1204,7 @@ __device__ __forceinline__ bool seg_info(const Geom &G, const FGeom &fg, int s, 
     comp = 0;
     local = s;
     cstart = 0;
-    const int r = s / G.tiles_x, tx = s % G.tiles_x;
+    const int r = (int)div_by((uint32_t)s, G.tx_m, G.tx_s), tx = s - r * G.tiles_x;
     first = r * fg.bw + tx * 16;
     return r < 2 * fg.rows && tx < fg.tiles_x;
   }
@@ -1208,7 +1212,7 @@ __device__ __forceinline__ bool seg_info(const Geom &G, const FGeom &fg, int s, 
   comp = 1 + (c >= G.nsc);
   local = comp == 1 ? c : c - G.nsc;
   cstart = comp == 1 ? fg.nY : fg.nY + fg.nC;
-  const int r = local / G.tiles_x, tx = local % G.tiles_x;
+  const int r = (int)div_by((uint32_t)local, G.tx_m, G.tx_s), tx = local - r * G.tiles_x;
   first = cstart + r * fg.mw + tx * 8;
   return r < fg.rows && tx < fg.tiles_x;
 }
@@ -1216,8 +1220,39 @@ __device__ __forceinline__ bool seg_info(const Geom &G, const FGeom &fg, int s, 
 // ===========================================================================
 // k_seg_dc: DC difference of every segment's first block (its predecessor
 // lies in another segment, encoder.c:168-177): token 0 of the segment and
-// the DC class histogram.  One thread per segment.
+// the DC class histogram h[luma, chroma][class] (LDS).  One thread per
+// segment; k_tables runs the same per-segment step in its DC-table waves.
 // ===========================================================================
+// (split in two so that callers can have several segments' loads in flight)
+struct SegDc {
+  int comp, dc, pred;
+  bool ok;
+};
+__device__ __forceinline__ SegDc seg_dc_load(const EntArgs &a, const FGeom &fg, int f, int s) {
+  SegDc r;
+  int first, cstart, local;
+  r.ok = seg_info(a.g, fg, s, r.comp, first, cstart, local);
+  r.dc = r.pred = 0;
+  if (r.ok) {
+    const long long fb = (long long)f * a.g.nblk;
+    // a component's first block is predicted from 0 (encoder.c:168-177), or
+    // from the previous band's last DC when the frame is split into bands
+    r.pred = first == cstart ? (a.dc_pred ? (int)a.dc_pred[f * 4 + r.comp] : 0) : (int)a.dc[fb + first - 1];
+    r.dc = (int)a.dc[fb + first];
+  }
+  return r;
+}
+__device__ __forceinline__ void seg_dc_store(const EntArgs &a, int f, int s, const SegDc &r, uint32_t (*h)[16]) {
+  if (!r.ok) return;
+  const int diff = r.dc - r.pred;
+  const int cls = mag_class(diff);
+#ifdef MIJ_K1_DIAG
+  if (!(a.seg_dc & 2))
+#endif
+  a.tok0[(long long)f * a.g.nseg + s] = (uint32_t)cls | (mag_bits(diff, cls) << 16);
+  atomicAdd(&h[r.comp ? 1 : 0][cls], 1u);
+}
+
 __global__ __launch_bounds__(256) void k_seg_dc(EntArgs a) {
   __shared__ uint32_t h[2][16];
   const int per = (a.g.nseg + 255) / 256;
@@ -1225,18 +1260,7 @@ __global__ __launch_bounds__(256) void k_seg_dc(EntArgs a) {
   const int s = (blockIdx.x - f * per) * 256 + threadIdx.x;
   if (threadIdx.x < 32) (&h[0][0])[threadIdx.x] = 0;
   __syncthreads();
-  int comp, first, cstart, local;
-  if (s < a.g.nseg && seg_info(a.g, frame_geom(a.g, a.fdims, f), s, comp, first, cstart, local)) {
-    const long long fb = (long long)f * a.g.nblk;
-    // a component's first block is predicted from 0 (encoder.c:168-177), or
-    // from the previous band's last DC when the frame is split into bands
-    const int pred = first == cstart ? (a.dc_pred ? (int)a.dc_pred[f * 4 + comp] : 0)
-                                     : (int)a.dc[fb + first - 1];
-    const int diff = (int)a.dc[fb + first] - pred;
-    const int cls = mag_class(diff);
-    a.tok[((long long)f * a.g.nseg + s) * SEG_TOK] = (uint32_t)cls | (mag_bits(diff, cls) << 16);
-    atomicAdd(&h[comp ? 1 : 0][cls], 1u);
-  }
+  if (s < a.g.nseg) seg_dc_store(a, f, s, seg_dc_load(a, frame_geom(a.g, a.fdims, f), f, s), h);
   __syncthreads();
   if (threadIdx.x < 32) {
     const uint32_t v = (&h[0][0])[threadIdx.x];
@@ -1279,7 +1303,8 @@ __device__ __forceinline__ void top2(unsigned long long &k1, unsigned long long 
   k2 = hi < m2 ? hi : m2;
 }
 
-__device__ void build_table_wave(const uint32_t *hist, HuffCode *hc, uint32_t *ehuf,
+// extra: DC class counts the caller adds to hist (the segment-first DCs), or null
+__device__ void build_table_wave(const uint32_t *hist, const uint32_t *extra, HuffCode *hc, uint32_t *ehuf,
                                  TabScratch *S, int lane, int *err) {
   uint32_t f[5];
   int cl[5], gr[5];
@@ -1287,6 +1312,7 @@ __device__ void build_table_wave(const uint32_t *hist, HuffCode *hc, uint32_t *e
   for (int i = 0; i < 5; i++) {
     const int s = lane + 64 * i;
     f[i] = s < 256 ? hist[s] : (s == 256 ? 1u : 0u);  // :364-367
+    if (extra && i == 0 && lane < 16) f[i] += extra[lane];
     cl[i] = 0;
     gr[i] = s;
     if (s < 257) {
@@ -1441,10 +1467,45 @@ __device__ void build_table_wave(const uint32_t *hist, HuffCode *hc, uint32_t *e
   }
 }
 
+// With a.seg_dc the DC-table waves (0, 2) first compute the segments' first
+// DC tokens and class counts (k_seg_dc's step; half of the frame's segments
+// each, 32 segments in flight per lane) while the AC-table waves, the long
+// pole (~160 symbols to merge against <= 12), already build theirs.
 __global__ __launch_bounds__(256) void k_tables(EntArgs a) {
   __shared__ TabScratch S[4];
+  __shared__ uint32_t h[2][16];
+  __shared__ int s_done;
   const int f = blockIdx.x, t = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  build_table_wave(a.hist + ((long long)f * 4 + t) * 257, (HuffCode *)a.hc + (long long)f * 4 + t,
+  const uint32_t *extra = nullptr;
+  if (a.seg_dc && t == 0) {
+    if (lane < 32) (&h[0][0])[lane] = 0;
+    if (lane == 0) s_done = 0;
+  }
+  __syncthreads();
+  if (a.seg_dc && !(t & 1)) {
+    uint32_t(*hh)[16] = h;
+    const FGeom fg = frame_geom(a.g, a.fdims, f);
+    const int half = (a.g.nseg + 1) / 2;
+    const int sb = t == 0 ? 0 : half, se = t == 0 ? half : a.g.nseg;
+    constexpr int U = 32;  // segments in flight per lane
+    for (int s0 = sb + lane; s0 < se; s0 += 64 * U) {
+      SegDc r[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int s = s0 + 64 * u;
+        r[u] = s < se ? seg_dc_load(a, fg, f, s) : SegDc{0, 0, 0, false};
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) seg_dc_store(a, f, s0 + 64 * u, r[u], hh);
+    }
+    // both DC waves' counts are in before either builds its table
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) atomicAdd(&s_done, 1);
+    while (__hip_atomic_load(&s_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 2)
+      __builtin_amdgcn_s_sleep(2);
+    extra = h[t >> 1];
+  }
+  build_table_wave(a.hist + ((long long)f * 4 + t) * 257, extra, (HuffCode *)a.hc + (long long)f * 4 + t,
                    (uint32_t *)a.ehuf + ((long long)f * 4 + t) * 256, &S[t], lane, a.err + f);
 }
 
@@ -1482,6 +1543,7 @@ __global__ __launch_bounds__(256) void k_seg_bits(EntArgs a) {
     const long long fs = (long long)f * a.g.nseg + s;
     const int n = min((int)a.seg_ntok[fs], SEG_TOK);
     const uint32_t *tk = a.tok + fs * SEG_TOK;
+    const uint32_t tz = a.tok0[fs];  // token 0
     const int chroma = s >= a.g.nsy;
     uint32_t b = 0;
     // four loads in flight per lane before any is used (latency-bound loop)
@@ -1490,7 +1552,7 @@ __global__ __launch_bounds__(256) void k_seg_bits(EntArgs a) {
 #pragma unroll
       for (int u = 0; u < 4; u++) {
         const int i = i0 + 16 * u + sub;
-        t[u] = i < n ? tk[i] : 0u;
+        t[u] = i < n ? (i ? tk[i] : tz) : 0u;
       }
 #pragma unroll
       for (int u = 0; u < 4; u++)
@@ -1622,6 +1684,7 @@ __global__ __launch_bounds__(256) void k_pack(EntArgs a) {
       uint32_t tq[4];  // tokens of the next 64, loaded ahead (latency-bound loop)
 #pragma unroll
       for (int u = 0; u < 4; u++) tq[u] = 16 * u + sub < n ? tk[16 * u + sub] : 0u;
+      if (sub == 0) tq[0] = a.tok0[fs];  // token 0
       for (int i0 = 0; i0 < n; i0 += 16) {
         const int i = i0 + sub;
         const uint32_t t = tq[0];
@@ -1727,13 +1790,14 @@ __global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
     const long long fs = fs0 + sl;
     const int n = min((int)a.seg_ntok[fs], SEG_TOK);
     const uint32_t *tk = a.tok + fs * SEG_TOK;
+    const uint32_t tz = a.tok0[fs];  // token 0
     uint32_t b = 0;
     for (int i0 = 0; i0 < n; i0 += 16 * LB_DEPTH) {
       uint32_t t[LB_DEPTH];
 #pragma unroll
       for (int u = 0; u < LB_DEPTH; u++) {
         const int i = i0 + 16 * u + sub;
-        t[u] = i < n ? tk[i] : 0u;
+        t[u] = i < n ? (i ? tk[i] : tz) : 0u;
       }
 #pragma unroll
       for (int u = 0; u < LB_DEPTH; u++) {  // encoder.c:434-460, ZRLs :490-494
@@ -1812,6 +1876,7 @@ __global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
       uint32_t tq[LB_DEPTH];  // tokens of the next 16 * LB_DEPTH, loaded ahead (latency-bound loop)
 #pragma unroll
       for (int u = 0; u < LB_DEPTH; u++) tq[u] = 16 * u + sub < n ? tk[16 * u + sub] : 0u;
+      if (sub == 0) tq[0] = a.tok0[fs];  // token 0
       for (int i0 = 0; i0 < n; i0 += 16) {
         const int i = i0 + sub;
         const uint32_t t = tq[0];
