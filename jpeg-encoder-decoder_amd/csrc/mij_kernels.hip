@@ -1740,7 +1740,7 @@ __global__ __launch_bounds__(256) void k_pack(EntArgs a) {
 // ===========================================================================
 constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1;
 #ifndef MIJ_LB_DEPTH
-#define MIJ_LB_DEPTH 12
+#define MIJ_LB_DEPTH 8
 #endif
 constexpr int LB_DEPTH = MIJ_LB_DEPTH;  // token loads in flight per lane
 
@@ -1784,8 +1784,13 @@ __global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
   __syncthreads();
   const uint32_t zac = tab[1][0xF0];
   const uint32_t Lz = zac >> 16;
-  // ---- 1. bits of each segment (16 lanes per segment) --------------------
   const int sub = tid & 15, row = tid >> 4;
+  // bits of a token (encoder.c:434-460, ZRLs :490-494)
+  auto tok_nb = [&](uint32_t t) -> uint32_t {
+    const uint32_t sym = t & 255u;
+    return (tab[(t & TOK_AC) ? 1 : 0][sym] >> 16) + (sym & 15u) + ((t >> 8) & 3u) * Lz;
+  };
+  // ---- 1. bits of each segment (16 lanes per segment) --------------------
   for (int sl = row; sl < nsg; sl += 16) {
     const long long fs = fs0 + sl;
     const int n = min((int)a.seg_ntok[fs], SEG_TOK);
@@ -1800,11 +1805,8 @@ __global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
         t[u] = i < n ? (i ? tk[i] : tz) : 0u;
       }
 #pragma unroll
-      for (int u = 0; u < LB_DEPTH; u++) {  // encoder.c:434-460, ZRLs :490-494
-        const uint32_t tk4 = t[u], sym = tk4 & 255u;
-        if (i0 + 16 * u + sub < n)
-          b += (tab[(tk4 & TOK_AC) ? 1 : 0][sym] >> 16) + (sym & 15u) + ((tk4 >> 8) & 3u) * Lz;
-      }
+      for (int u = 0; u < LB_DEPTH; u++)
+        if (i0 + 16 * u + sub < n) b += tok_nb(t[u]);
     }
     b = row_scan16(b);
     if (sub == 15) s_bits[sl] = b;
@@ -1866,6 +1868,9 @@ __global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
     const uint32_t lo_bit = w0 * 32, hi_bit = (w0 + wn) * 32;
     for (uint32_t i = tid; i < wn; i += 256) buf[i] = 0;
     __syncthreads();
+    // one window covers the group (all but near worst-case entropy): no
+    // per-piece window test
+    const bool whole = w0 == 0 && wn == nw;
     for (int sl = row; sl < nsg; sl += 16) {
       const long long fs = fs0 + sl;
       const uint32_t sb = bit0 + s_off[sl];
@@ -1873,31 +1878,48 @@ __global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
       const int n = min((int)a.seg_ntok[fs], SEG_TOK);
       const uint32_t *tk = a.tok + fs * SEG_TOK;
       uint32_t pos0 = sb;
-      uint32_t tq[LB_DEPTH];  // tokens of the next 16 * LB_DEPTH, loaded ahead (latency-bound loop)
+      // LB_DEPTH tokens per lane loaded one batch ahead (latency-bound loop)
+      uint32_t cur[LB_DEPTH], nxt[LB_DEPTH];
 #pragma unroll
-      for (int u = 0; u < LB_DEPTH; u++) tq[u] = 16 * u + sub < n ? tk[16 * u + sub] : 0u;
-      if (sub == 0) tq[0] = a.tok0[fs];  // token 0
-      for (int i0 = 0; i0 < n; i0 += 16) {
-        const int i = i0 + sub;
-        const uint32_t t = tq[0];
+      for (int u = 0; u < LB_DEPTH; u++) cur[u] = 16 * u + sub < n ? tk[16 * u + sub] : 0u;
+      if (sub == 0) cur[0] = a.tok0[fs];  // token 0
+      for (int i0 = 0; i0 < n; i0 += 16 * LB_DEPTH) {
 #pragma unroll
-        for (int u = 0; u + 1 < LB_DEPTH; u++) tq[u] = tq[u + 1];
-        tq[LB_DEPTH - 1] = i + 16 * LB_DEPTH < n ? tk[i + 16 * LB_DEPTH] : 0u;
-        const uint32_t sym = t & 255u, cls = sym & 15u;
-        const uint32_t e = i < n ? tab[(t & TOK_AC) ? 1 : 0][sym] : 0u;
-        const uint32_t nz = (t >> 8) & 3u;
-        const uint32_t L = (e >> 16) + cls;
-        const uint32_t nb = i < n ? L + nz * Lz : 0u;
-        const uint32_t x = row_scan16(nb);
-        uint32_t pos = pos0 + x - nb;
-        if (nb && pos < hi_bit && pos + nb > lo_bit) {
-          for (uint32_t k = nz; k; k--) {  // encoder.c:490-494 ZRL
-            put_bits_window(buf, pos, lo_bit, hi_bit, zac & 0xFFFFu, (int)Lz);
-            pos += Lz;
-          }
-          if (L) put_bits_window(buf, pos, lo_bit, hi_bit, ((e & 0xFFFFu) << cls) | (t >> 16), (int)L);
+        for (int u = 0; u < LB_DEPTH; u++) {
+          const int i = i0 + 16 * (LB_DEPTH + u) + sub;
+          nxt[u] = i < n ? tk[i] : 0u;
         }
-        pos0 += row_last(x);
+#pragma unroll
+        for (int u = 0; u < LB_DEPTH; u++) {
+          if (i0 + 16 * u >= n) break;  // row-uniform
+          const int i = i0 + 16 * u + sub;
+          const uint32_t t = cur[u];
+          const uint32_t sym = t & 255u, cls = sym & 15u;
+          const uint32_t e = i < n ? tab[(t & TOK_AC) ? 1 : 0][sym] : 0u;
+          const uint32_t nz = (t >> 8) & 3u;
+          const uint32_t L = (e >> 16) + cls;
+          const uint32_t nb = i < n ? L + nz * Lz : 0u;
+          const uint32_t x = row_scan16(nb);
+          uint32_t pos = pos0 + x - nb;
+          if (whole) {
+            if (nb) {
+              for (uint32_t k = nz; k; k--) {  // encoder.c:490-494 ZRL
+                put_bits(buf, pos - lo_bit, zac & 0xFFFFu, (int)Lz);
+                pos += Lz;
+              }
+              if (L) put_bits(buf, pos - lo_bit, ((e & 0xFFFFu) << cls) | (t >> 16), (int)L);
+            }
+          } else if (nb && pos < hi_bit && pos + nb > lo_bit) {
+            for (uint32_t k = nz; k; k--) {  // encoder.c:490-494 ZRL
+              put_bits_window(buf, pos, lo_bit, hi_bit, zac & 0xFFFFu, (int)Lz);
+              pos += Lz;
+            }
+            if (L) put_bits_window(buf, pos, lo_bit, hi_bit, ((e & 0xFFFFu) << cls) | (t >> 16), (int)L);
+          }
+          pos0 += row_last(x);
+        }
+#pragma unroll
+        for (int u = 0; u < LB_DEPTH; u++) cur[u] = nxt[u];
       }
     }
     __syncthreads();
