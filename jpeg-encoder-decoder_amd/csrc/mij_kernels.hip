@@ -602,7 +602,7 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
     const unsigned long long eobs = __ballot(g == 0 && valid && eob);
     if (lane == 0 && eobs) atomicAdd(&hAC[0x00], (unsigned)__popcll(eobs));
   }
-  if (valid) {  // lane (g, b) takes the zigzag positions z == g (mod 4)
+  if (valid && !(kflags & K1F_NO_ACLOOP)) {  // lane (g, b) takes the zigzag positions z == g (mod 4)
     unsigned long long mm = M & (0x1111111111111111ull << g);
     while (mm) {
       const int z = __ffsll((long long)mm) - 1;
@@ -915,7 +915,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
           }
         }
         if (PIX && valid && g == 0) a.dc[(long long)p.f * G.nblk + blk] = (int16_t)o[0];
-        if (TOK) {
+        if (TOK && !(kflags & K1F_NO_EMIT)) {
           const long long fs = (long long)p.f * G.nseg + seg;
           const int slot = p.f - f0;
           // the coefficient-input variant predicts a segment's first DC from the
@@ -1739,14 +1739,43 @@ __global__ __launch_bounds__(256) void k_pack(EntArgs a) {
 // and the kernel is latency-bound.)
 // ===========================================================================
 constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1;
-#ifndef MIJ_LB_DEPTH
-#define MIJ_LB_DEPTH 8
+// k_pack_lb: a lane takes 4 consecutive tokens of a segment (one 16-byte
+// load), 16 lanes a segment, 64 tokens per row step; the first LB_STEPS steps
+// of each of a row's PACK_SEGS / 16 segments stay in registers from phase 1 to
+// phase 3 (tokens are read once unless a segment holds more than
+// 64 * LB_STEPS tokens)
+constexpr int LB_SEGS_PER_ROW = PACK_SEGS / 16;
+#ifndef MIJ_LB_STEPS
+#define MIJ_LB_STEPS 1
 #endif
-constexpr int LB_DEPTH = MIJ_LB_DEPTH;  // token loads in flight per lane
+#ifndef MIJ_LB_OCC
+#define MIJ_LB_OCC 7
+#endif
+constexpr int LB_STEPS = MIJ_LB_STEPS;
+static_assert(PACK_SEGS % 16 == 0, "k_pack_lb: 16 lanes per segment");
 
-__global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
+// bits of a token (encoder.c:434-460, ZRLs :490-494); tab = [DC | AC][256]
+// len << 16 | code of this scan's tables
+__device__ __forceinline__ uint32_t lb_tok_code(const uint32_t *tab, uint32_t t, uint32_t &code) {
+  const uint32_t sym = t & 255u, cls = sym & 15u;
+  const uint32_t e = tab[((t >> 2) & 256u) | sym];  // TOK_AC (bit 10) selects the AC table
+  code = ((e & 0xFFFFu) << cls) | (t >> 16);
+  return (e >> 16) + cls;
+}
+
+// OR `len` (1..64) bits, left-aligned in v, into the big-endian word buffer at
+// bit pos (pos + len within the buffer)
+__device__ __forceinline__ void put_bits64(uint32_t *buf, uint32_t pos, unsigned long long v, uint32_t len) {
+  const uint32_t w = pos >> 5, off = pos & 31u;
+  const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+  atomicOr(&buf[w], hi >> off);
+  if (off + len > 32) atomicOr(&buf[w + 1], __builtin_amdgcn_alignbit(hi, lo, off));
+  if (off + len > 64) atomicOr(&buf[w + 2], __builtin_amdgcn_alignbit(lo, 0u, off));
+}
+
+__global__ __launch_bounds__(256, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
   __shared__ uint32_t buf[PACK_WORDS];
-  __shared__ uint32_t tab[2][256];
+  __shared__ uint32_t tab[2 * 256];
   __shared__ uint32_t s_bits[PACK_SEGS], s_off[PACK_SEGS];
   __shared__ unsigned long long s_prefix;
   __shared__ int s_ticket;
@@ -1780,34 +1809,56 @@ __global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
   const int chroma = comp != 0;
   const int s0 = q * PACK_SEGS, s1 = min(ns, s0 + PACK_SEGS), nsg = s1 - s0;
   const long long fs0 = (long long)f * G.nseg + sbase + s0;  // the group's first segment
-  for (int i = tid; i < 512; i += 256) tab[i >> 8][i & 255] = a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + i];
-  __syncthreads();
-  const uint32_t zac = tab[1][0xF0];
-  const uint32_t Lz = zac >> 16;
   const int sub = tid & 15, row = tid >> 4;
-  // bits of a token (encoder.c:434-460, ZRLs :490-494)
-  auto tok_nb = [&](uint32_t t) -> uint32_t {
-    const uint32_t sym = t & 255u;
-    return (tab[(t & TOK_AC) ? 1 : 0][sym] >> 16) + (sym & 15u) + ((t >> 8) & 3u) * Lz;
-  };
-  // ---- 1. bits of each segment (16 lanes per segment) --------------------
-  for (int sl = row; sl < nsg; sl += 16) {
-    const long long fs = fs0 + sl;
-    const int n = min((int)a.seg_ntok[fs], SEG_TOK);
-    const uint32_t *tk = a.tok + fs * SEG_TOK;
-    const uint32_t tz = a.tok0[fs];  // token 0
-    uint32_t b = 0;
-    for (int i0 = 0; i0 < n; i0 += 16 * LB_DEPTH) {
-      uint32_t t[LB_DEPTH];
+  // ---- 0. this row's segments: token counts, then their first LB_STEPS
+  // 64-token steps into registers (the loads overlap the table fill) --------
+  int nt[LB_SEGS_PER_ROW];
 #pragma unroll
-      for (int u = 0; u < LB_DEPTH; u++) {
-        const int i = i0 + 16 * u + sub;
-        t[u] = i < n ? (i ? tk[i] : tz) : 0u;
-      }
+  for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
+    const int sl = row + 16 * k;
+    nt[k] = sl < nsg ? min((int)a.seg_ntok[fs0 + sl], SEG_TOK) : 0;
+  }
+  u4v tq[LB_SEGS_PER_ROW][LB_STEPS];
 #pragma unroll
-      for (int u = 0; u < LB_DEPTH; u++)
-        if (i0 + 16 * u + sub < n) b += tok_nb(t[u]);
+  for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
+    const uint32_t *tk = a.tok + (fs0 + row + 16 * k) * SEG_TOK;
+#pragma unroll
+    for (int st = 0; st < LB_STEPS; st++) {
+      const int j = 64 * st + 4 * sub;
+      tq[k][st] = j < nt[k] ? *(const u4v *)(tk + j) : u4v{0u, 0u, 0u, 0u};
     }
+    if (sub == 0 && nt[k] > 0) tq[k][0][0] = a.tok0[fs0 + row + 16 * k];  // token 0
+  }
+  for (int i = tid; i < 512; i += 256) tab[i] = a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + i];
+  __syncthreads();
+  const uint32_t zac = tab[256 + 0xF0];
+  const uint32_t Lz = zac >> 16, zcode = zac & 0xFFFFu;
+  // a step's 4 tokens (those below lim = tokens left - 4 * sub): bits, ZRLs included
+  auto step_bits = [&](const u4v &t, int lim) -> uint32_t {
+    uint32_t b = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      uint32_t code;
+      const uint32_t L = lb_tok_code(tab, t[e], code);
+      b += e < lim ? L + ((t[e] >> 8) & 3u) * Lz : 0u;
+    }
+    return b;
+  };
+  // steps past the registers (segments of more than 64 * LB_STEPS tokens)
+  auto load_step = [&](int k, int i0) -> u4v {
+    const uint32_t *tk = a.tok + (fs0 + row + 16 * k) * SEG_TOK;
+    const int j = i0 + 4 * sub;
+    return j < nt[k] ? *(const u4v *)(tk + j) : u4v{0u, 0u, 0u, 0u};
+  };
+  // ---- 1. bits of each segment ---------------------------------------------
+#pragma unroll
+  for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
+    const int sl = row + 16 * k;
+    if (sl >= nsg) break;  // row-uniform
+    uint32_t b = 0;
+#pragma unroll
+    for (int st = 0; st < LB_STEPS; st++) b += step_bits(tq[k][st], nt[k] - 64 * st - 4 * sub);
+    for (int i0 = 64 * LB_STEPS; i0 < nt[k]; i0 += 64) b += step_bits(load_step(k, i0), nt[k] - i0 - 4 * sub);
     b = row_scan16(b);
     if (sub == 15) s_bits[sl] = b;
   }
@@ -1820,15 +1871,15 @@ __global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
     if (lane < nsg) s_off[lane] = incl - v;
     const unsigned long long T = __shfl(incl, 63);
     const unsigned long long base = a.bit_base ? a.bit_base[f * 4 + comp] : 0u;
-    unsigned long long *st = a.pack_state;
+    unsigned long long *stt = a.pack_state;
     unsigned long long prefix = base;
     if (q > 0) {
-      if (lane == 0) __hip_atomic_store(&st[gid], LB_AGG | T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) __hip_atomic_store(&stt[gid], LB_AGG | T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       prefix = 0;
       long long j = gid - 1;
       while (true) {
         const long long jj = j - lane;
-        unsigned long long sv = jj >= gscan0 ? __hip_atomic_load(&st[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+        unsigned long long sv = jj >= gscan0 ? __hip_atomic_load(&stt[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                              : (LB_INC | base);
         const unsigned long long m2 = __ballot((sv >> 62) == 2), m0 = __ballot((sv >> 62) == 0);
         const unsigned long long upto = m2 ? (m2 & (~m2 + 1)) : 0ull;  // lowest inclusive lane
@@ -1836,8 +1887,8 @@ __global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
           __builtin_amdgcn_s_sleep(1);
           continue;
         }
-        const int k = upto ? __ffsll((long long)m2) - 1 : 63;
-        unsigned long long add = lane <= k ? (sv & LB_VAL) : 0ull;
+        const int kk = upto ? __ffsll((long long)m2) - 1 : 63;
+        unsigned long long add = lane <= kk ? (sv & LB_VAL) : 0ull;
         for (int off = 32; off; off >>= 1) add += __shfl_xor(add, off);
         prefix += add;
         if (upto) break;
@@ -1845,14 +1896,14 @@ __global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
       }
     }
     if (lane == 0) {
-      __hip_atomic_store(&st[gid], LB_INC | (prefix + T), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&stt[gid], LB_INC | (prefix + T), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (q == nq - 1) a.scan_bits[f * 3 + comp] = prefix + T;
       s_prefix = prefix;
     }
   }
   __syncthreads();
   LB_STAMP(2);
-  // ---- 3. pack the group's tokens (as k_pack) -------------------------------
+  // ---- 3. pack the group's tokens ------------------------------------------
   const unsigned long long gbase = s_prefix;
   const uint32_t bit0 = (uint32_t)(gbase & 31);
   const unsigned long long gbits = (unsigned long long)(nsg ? s_off[nsg - 1] + s_bits[nsg - 1] : 0u);
@@ -1868,58 +1919,89 @@ __global__ __launch_bounds__(256) void k_pack_lb(EntArgs a) {
     const uint32_t lo_bit = w0 * 32, hi_bit = (w0 + wn) * 32;
     for (uint32_t i = tid; i < wn; i += 256) buf[i] = 0;
     __syncthreads();
-    // one window covers the group (all but near worst-case entropy): no
-    // per-piece window test
+    // one window covers the group (all but near worst-case entropy): lanes
+    // merge their 4 tokens in a 64-bit register and OR it in with <= 3 LDS
+    // atomics.  A smaller window, or a lane whose 4 tokens exceed 64 bits,
+    // goes token by token in a second pass that reloads the tokens.
     const bool whole = w0 == 0 && wn == nw;
-    for (int sl = row; sl < nsg; sl += 16) {
-      const long long fs = fs0 + sl;
-      const uint32_t sb = bit0 + s_off[sl];
-      if (sb >= hi_bit || sb + s_bits[sl] <= lo_bit) continue;  // row-uniform
-      const int n = min((int)a.seg_ntok[fs], SEG_TOK);
-      const uint32_t *tk = a.tok + fs * SEG_TOK;
-      uint32_t pos0 = sb;
-      // LB_DEPTH tokens per lane loaded one batch ahead (latency-bound loop)
-      uint32_t cur[LB_DEPTH], nxt[LB_DEPTH];
+    // (tokens opaque here: otherwise the compiler hoists their per-token table
+    // addresses and masks out of the window loop and keeps them all live)
 #pragma unroll
-      for (int u = 0; u < LB_DEPTH; u++) cur[u] = 16 * u + sub < n ? tk[16 * u + sub] : 0u;
-      if (sub == 0) cur[0] = a.tok0[fs];  // token 0
-      for (int i0 = 0; i0 < n; i0 += 16 * LB_DEPTH) {
+    for (int k = 0; k < LB_SEGS_PER_ROW; k++)
 #pragma unroll
-        for (int u = 0; u < LB_DEPTH; u++) {
-          const int i = i0 + 16 * (LB_DEPTH + u) + sub;
-          nxt[u] = i < n ? tk[i] : 0u;
+      for (int st = 0; st < LB_STEPS; st++) asm volatile("" : "+v"(tq[k][st]));
+    auto decode = [&](const u4v &t, int lim, uint32_t (&L)[4], uint32_t (&code)[4], uint32_t (&nzr)[4]) {
+      uint32_t nb = 0;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        L[e] = lb_tok_code(tab, t[e], code[e]);
+        nzr[e] = (t[e] >> 8) & 3u;
+        if (e >= lim) L[e] = nzr[e] = code[e] = 0u;
+        nb += L[e] + nzr[e] * Lz;
+      }
+      return nb;
+    };
+    bool slow = !whole;
+    // one 64-token step of a row: positions, then the lane's merged bits
+    auto fast_step = [&](const u4v &t, int lim, uint32_t &pos0) {
+      uint32_t L[4], code[4], nzr[4];
+      const uint32_t nb = decode(t, lim, L, code, nzr);
+      const uint32_t x = row_scan16(nb);
+      const uint32_t pos = pos0 + x - nb;
+      pos0 += row_last(x);
+      if (nb > 64) {
+        slow = true;
+      } else if (nb) {
+        unsigned long long acc = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          for (uint32_t z = nzr[e]; z; z--) acc = (acc << Lz) | zcode;  // encoder.c:490-494 ZRL
+          acc = (acc << L[e]) | code[e];
         }
+        put_bits64(buf, pos, acc << (64 - nb), nb);
+      }
+    };
+    if (whole) {
 #pragma unroll
-        for (int u = 0; u < LB_DEPTH; u++) {
-          if (i0 + 16 * u >= n) break;  // row-uniform
-          const int i = i0 + 16 * u + sub;
-          const uint32_t t = cur[u];
-          const uint32_t sym = t & 255u, cls = sym & 15u;
-          const uint32_t e = i < n ? tab[(t & TOK_AC) ? 1 : 0][sym] : 0u;
-          const uint32_t nz = (t >> 8) & 3u;
-          const uint32_t L = (e >> 16) + cls;
-          const uint32_t nb = i < n ? L + nz * Lz : 0u;
+      for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
+        const int sl = row + 16 * k;
+        if (sl >= nsg) break;  // row-uniform
+        uint32_t pos0 = bit0 + s_off[sl];
+#pragma unroll
+        for (int st = 0; st < LB_STEPS; st++) {
+          if (64 * st >= nt[k]) break;  // row-uniform
+          fast_step(tq[k][st], nt[k] - 64 * st - 4 * sub, pos0);
+        }
+        for (int i0 = 64 * LB_STEPS; i0 < nt[k]; i0 += 64) fast_step(load_step(k, i0), nt[k] - i0 - 4 * sub, pos0);
+      }
+    }
+    if (__ballot(slow)) {  // second pass over this wave's rows, tokens reloaded
+      for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
+        const int sl = row + 16 * k;
+        if (sl >= nsg) break;  // row-uniform
+        uint32_t pos0 = bit0 + s_off[sl];
+        if (pos0 >= hi_bit || pos0 + s_bits[sl] <= lo_bit) continue;  // row-uniform
+        const uint32_t *tk = a.tok + (fs0 + sl) * SEG_TOK;
+        for (int i0 = 0; i0 < nt[k]; i0 += 64) {
+          const int j = i0 + 4 * sub;
+          u4v t = j < nt[k] ? *(const u4v *)(tk + j) : u4v{0u, 0u, 0u, 0u};
+          if (j == 0 && nt[k] > 0) t[0] = a.tok0[fs0 + sl];
+          uint32_t L[4], code[4], nzr[4];
+          const uint32_t nb = decode(t, nt[k] - j, L, code, nzr);
           const uint32_t x = row_scan16(nb);
           uint32_t pos = pos0 + x - nb;
-          if (whole) {
-            if (nb) {
-              for (uint32_t k = nz; k; k--) {  // encoder.c:490-494 ZRL
-                put_bits(buf, pos - lo_bit, zac & 0xFFFFu, (int)Lz);
-                pos += Lz;
-              }
-              if (L) put_bits(buf, pos - lo_bit, ((e & 0xFFFFu) << cls) | (t >> 16), (int)L);
-            }
-          } else if (nb && pos < hi_bit && pos + nb > lo_bit) {
-            for (uint32_t k = nz; k; k--) {  // encoder.c:490-494 ZRL
-              put_bits_window(buf, pos, lo_bit, hi_bit, zac & 0xFFFFu, (int)Lz);
+          pos0 += row_last(x);
+          // the first pass placed the steps of lanes within 64 bits
+          if (whole && nb <= 64) continue;
+          for (int e = 0; e < 4; e++) {
+            for (uint32_t z = nzr[e]; z; z--) {  // encoder.c:490-494 ZRL
+              if (pos < hi_bit && pos + Lz > lo_bit) put_bits_window(buf, pos, lo_bit, hi_bit, zcode, (int)Lz);
               pos += Lz;
             }
-            if (L) put_bits_window(buf, pos, lo_bit, hi_bit, ((e & 0xFFFFu) << cls) | (t >> 16), (int)L);
+            if (L[e] && pos < hi_bit && pos + L[e] > lo_bit) put_bits_window(buf, pos, lo_bit, hi_bit, code[e], (int)L[e]);
+            pos += L[e];
           }
-          pos0 += row_last(x);
         }
-#pragma unroll
-        for (int u = 0; u < LB_DEPTH; u++) cur[u] = nxt[u];
       }
     }
     __syncthreads();
