@@ -80,7 +80,9 @@ def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # MIJ_DIST_FORCE=1: a process group even for one rank (runs the device
+    # branch of the nccl exchanges on a single GPU)
+    if world > 1 or os.environ.get("MIJ_DIST_FORCE"):
         import torch
         import torch.distributed as dist
         # nccl (= RCCL) between GPUs; MIJ_DIST_BACKEND=gloo rehearses several
@@ -104,15 +106,20 @@ def run_config4(args, world, rank, local, dist):
     packed words to rank 0 -- RCCL when the backend is nccl)."""
     W, H, n = 7680, 4320, args.frames4
     gpu = 0 if dist is not None and dist.get_backend() != "nccl" else local
+    if dist is None:  # one rank: the word buffer stays in HBM (torch's runtime first)
+        import torch
+        torch.cuda.set_device(gpu)
     r0, rows = sharding.band_rows(H, world, rank)
     band = mijpeg.Batch(W, rows, n, args.quality, device=gpu)
     distinct = min(n, args.distinct)
     frames = [recipes.config4_frame(f) for f in range(distinct)]
     for f in range(n):
         band.upload(np.ascontiguousarray(frames[f % distinct][r0:r0 + rows]), first=f)
-    full = mijpeg.Batch(W, H, n, args.quality, device=gpu) if rank == 0 else None
+    # the root assembles on an assembler batch: tables, scan buffers and
+    # outputs only (no whole-frame input, coefficient or token buffers)
+    full = mijpeg.Batch(W, H, n, args.quality, device=gpu, assembler=True) if rank == 0 else None
     xch = sharding.TorchExchange(dist, dist_device(dist, local)) if dist is not None \
-        else sharding.LocalExchange()
+        else sharding.LocalExchange(f"cuda:{gpu}")
 
     def barrier():
         if dist is not None:

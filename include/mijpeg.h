@@ -257,6 +257,20 @@ int mij_assemble_begin(mij_batch *b, int n, const uint32_t *hist);
 int mij_assemble_words(mij_batch *b, int frame, int comp, unsigned long long first_word,
                        const void *src, size_t nwords, int src_on_device);
 int mij_assemble_end(mij_batch *b, int n, const unsigned long long *total_bits);
+/* The same exchange in one call per side (what sharding.encode_banded uses):
+ * mij_band_words_all copies every scan's band words of frames 0..n-1, in
+ * (frame, comp) order, into one buffer (word counts from mij_band_pack);
+ * mij_assemble_pieces ORs pieces of one buffer (the gathered band words of
+ * all ranks) into the scans in one launch: piece i = pieces[4i..4i+3] =
+ * {frame * 3 + comp, first word in the scan, first word in src, words}.  Both
+ * return once the copy is done (src / dst may be reused).
+ * mij_assembler_create makes a batch that only assembles (tables, scan
+ * buffers, outputs: no input, coefficient or token buffers); use it with
+ * mij_assemble_begin / _pieces / _words / _end and the output calls. */
+int mij_band_words_all(mij_batch *b, int n, void *dst, size_t cap_words, int dst_on_device);
+int mij_assemble_pieces(mij_batch *b, const void *src, size_t src_words, int src_on_device,
+                        const unsigned long long *pieces, int npieces);
+mij_batch *mij_assembler_create(int device, int width, int height, int max_frames, int quality);
 
 /* ---- diagnostics used by the test-suite -----------------------------------*/
 /* 16x16x64 i8 MFMA layout probe: A, B are 64 lanes x 16 int8, D 64 x 4 int32 */

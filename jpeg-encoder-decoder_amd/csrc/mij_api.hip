@@ -32,6 +32,8 @@ hipError_t launch_pack(const EntArgs &a, hipStream_t s);
 hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s);
 hipError_t launch_emit(const EntArgs &a, hipStream_t s);
 hipError_t launch_or_words(uint32_t *dst, const uint32_t *src, long long n, hipStream_t s);
+hipError_t launch_or_pieces(uint32_t *raw, const Geom &g, const uint32_t *src,
+                            const unsigned long long *d_pieces, int npieces, long long max_words, hipStream_t s);
 hipError_t launch_gather_regions(uint8_t *dst, long long slot_bytes, int pitch, const uint8_t *src,
                                  long long src_pitch, const int4 *regions, int n, int max_h,
                                  hipStream_t s);
@@ -256,8 +258,13 @@ struct mij_batch {
   // bands of one large frame (mij_band_*, mij_assemble_*): per frame [4]
   int16_t *d_dcpred = nullptr;
   uint32_t *d_bitbase = nullptr;
-  uint32_t *d_stage = nullptr;      // H2D staging for mij_assemble_words
+  uint32_t *d_stage = nullptr;      // H2D staging for mij_assemble_words / _pieces
   size_t stage_words = 0;
+  unsigned long long *d_pieces = nullptr;  // mij_assemble_pieces: piece table
+  size_t pieces_cap = 0;
+  // an assembler (mij_assembler_create): only what the JFIF assembly of
+  // whole frames from band words needs -- tables, scan buffers, outputs
+  bool assembler = false;
   std::vector<unsigned long long> band_words;  // per frame x 3: packed words after mij_band_pack
   // region batches (mij_batch_set_frame_dims / _gather_regions): per-frame
   // image size inside the canvas slots; d_frame stages a host frame
@@ -295,7 +302,7 @@ static void batch_free(mij_batch *b) {
                   b->d_ehuf, b->d_raw, b->d_tok, b->d_tok0, b->d_seg_ntok, b->d_seg_bits, b->d_seg_off,
                   b->d_scan_bits, b->d_out_len, b->d_hc, b->d_out, b->d_err, b->d_replays,
                   b->d_dcpred, b->d_bitbase, b->d_stage, b->d_fix, b->d_fix_count, b->d_ffc, b->d_choff,
-                  b->d_pack_state, b->d_pack_ticket, b->d_fdims, b->d_frame, b->d_regions};
+                  b->d_pack_state, b->d_pack_ticket, b->d_fdims, b->d_frame, b->d_regions, b->d_pieces};
   for (void *p : ptrs)
     if (p) hipFree(p);
   for (auto &row : b->evh)
@@ -313,9 +320,10 @@ static int check_device(int device) {
   return MIJ_OK;
 }
 
-static int batch_init(mij_batch *b, int device, int w, int h, int frames, int quality) {
+static int batch_init(mij_batch *b, int device, int w, int h, int frames, int quality, bool assembler = false) {
   if (check_device(device)) return g_err;
   b->dev = device;
+  b->assembler = assembler;
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
   b->g = make_geom(w, h);
@@ -336,17 +344,24 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
   }
   b->pitch = w * 3;
   b->in_fs = (long long)w * h * 3;
-  HIP_TRY(dalloc(&b->d_in, F * b->in_fs));
-  b->own_in = true;
-  HIP_TRY(dalloc(&b->d_coef, F * g.coef_fs));
-  HIP_TRY(dalloc(&b->d_dc, F * g.nblk));
+  if (!assembler) {
+    HIP_TRY(dalloc(&b->d_in, F * b->in_fs));
+    b->own_in = true;
+    HIP_TRY(dalloc(&b->d_coef, F * g.coef_fs));
+    HIP_TRY(dalloc(&b->d_dc, F * g.nblk));
+    HIP_TRY(dalloc(&b->d_tok, F * g.nseg * SEG_TOK));
+    HIP_TRY(dalloc(&b->d_tok0, F * g.nseg));
+    HIP_TRY(dalloc(&b->d_seg_ntok, F * g.nseg));
+    HIP_TRY(dalloc(&b->d_seg_bits, F * g.nseg));
+    HIP_TRY(dalloc(&b->d_seg_off, F * g.nseg));
+    HIP_TRY(dalloc(&b->d_fix, F * g.nblk));
+    HIP_TRY(dalloc(&b->d_pack_state, F * ((g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((g.nsc + PACK_SEGS - 1) / PACK_SEGS))));
+    HIP_TRY(dalloc(&b->d_pack_ticket, 1));
+    HIP_TRY(dalloc(&b->d_fix_count, 1));
+    HIP_TRY(dalloc(&b->d_regions, F));
+  }
   HIP_TRY(dalloc(&b->d_hist, F * 4 * 257));
   HIP_TRY(dalloc(&b->d_ehuf, F * 4 * 256));
-  HIP_TRY(dalloc(&b->d_tok, F * g.nseg * SEG_TOK));
-  HIP_TRY(dalloc(&b->d_tok0, F * g.nseg));
-  HIP_TRY(dalloc(&b->d_seg_ntok, F * g.nseg));
-  HIP_TRY(dalloc(&b->d_seg_bits, F * g.nseg));
-  HIP_TRY(dalloc(&b->d_seg_off, F * g.nseg));
   HIP_TRY(dalloc(&b->d_raw, F * g.raw_fs));
   HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * F * g.raw_fs, b->stream));
   HIP_TRY(dalloc(&b->d_scan_bits, F * 3));
@@ -355,15 +370,10 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
   HIP_TRY(dalloc(&b->d_out, F * g.out_cap));
   HIP_TRY(dalloc(&b->d_err, F));
   HIP_TRY(dalloc(&b->d_replays, 1));
-  HIP_TRY(dalloc(&b->d_fix, F * g.nblk));
   HIP_TRY(dalloc(&b->d_ffc, F * 3 * emit_chunks(g)));
   HIP_TRY(dalloc(&b->d_choff, F * 3 * emit_chunks(g)));
-  HIP_TRY(dalloc(&b->d_pack_state, F * ((g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((g.nsc + PACK_SEGS - 1) / PACK_SEGS))));
-  HIP_TRY(dalloc(&b->d_pack_ticket, 1));
-  HIP_TRY(dalloc(&b->d_fix_count, 1));
   HIP_TRY(hipMemsetAsync(b->d_replays, 0, sizeof(unsigned), b->stream));
   HIP_TRY(dalloc(&b->d_fdims, F));
-  HIP_TRY(dalloc(&b->d_regions, F));
   b->h_fdims.assign((size_t)F, make_int2(w, h));
   HIP_TRY(dalloc(&b->d_dcpred, F * 4));
   HIP_TRY(dalloc(&b->d_bitbase, F * 4));
@@ -392,12 +402,36 @@ extern "C" mij_batch *mij_batch_create(int device, int width, int height, int ma
   return b;
 }
 
+extern "C" mij_batch *mij_assembler_create(int device, int width, int height, int max_frames,
+                                           int quality) {
+  if (!valid_dims(width, height) || max_frames < 1 || quality < 1 || quality > 100) {
+    fail(MIJ_EINVAL, "assembler_create: bad geometry %dx%d x%d or quality %d", width, height,
+         max_frames, quality);
+    return nullptr;
+  }
+  mij_batch *b = new mij_batch;
+  if (batch_init(b, device, width, height, max_frames, quality, true)) {
+    batch_free(b);
+    return nullptr;
+  }
+  g_err = MIJ_OK;
+  return b;
+}
+
+// entry points that run the encoder itself: not on an assembler
+static int pipe_check(const mij_batch *b, const char *what) {
+  if (!b) return fail(MIJ_EINVAL, "%s: null batch", what);
+  if (b->assembler) return fail(MIJ_EINVAL, "%s: an assembler only assembles band words", what);
+  return MIJ_OK;
+}
+
 extern "C" void mij_batch_destroy(mij_batch *b) { batch_free(b); }
 
 extern "C" void *mij_batch_stream(mij_batch *b) { return b ? (void *)b->stream : nullptr; }
 
 extern "C" int mij_batch_upload(mij_batch *b, const uint8_t *bgr, int first, int nframes) {
-  if (!b || !bgr || first < 0 || nframes < 1 || first + nframes > b->cap)
+  if (pipe_check(b, "upload")) return g_err;
+  if (!bgr || first < 0 || nframes < 1 || first + nframes > b->cap)
     return fail(MIJ_EINVAL, "upload: bad args");
   if (!b->own_in) return fail(MIJ_EINVAL, "upload: batch reads external device input");
   HIP_TRY(hipSetDevice(b->dev));
@@ -410,7 +444,8 @@ extern "C" int mij_batch_upload(mij_batch *b, const uint8_t *bgr, int first, int
 
 extern "C" int mij_batch_set_input(mij_batch *b, const void *d_bgr, long long frame_stride,
                                    int pitch) {
-  if (!b || !d_bgr || ((uintptr_t)d_bgr & 15) || (pitch & 15) || (frame_stride & 15) ||
+  if (pipe_check(b, "set_input")) return g_err;
+  if (!d_bgr || ((uintptr_t)d_bgr & 15) || (pitch & 15) || (frame_stride & 15) ||
       pitch < b->g.w * 3)
     return fail(MIJ_EINVAL, "set_input: pointer, pitch and frame stride must be 16-byte "
                             "aligned, pitch >= 3*w");
@@ -605,7 +640,8 @@ static void next_slot(mij_batch *b) {
 }
 
 extern "C" int mij_batch_encode(mij_batch *b, int nframes) {
-  if (!b || nframes < 1 || nframes > b->cap) return fail(MIJ_EINVAL, "encode: bad frame count");
+  if (pipe_check(b, "encode")) return g_err;
+  if (nframes < 1 || nframes > b->cap) return fail(MIJ_EINVAL, "encode: bad frame count");
   HIP_TRY(hipSetDevice(b->dev));
   next_slot(b);
   if (encode_frames(b, nframes)) return g_err;
@@ -741,7 +777,8 @@ extern "C" int mij_batch_set_split(mij_batch *b, int on) {
 }
 
 extern "C" int mij_batch_dct(mij_batch *b, int nframes) {
-  if (!b || nframes < 1 || nframes > b->cap) return fail(MIJ_EINVAL, "dct: bad frame count");
+  if (pipe_check(b, "dct")) return g_err;
+  if (nframes < 1 || nframes > b->cap) return fail(MIJ_EINVAL, "dct: bad frame count");
   HIP_TRY(hipSetDevice(b->dev));
   next_slot(b);
   if (b->timing) HIP_TRY(hipEventRecord(b->ev[0], b->stream));
@@ -801,7 +838,7 @@ extern "C" int mij_batch_stage_ms(mij_batch *b, float *ms, int n) {
 }
 
 extern "C" unsigned long long mij_batch_token_count(mij_batch *b, int nframes) {
-  if (!b || nframes < 1 || nframes > b->cap) return 0;
+  if (!b || b->assembler || nframes < 1 || nframes > b->cap) return 0;
   hipSetDevice(b->dev);
   hipStreamSynchronize(b->stream);
   std::vector<uint32_t> v((size_t)nframes * b->g.nseg);
@@ -1128,8 +1165,9 @@ extern "C" int mij_encode_regions(const uint8_t *bgr, int stride_px, int frame_h
 // band's last DC, the tables are built from the summed histograms, and each
 // band's share of a scan starts at the sum of the earlier bands' bits.
 // ---------------------------------------------------------------------------
-static int band_check(mij_batch *b, int n, const char *what) {
+static int band_check(mij_batch *b, int n, const char *what, bool assembling = false) {
   if (!b || n < 1 || n > b->cap) return fail(MIJ_EINVAL, "%s: bad frame count", what);
+  if (!assembling && pipe_check(b, what)) return g_err;
   HIP_TRY(hipSetDevice(b->dev));
   return MIJ_OK;
 }
@@ -1226,7 +1264,8 @@ static uint32_t *scan_words(mij_batch *b, int frame, int comp) {
 
 extern "C" int mij_band_words(mij_batch *b, int frame, int comp, void *dst, size_t cap_words,
                               int dst_on_device) {
-  if (!b || frame < 0 || frame >= b->cap || comp < 0 || comp > 2 || !dst)
+  if (pipe_check(b, "band_words")) return g_err;
+  if (frame < 0 || frame >= b->cap || comp < 0 || comp > 2 || !dst)
     return fail(MIJ_EINVAL, "band_words: bad arguments");
   HIP_TRY(hipSetDevice(b->dev));
   const unsigned long long nw = b->band_words[frame * 3 + comp];
@@ -1237,8 +1276,68 @@ extern "C" int mij_band_words(mij_batch *b, int frame, int comp, void *dst, size
   return MIJ_OK;
 }
 
+extern "C" int mij_band_words_all(mij_batch *b, int n, void *dst, size_t cap_words, int dst_on_device) {
+  if (band_check(b, n, "band_words_all")) return g_err;
+  if (!dst) return fail(MIJ_EINVAL, "band_words_all: null dst");
+  unsigned long long total = 0;
+  for (int i = 0; i < 3 * n; i++) total += b->band_words[i];
+  if (cap_words < total) return fail(MIJ_ENOSPC, "band_words_all: need %llu words", total);
+  // (frame, comp) order, one stream-ordered copy each, one synchronisation
+  uint8_t *d = (uint8_t *)dst;
+  for (int f = 0; f < n; f++)
+    for (int c = 0; c < 3; c++) {
+      const unsigned long long nw = b->band_words[f * 3 + c];
+      if (nw)
+        HIP_TRY(hipMemcpyAsync(d, scan_words(b, f, c), nw * 4,
+                               dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, b->stream));
+      d += nw * 4;
+    }
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  return MIJ_OK;
+}
+
+extern "C" int mij_assemble_pieces(mij_batch *b, const void *src, size_t src_words, int src_on_device,
+                                   const unsigned long long *pieces, int npieces) {
+  if (!b || npieces < 0 || (npieces && (!src || !pieces)))
+    return fail(MIJ_EINVAL, "assemble_pieces: bad arguments");
+  long long max_words = 0;
+  for (int i = 0; i < npieces; i++) {
+    const unsigned long long *p = pieces + 4 * i;
+    const unsigned long long fc = p[0], f = fc / 3, c = fc % 3;
+    if (f >= (unsigned long long)b->cap || p[1] + p[3] > (unsigned long long)b->g.raw_words[c] ||
+        p[2] + p[3] > src_words)
+      return fail(MIJ_ENOSPC, "assemble_pieces: piece %d (frame %llu comp %llu) out of bounds", i, f, c);
+    max_words = std::max(max_words, (long long)p[3]);
+  }
+  if (!npieces || !max_words) return MIJ_OK;
+  HIP_TRY(hipSetDevice(b->dev));
+  const uint32_t *s32 = (const uint32_t *)src;
+  if (!src_on_device) {
+    if (b->stage_words < src_words) {
+      if (b->d_stage) HIP_TRY(hipFree(b->d_stage));
+      b->d_stage = nullptr;
+      HIP_TRY(dalloc(&b->d_stage, src_words));
+      b->stage_words = src_words;
+    }
+    HIP_TRY(hipMemcpyAsync(b->d_stage, src, src_words * 4, hipMemcpyHostToDevice, b->stream));
+    s32 = b->d_stage;
+  }
+  if (b->pieces_cap < (size_t)npieces) {
+    if (b->d_pieces) HIP_TRY(hipFree(b->d_pieces));
+    b->d_pieces = nullptr;
+    HIP_TRY(dalloc(&b->d_pieces, (size_t)npieces * 4));
+    b->pieces_cap = (size_t)npieces;
+  }
+  HIP_TRY(hipMemcpyAsync(b->d_pieces, pieces, sizeof(unsigned long long) * 4 * npieces, hipMemcpyHostToDevice,
+                         b->stream));
+  HIP_TRY(launch_or_pieces(b->d_raw, b->g, s32, b->d_pieces, npieces, max_words, b->stream));
+  // the caller may release or reuse src (and pieces) once this returns
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  return MIJ_OK;
+}
+
 extern "C" int mij_assemble_begin(mij_batch *b, int n, const uint32_t *hist) {
-  if (band_check(b, n, "assemble_begin")) return g_err;
+  if (band_check(b, n, "assemble_begin", true)) return g_err;
   if (!hist) return fail(MIJ_EINVAL, "assemble_begin: null hist");
   HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * n * b->g.raw_fs, b->stream));
   return upload_hist_tables(b, n, hist);
@@ -1269,7 +1368,7 @@ extern "C" int mij_assemble_words(mij_batch *b, int frame, int comp, unsigned lo
 }
 
 extern "C" int mij_assemble_end(mij_batch *b, int n, const unsigned long long *total_bits) {
-  if (band_check(b, n, "assemble_end")) return g_err;
+  if (band_check(b, n, "assemble_end", true)) return g_err;
   if (!total_bits) return fail(MIJ_EINVAL, "assemble_end: null total_bits");
   HIP_TRY(hipMemcpyAsync(b->d_scan_bits, total_bits, sizeof(uint64_t) * n * 3,
                          hipMemcpyHostToDevice, b->stream));

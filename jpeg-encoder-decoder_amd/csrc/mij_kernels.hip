@@ -2298,6 +2298,24 @@ __global__ void k_or_words(uint32_t *dst, const uint32_t *src, long long n) {
   if (i < n) dst[i] |= src[i];
 }
 
+// All bands' pieces of all scans in one launch (mij_assemble_pieces): piece
+// y = {frame * 3 + comp, first word in the scan, first source word, words};
+// blockIdx.x strides over the piece's words
+__global__ void k_or_pieces(uint32_t *raw, long long raw_fs, long long rw0, long long rw1,
+                            const uint32_t *src, const unsigned long long *pieces) {
+  const unsigned long long *pc = pieces + 4 * (long long)blockIdx.y;
+  const long long fc = (long long)pc[0], n = (long long)pc[3];
+  const long long f = fc / 3, c = fc - 3 * f;
+  uint32_t *dst = raw + f * raw_fs + (c == 0 ? 0 : rw0 + (c == 2 ? rw1 : 0)) + (long long)pc[1];
+  const uint32_t *sp = src + (long long)pc[2];
+  // neighbouring bands share at most their boundary word, and their pieces
+  // run concurrently: the first and last word of a piece are OR-ed atomically
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    if (i == 0 || i == n - 1) atomicOr(&dst[i], sp[i]);
+    else dst[i] |= sp[i];
+  }
+}
+
 // ---- tiny self-test used by the test-suite: exact i8 MFMA layout check ----
 __global__ void k_mfma_probe(const int4 *A, const int4 *B, int4 *D) {
   const int lane = threadIdx.x;
@@ -2417,6 +2435,15 @@ hipError_t launch_scan(const EntArgs &a, hipStream_t s) {
 hipError_t launch_or_words(uint32_t *dst, const uint32_t *src, long long n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_or_words, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dst, src, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_or_pieces(uint32_t *raw, const Geom &g, const uint32_t *src,
+                            const unsigned long long *d_pieces, int npieces, long long max_words, hipStream_t s) {
+  if (npieces <= 0 || max_words <= 0) return hipSuccess;
+  const long long chunks = (max_words + 1023) / 1024;
+  hipLaunchKernelGGL(k_or_pieces, dim3((unsigned)(chunks < 64 ? chunks : 64), (unsigned)npieces), dim3(256), 0, s,
+                     raw, g.raw_fs, g.raw_words[0], g.raw_words[1], src, d_pieces);
   return hipGetLastError();
 }
 

@@ -27,6 +27,7 @@ EXPORTS = [
     "mij_batch_stage_ms", "mij_batch_stage_history", "mij_batch_token_count", "mij_batch_geometry", "mij_batch_replays", "mij_batch_stream",
     "mij_band_analyze", "mij_band_histograms", "mij_band_tables", "mij_band_pack", "mij_band_words",
     "mij_assemble_begin", "mij_assemble_words", "mij_assemble_end",
+    "mij_band_words_all", "mij_assemble_pieces", "mij_assembler_create",
     "mij_probe_mfma", "mij_colour_lut", "mij_build_target",
     # change detector (reference include/brain.h:7-10 drop-in + extensions)
     "subsample", "store", "compare", "enlargeAdjust", "mij_set_frame_height",
@@ -125,6 +126,10 @@ def load() -> C.CDLL:
     lib.mij_assemble_begin.argtypes = [p, i, p]
     lib.mij_assemble_words.argtypes = [p, i, i, u64, p, C.c_size_t, i]
     lib.mij_assemble_end.argtypes = [p, i, p]
+    lib.mij_band_words_all.argtypes = [p, i, p, C.c_size_t, i]
+    lib.mij_assemble_pieces.argtypes = [p, p, C.c_size_t, i, p, i]
+    lib.mij_assembler_create.restype = p
+    lib.mij_assembler_create.argtypes = [i, i, i, i, i]
     lib.mij_probe_mfma.argtypes = [p, p, p]
     lib.mij_colour_lut.argtypes = [p]
     lib.mij_build_target.restype = C.c_char_p
@@ -286,13 +291,16 @@ class Batch:
     STAGES = ["k1_colour_dct_quant", "fix", "tokenize", "stats", "tables", "pack", "emit", "total"]
 
     def __init__(self, w: int, h: int, max_frames: int, quality: int = 50, device: int = 0,
-                 keep_coefs: bool = False):
+                 keep_coefs: bool = False, assembler: bool = False):
+        """assembler=True: mij_assembler_create -- a batch that only assembles
+        whole frames from band words (no input, coefficient or token buffers)."""
         self.lib = load()
         self.w, self.h, self.max_frames = w, h, max_frames
-        self.h_ = self.lib.mij_batch_create(device, w, h, max_frames, quality)
+        create = self.lib.mij_assembler_create if assembler else self.lib.mij_batch_create
+        self.h_ = create(device, w, h, max_frames, quality)
         self.fdims = None  # per-frame (w, h) of a region batch
         if not self.h_:
-            raise MijError(f"mij_batch_create failed: "
+            raise MijError(f"{'mij_assembler_create' if assembler else 'mij_batch_create'} failed: "
                            f"{self.lib.mij_strerror(self.lib.mij_last_error()).decode()}")
         if keep_coefs:
             _check(self.lib.mij_batch_keep_coefs(self.h_, 1), "keep_coefs")
@@ -442,6 +450,30 @@ class Batch:
         out = np.zeros(max(nwords, 1), np.uint32)
         _check(self.lib.mij_band_words(self.h_, frame, comp, _ptr(out), nwords, 0), "band_words")
         return out[:nwords]
+
+    def band_words_all(self, n: int, dst=None, dst_dev_ptr: int = 0, cap_words: int = 0):
+        """Every scan's band words of frames 0..n-1 in (frame, comp) order, one
+        call: into device memory at dst_dev_ptr (cap_words words), into the
+        host array dst, or into a returned host array."""
+        if dst_dev_ptr:
+            _check(self.lib.mij_band_words_all(self.h_, n, dst_dev_ptr, cap_words, 1), "band_words_all")
+            return None
+        if dst is None:
+            dst = np.zeros(max(cap_words, 1), np.uint32)
+        _check(self.lib.mij_band_words_all(self.h_, n, _ptr(dst), dst.size, 0), "band_words_all")
+        return dst
+
+    def assemble_pieces(self, pieces: np.ndarray, src=None, src_dev_ptr: int = 0, src_words: int = 0) -> None:
+        """OR pieces {frame*3+comp, first word, first src word, words} of one
+        source buffer (device pointer or host array) into the scans."""
+        pc = np.ascontiguousarray(pieces, np.uint64).reshape(-1, 4)
+        if src_dev_ptr:
+            _check(self.lib.mij_assemble_pieces(self.h_, src_dev_ptr, src_words, 1, _ptr(pc), pc.shape[0]),
+                   "assemble_pieces")
+        else:
+            w = np.ascontiguousarray(src).view(np.uint32).reshape(-1)
+            _check(self.lib.mij_assemble_pieces(self.h_, _ptr(w), w.size, 0, _ptr(pc), pc.shape[0]),
+                   "assemble_pieces")
 
     def assemble_begin(self, n: int, hist: np.ndarray) -> None:
         h = np.ascontiguousarray(hist, np.uint32).reshape(n, 4, 257)

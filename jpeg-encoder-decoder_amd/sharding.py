@@ -57,129 +57,151 @@ def band_rows(height: int, world: int, rank: int):
 
 
 class TorchExchange:
-    """The four exchanges of a banded encode over torch.distributed: small
-    all-gathers / one all-reduce, plus point-to-point transfer of the packed
-    words to the root.  `device` is "cuda:<local>" for nccl (RCCL over xGMI)
-    or "cpu" for gloo."""
+    """The exchanges of a banded encode over torch.distributed: three small
+    collectives (all-gather of the last DCs, all-reduce of the histograms,
+    all-gather of the bit counts) and one gather of every rank's packed words
+    to the root.  `device` is "cuda:<local>" for nccl (RCCL over xGMI: the
+    words never leave HBM) or "cpu" for gloo."""
 
     def __init__(self, dist, device="cpu"):
         import torch
         self.torch, self.dist, self.device = torch, dist, device
         self.world = dist.get_world_size()
         self.rank = dist.get_rank()
+        self.on_dev = str(device).startswith("cuda")
+
+    def _tensor(self, arr):
+        # int16 / uint32 / uint64 counts travel as int32 / int32 / int64 (same bits)
+        import numpy as np
+        a = np.ascontiguousarray(arr)
+        view = {np.dtype(np.int16): np.int32, np.dtype(np.uint32): np.int32,
+                np.dtype(np.uint64): np.int64}.get(a.dtype)
+        a = a.astype(np.int32) if a.dtype == np.int16 else (a.view(view) if view else a)
+        return self.torch.from_numpy(a).to(self.device)
 
     def all_gather(self, arr):
         import numpy as np
-        t = self.torch.from_numpy(np.ascontiguousarray(arr).astype(np.int64)).to(self.device)
+        t = self._tensor(arr)
         out = [self.torch.empty_like(t) for _ in range(self.world)]
         self.dist.all_gather(out, t)
-        return [o.cpu().numpy() for o in out]
+        dt = np.asarray(arr).dtype
+        res = [o.cpu().numpy() for o in out]
+        return [r.astype(dt) if dt == np.int16 else r.view(dt) for r in res]
 
     def all_reduce_sum(self, arr):
         import numpy as np
-        t = self.torch.from_numpy(np.ascontiguousarray(arr).astype(np.int64)).to(self.device)
+        t = self._tensor(arr)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return t.cpu().numpy()
+        return t.cpu().numpy().view(np.asarray(arr).dtype)
 
     def words_buffer(self, nwords: int):
         # empty, not zeros: a fill kernel on torch's stream could race with the
         # library's copy into the buffer on its own stream
-        return self.torch.empty(max(int(nwords), 1), dtype=self.torch.int32, device=self.device)
+        t = self.torch.empty(max(int(nwords), 1), dtype=self.torch.int32, device=self.device)
+        if self.on_dev:  # the block is free on torch's stream order; the library writes on its own
+            self.torch.cuda.current_stream(self.device).synchronize()
+        return t
 
-    def send_to_root(self, buf):
-        self.dist.send(buf, dst=0)
-
-    def recv_from(self, buf, src: int):
-        self.dist.recv(buf, src=src)
+    def gather_words(self, buf):
+        """Every rank's equally sized word buffer to the root: [world, n] there,
+        None elsewhere."""
+        out = None
+        if self.rank == 0:
+            out = self.torch.empty((self.world, buf.numel()), dtype=buf.dtype, device=buf.device)
+            self.dist.gather(buf, gather_list=list(out.unbind(0)), dst=0)
+            if self.on_dev:  # the library reads it on its own stream
+                self.torch.cuda.synchronize(self.device)
+        else:
+            self.dist.gather(buf, dst=0)
+        return out
 
 
 class LocalExchange:
-    """world = 1: the exchanges of encode_banded degenerate to identities."""
-    world, rank, device = 1, 0, "cpu"
+    """world = 1: the exchanges of encode_banded degenerate to identities.
+    device "cuda:<n>" keeps the word buffer in HBM (torch's HIP runtime must
+    then have been initialised before the library's, as bench.py does)."""
+    world, rank = 1, 0
 
-    def __init__(self):
+    def __init__(self, device="cpu"):
         import torch
-        self.torch = torch
+        self.torch, self.device = torch, device
+        self.on_dev = str(device).startswith("cuda")
 
     def all_gather(self, arr):
         import numpy as np
-        return [np.ascontiguousarray(arr).astype(np.int64)]
+        return [np.ascontiguousarray(arr)]
 
     def all_reduce_sum(self, arr):
         import numpy as np
-        return np.ascontiguousarray(arr).astype(np.int64)
+        return np.ascontiguousarray(arr)
 
     def words_buffer(self, nwords: int):
-        return self.torch.empty(max(int(nwords), 1), dtype=self.torch.int32)
+        t = self.torch.empty(max(int(nwords), 1), dtype=self.torch.int32, device=self.device)
+        if self.on_dev:
+            self.torch.cuda.current_stream(self.device).synchronize()
+        return t
+
+    def gather_words(self, buf):
+        return buf.reshape(1, -1)
+
+
+def band_pieces(allbits, alloff):
+    """Word counts of every (rank, frame, scan) band share -- they follow from
+    the bit counts, so they need no exchange of their own -- and the
+    assemble_pieces table for a [world, maxw] gathered buffer whose rank-r row
+    holds that rank's words in (frame, scan) order: rows {frame * 3 + scan,
+    first word in the scan, first source word, words}."""
+    import numpy as np
+    world, n = allbits.shape[:2]
+    allnw = ((alloff & np.uint64(31)) + allbits + np.uint64(31)) >> np.uint64(5)   # [world, n, 3]
+    flat = allnw.reshape(world, n * 3)
+    starts = np.concatenate([np.zeros((world, 1), np.uint64), np.cumsum(flat, axis=1)[:, :-1]], axis=1)
+    maxw = int(flat.sum(axis=1).max()) if world else 0
+    r, k = np.nonzero(flat)
+    pieces = np.stack([k.astype(np.uint64), alloff.reshape(world, n * 3)[r, k] >> np.uint64(5),
+                       r.astype(np.uint64) * np.uint64(max(maxw, 1)) + starts[r, k], flat[r, k]], axis=1)
+    return allnw, maxw, pieces.astype(np.uint64)
 
 
 def encode_banded(band, n: int, xch, frame_batch=None):
     """This rank's share of encoding n frames split into xch.world bands.
 
     `band` is a mijpeg.Batch of width x band rows holding this rank's bands of
-    the n frames; `frame_batch` (root only) a Batch of the whole frame that
-    receives the assembled JFIF streams (read them with frame_batch.output).
-    Returns the per-frame, per-scan total bits.  The exchanges follow
+    the n frames; `frame_batch` (root only) a Batch of the whole frame -- an
+    assembler (mijpeg.Batch(..., assembler=True)) is enough -- that receives
+    the assembled JFIF streams (read them with frame_batch.output).  Returns
+    the per-frame, per-scan total bits.  The exchanges follow
     include/mijpeg.h: last DCs (all-gather), histograms (all-reduce), bits
-    (all-gather), packed words (to the root)."""
+    (all-gather), then every rank's packed words in one buffer (one library
+    copy), gathered to the root in one collective and OR-ed into the scans in
+    one launch."""
     import numpy as np
     rank, world = xch.rank, xch.world
-    last = band.band_analyze(n)                                    # [n, 3]
+    last = band.band_analyze(n)                                    # [n, 3] int16
     lasts = xch.all_gather(last)
-    prev = np.zeros((n, 3), np.int16) if rank == 0 else lasts[rank - 1].astype(np.int16)
-    hist = band.band_histograms(n, prev)                           # [n, 4, 257]
-    ghist = xch.all_reduce_sum(hist).astype(np.uint32)
-    bits = band.band_tables(n, ghist)                              # [n, 3]
-    allbits = np.stack(xch.all_gather(bits)).astype(np.uint64)    # [world, n, 3]
-    offset = allbits[:rank].sum(axis=0) if rank else np.zeros((n, 3), np.uint64)
-    total = allbits.sum(axis=0)
-    nw = band.band_pack(n, offset).astype(np.int64)                # [n, 3]
-    allnw = np.stack(xch.all_gather(nw))                           # [world, n, 3]
+    prev = np.zeros((n, 3), np.int16) if rank == 0 else lasts[rank - 1]
+    hist = band.band_histograms(n, prev)                           # [n, 4, 257] uint32
+    ghist = xch.all_reduce_sum(hist)
+    bits = band.band_tables(n, ghist)                              # [n, 3] uint64
+    allbits = np.stack(xch.all_gather(bits))                       # [world, n, 3]
     alloff = np.concatenate([np.zeros((1, n, 3), np.uint64), np.cumsum(allbits, axis=0)[:-1]])
-    on_dev = str(xch.device).startswith("cuda")
-
-    def flat_words(r_nw):
-        starts = np.concatenate([[0], np.cumsum(r_nw.reshape(-1))])
-        return starts
-
-    my_starts = flat_words(nw)
-    buf = xch.words_buffer(my_starts[-1])
-    for f in range(n):
-        for c in range(3):
-            k = f * 3 + c
-            cnt = int(nw[f, c])
-            if not cnt:
-                continue
-            if on_dev:
-                band.band_words(f, c, cnt, dst_dev_ptr=buf.data_ptr() + 4 * int(my_starts[k]))
-            else:
-                buf[int(my_starts[k]):int(my_starts[k]) + cnt] = xch.torch.from_numpy(
-                    band.band_words(f, c, cnt).view(np.int32))
+    total = allbits.sum(axis=0)
+    nw = band.band_pack(n, alloff[rank])                           # [n, 3]
+    allnw, maxw, pieces = band_pieces(allbits, alloff)
+    if not np.array_equal(allnw[rank], nw):
+        raise RuntimeError("band word counts differ from the ones the bit counts imply")
+    buf = xch.words_buffer(maxw)
+    if xch.on_dev:
+        band.band_words_all(n, dst_dev_ptr=buf.data_ptr(), cap_words=buf.numel())
+    else:
+        band.band_words_all(n, dst=buf.numpy())
+    gathered = xch.gather_words(buf)
     if rank != 0:
-        xch.send_to_root(buf)
         return total
     frame_batch.assemble_begin(n, ghist)
-    for r in range(world):
-        starts = flat_words(allnw[r])
-        if r == 0:
-            rbuf = buf
-        else:
-            rbuf = xch.words_buffer(starts[-1])
-            xch.recv_from(rbuf, r)
-        if on_dev:
-            xch.torch.cuda.synchronize(xch.device)
-        for f in range(n):
-            for c in range(3):
-                k = f * 3 + c
-                cnt = int(allnw[r][f, c])
-                if not cnt:
-                    continue
-                first_word = int(alloff[r][f, c]) >> 5
-                if on_dev:
-                    frame_batch.assemble_words(f, c, first_word, src_dev_ptr=rbuf.data_ptr() + 4 * int(starts[k]),
-                                               nwords=cnt)
-                else:
-                    frame_batch.assemble_words(f, c, first_word,
-                                               rbuf[int(starts[k]):int(starts[k]) + cnt].numpy().view(np.uint32))
+    if xch.on_dev:
+        frame_batch.assemble_pieces(pieces, src_dev_ptr=gathered.data_ptr(), src_words=gathered.numel())
+    else:
+        frame_batch.assemble_pieces(pieces, src=gathered.numpy())
     frame_batch.assemble_end(n, total)
     return total

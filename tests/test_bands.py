@@ -16,8 +16,10 @@ import sharding
 pytestmark = pytest.mark.gpu
 
 
-def encode_banded_local(frames: np.ndarray, world: int, quality: int = 50):
-    """All bands of n frames in one process; mirrors sharding.encode_banded."""
+def encode_banded_local(frames: np.ndarray, world: int, quality: int = 50, per_scan: bool = False):
+    """All bands of n frames in one process; mirrors sharding.encode_banded
+    (per_scan: the per-(frame, scan) calls mij_band_words / mij_assemble_words
+    on a full batch instead of the one-call exchange on an assembler)."""
     import mijpeg
     n, H, W = frames.shape[:3]
     bands = []
@@ -32,14 +34,22 @@ def encode_banded_local(frames: np.ndarray, world: int, quality: int = 50):
     ghist = np.sum(np.stack(hists).astype(np.int64), axis=0).astype(np.uint32)
     bits = np.stack([b.band_tables(n, ghist) for b in bands]).astype(np.uint64)
     offs = np.concatenate([np.zeros((1, n, 3), np.uint64), np.cumsum(bits, axis=0)[:-1]])
-    full = mijpeg.Batch(W, H, n, quality)
+    full = mijpeg.Batch(W, H, n, quality, assembler=not per_scan)
     full.assemble_begin(n, ghist)
-    for r, b in enumerate(bands):
-        nw = b.band_pack(n, offs[r])
-        for f in range(n):
-            for c in range(3):
-                words = b.band_words(f, c, int(nw[f, c]))
-                full.assemble_words(f, c, int(offs[r][f, c]) >> 5, words)
+    if per_scan:
+        for r, b in enumerate(bands):
+            nw = b.band_pack(n, offs[r])
+            for f in range(n):
+                for c in range(3):
+                    words = b.band_words(f, c, int(nw[f, c]))
+                    full.assemble_words(f, c, int(offs[r][f, c]) >> 5, words)
+    else:
+        allnw, maxw, pieces = sharding.band_pieces(bits, offs)
+        gathered = np.zeros((world, max(maxw, 1)), np.uint32)
+        for r, b in enumerate(bands):
+            assert np.array_equal(b.band_pack(n, offs[r]), allnw[r])
+            b.band_words_all(n, dst=gathered[r])
+        full.assemble_pieces(pieces, src=gathered)
     full.assemble_end(n, bits.sum(axis=0))
     out = [full.output(f) for f in range(n)]
     for b in bands:
@@ -63,6 +73,7 @@ def test_bands_one_mcu_row_each_and_quality():
     import recipes
     frame = recipes.config3_frame(3, 64, 640)[None]  # 4 MCU rows -> 4 one-row bands
     assert encode_banded_local(frame, 4, 75)[0] == O.cref_encode(frame[0], 75)
+    assert encode_banded_local(frame, 4, 75, per_scan=True)[0] == O.cref_encode(frame[0], 75)
 
 
 def test_bands_config4_shape_two_bands():
@@ -123,7 +134,7 @@ def _rank(rank, world, port, q):
         r0, rows = sharding.band_rows(H, world, rank)
         band = mijpeg.Batch(W, rows, 2)
         band.upload(np.ascontiguousarray(frames[:, r0:r0 + rows]))
-        full = mijpeg.Batch(W, H, 2) if rank == 0 else None
+        full = mijpeg.Batch(W, H, 2, assembler=True) if rank == 0 else None
         sharding.encode_banded(band, 2, sharding.TorchExchange(dist, "cpu"), full)
         if rank == 0:
             q.put([full.output(f) for f in range(2)])
@@ -147,3 +158,98 @@ def test_two_process_banded_encode_gloo():
         assert p.exitcode == 0
     frames = [recipes.config3_frame(1, 320, 480), recipes.noise(320, 480, 9)]
     assert outs == [O.cref_encode(f) for f in frames]
+
+
+def _nccl_rank(port, q):
+    # torch's HIP runtime first (as bench.py's dist_setup does): the bundled
+    # runtime of torch does not initialise after the library's in one process
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    import mijpeg
+    import recipes
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        frames = np.stack([recipes.config3_frame(2, 320, 480), recipes.noise(320, 480, 4)])
+        band = mijpeg.Batch(480, 320, 2)
+        band.upload(frames)
+        full = mijpeg.Batch(480, 320, 2, assembler=True)
+        xch = sharding.TorchExchange(dist, "cuda:0")
+        outs = []
+        for _ in range(2):  # a second step reuses torch's freed blocks
+            sharding.encode_banded(band, 2, xch, full)
+            outs.append([full.output(f) for f in range(2)])
+        try:
+            full.encode(1)
+            rejected = False
+        except mijpeg.MijError:
+            rejected = True
+        band.close()
+        full.close()
+        q.put((outs, rejected))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_one_rank_nccl_exchange_device_branch():
+    """encode_banded over a one-rank nccl (RCCL) process group: the device
+    branch -- band words copied into a device tensor in one call, gathered by
+    RCCL, OR-ed into an assembler's scans from device memory in one launch --
+    against the reference, in a fresh process."""
+    import multiprocessing as mp
+    import oracle as O
+    import recipes
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_rank, args=(_free_port(), q))
+    p.start()
+    outs, rejected = q.get(timeout=300)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    want = [O.cref_encode(recipes.config3_frame(2, 320, 480)), O.cref_encode(recipes.noise(320, 480, 4))]
+    assert outs == [want, want]
+    assert rejected, "an assembler batch must refuse to encode"
+
+
+def _fp_rank(rank, world, port, q):
+    """frame-parallel config-3 path on GPU 0: this rank's shard of the frames
+    through the HIP library, the timing reduction, the blobs to rank 0"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    import mijpeg
+    import recipes
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        frames = [recipes.config3_frame(f, 160, 256) for f in range(5)]
+        mine = sharding.frame_range(len(frames), world, rank)
+        b = mijpeg.Batch(256, 160, len(mine))
+        b.upload(np.stack([frames[i] for i in mine]))
+        b.encode(len(mine))
+        blobs = [b.output(i) for i in range(len(mine))]
+        b.close()
+        el, units = sharding.reduce_timing(1.0 + rank, len(mine), dist, "cpu")
+        got = [None] * world
+        dist.all_gather_object(got, blobs)
+        if rank == 0:
+            q.put((el, units, [x for g in got for x in g]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_process_frame_parallel_hip_gloo():
+    import multiprocessing as mp
+    import oracle as O
+    import recipes
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fp_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    el, units, blobs = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert (el, units) == (2.0, 5)
+    assert blobs == [O.cref_encode(recipes.config3_frame(f, 160, 256)) for f in range(5)]

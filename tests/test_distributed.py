@@ -91,16 +91,19 @@ def _xch_worker(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        import torch
         x = sharding.TorchExchange(dist, "cpu")
         g = x.all_gather(np.full((2, 3), rank + 1, np.int16))
+        b = x.all_gather(np.full((2, 3), (1 << 40) + rank, np.uint64))
         s = x.all_reduce_sum(np.full((2, 4, 257), rank + 1, np.uint32))
+        buf = x.words_buffer(5)
+        buf.copy_(torch.arange(5, dtype=torch.int32) + 10 * rank)
+        got = x.gather_words(buf)
         if rank == 0:
-            buf = x.words_buffer(5)
-            x.recv_from(buf, 1)
-            out.put(([a.tolist() for a in g], int(s.sum()), buf.tolist()))
+            out.put(([a.tolist() for a in g], [a.tolist() for a in b], str(b[0].dtype), int(s.sum()),
+                     str(s.dtype), got.tolist()))
         else:
-            import torch
-            x.send_to_root(torch.arange(5, dtype=torch.int32))
+            assert got is None
     finally:
         dist.destroy_process_group()
 
@@ -112,10 +115,45 @@ def test_torch_exchange_gloo_two_ranks():
     procs = [ctx.Process(target=_xch_worker, args=(r, 2, port, out)) for r in range(2)]
     for p in procs:
         p.start()
-    g, total, words = out.get(timeout=120)
+    g, b, bdt, total, sdt, words = out.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     assert g == [[[1] * 3] * 2, [[2] * 3] * 2]
-    assert total == (1 + 2) * 2 * 4 * 257
-    assert words == [0, 1, 2, 3, 4]
+    assert b == [[[(1 << 40)] * 3] * 2, [[(1 << 40) + 1] * 3] * 2] and bdt == "uint64"
+    assert total == (1 + 2) * 2 * 4 * 257 and sdt == "uint32"
+    assert words == [[0, 1, 2, 3, 4], [10, 11, 12, 13, 14]]
+
+
+def test_band_pieces_table_reassembles_scans():
+    """sharding.band_pieces: the word counts follow from the bit counts, and
+    OR-ing the pieces of a gathered [world, maxw] buffer at their first words
+    rebuilds each scan's bit string (a CPU model of mij_assemble_pieces)."""
+    rng = np.random.default_rng(5)
+    world, n = 4, 3
+    bits = rng.integers(0, 300, (world, n, 3)).astype(np.uint64)
+    bits[1, 0, 2] = 0  # an empty band share
+    off = np.concatenate([np.zeros((1, n, 3), np.uint64), np.cumsum(bits, axis=0)[:-1]])
+    allnw, maxw, pieces = sharding.band_pieces(bits, off)
+    # every band share as a bit string placed at its global offset
+    streams = {(f, c): rng.integers(0, 2, int(bits[:, f, c].sum())) for f in range(n) for c in range(3)}
+    gathered = np.zeros((world, maxw), np.uint32)
+    for r in range(world):
+        w = []
+        for f in range(n):
+            for c in range(3):
+                o, b = int(off[r, f, c]), int(bits[r, f, c])
+                nw = int(allnw[r, f, c])
+                assert nw == (o % 32 + b + 31) // 32
+                piece = np.zeros(nw * 32, np.uint8)
+                piece[o % 32:o % 32 + b] = streams[(f, c)][o:o + b]
+                w.append(np.packbits(piece).view(">u4").astype(np.uint32))
+        row = np.concatenate(w) if w else np.zeros(0, np.uint32)
+        gathered[r, :row.size] = row
+    scans = {k: np.zeros((v.size + 31) // 32 + 1, np.uint32) for k, v in streams.items()}
+    flat = gathered.reshape(-1)
+    for fc, first, src, cnt in pieces.tolist():
+        scans[(fc // 3, fc % 3)][first:first + cnt] |= flat[src:src + cnt]
+    for k, v in streams.items():
+        bitsout = np.unpackbits(scans[k].astype(">u4").view(np.uint8))[:v.size]
+        assert np.array_equal(bitsout, v), k
