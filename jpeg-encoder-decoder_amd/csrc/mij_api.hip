@@ -1223,12 +1223,11 @@ extern "C" int mij_band_tables(mij_batch *b, int n, const uint32_t *hist, unsign
   HIP_TRY(launch_scan(a, b->stream));
   HIP_TRY(hipMemcpyAsync(bits, b->d_scan_bits, sizeof(uint64_t) * n * 3, hipMemcpyDeviceToHost,
                          b->stream));
+  std::vector<int> err((size_t)n);
+  HIP_TRY(hipMemcpyAsync(err.data(), b->d_err, sizeof(int) * n, hipMemcpyDeviceToHost, b->stream));
   HIP_TRY(hipStreamSynchronize(b->stream));
-  int err = 0;
-  for (int f = 0; f < n; f++) {
-    HIP_TRY(hipMemcpy(&err, b->d_err + f, sizeof(int), hipMemcpyDeviceToHost));
-    if (err) return fail(MIJ_ETABLE, "band frame %d: Huffman table construction failed", f);
-  }
+  for (int f = 0; f < n; f++)
+    if (err[f]) return fail(MIJ_ETABLE, "band frame %d: Huffman table construction failed", f);
   return MIJ_OK;
 }
 
