@@ -529,7 +529,7 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int se
   static const bool wtime = getenv("MIJ_K1_WTIME") != nullptr;
   unsigned long long *d_wt = nullptr;
   const long long nw = grid * 16;
-  if (wtime && mode == 1) {
+  if (wtime && (mode == 1 || mode == 2)) {
     HIP_TRY(hipMalloc(&d_wt, sizeof(unsigned long long) * 3 * nw));
     HIP_TRY(hipMemsetAsync(d_wt, 0, sizeof(unsigned long long) * 3 * nw, b->stream));
     k.wtime = d_wt;

@@ -28,7 +28,10 @@ constexpr int DCTIE_WORDS = 33;      // DC tie bits for K = 0..1055 (|S| <= 8192
 constexpr int MAX_BLOCK_TOK = 65;                 // DC + 63 AC + EOB
 constexpr int SEG_TOK = 16 * MAX_BLOCK_TOK;       // 1040 tokens per segment slot
 constexpr int SEG_PER_WG = 64;                    // k_seg_bits segments per workgroup
-constexpr int PACK_SEGS = 64;                     // segments per k_pack workgroup
+#ifndef MIJ_PACK_SEGS
+#define MIJ_PACK_SEGS 64
+#endif
+constexpr int PACK_SEGS = MIJ_PACK_SEGS;          // segments per k_pack workgroup
 constexpr int MAX_BLOCK_BITS = 1729;              // 28 DC + 63 * 27 AC bits
 // k_pack assembles a group in LDS windows of PACK_WORDS words; a group wider
 // than one window (only near worst-case entropy) is packed in several passes.

@@ -20,6 +20,8 @@
 // Compiled with -ffp-contract=off: every FP64 operation that has to match the
 // reference is written with explicit __dmul_rn/__dadd_rn in the reference's
 // evaluation order; fp32 FMAs are explicit fmaf() calls.
+#include <stdlib.h>
+
 #include "mij_internal.h"
 
 namespace mij {
@@ -542,12 +544,15 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
                                             uint32_t *hAC, int16_t (*st)[16], int kflags = 0) {
   u4v c0, c1;
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    c0[k] = (uint32_t)(uint16_t)o[2 * k] | ((uint32_t)o[2 * k + 1] << 16);
-    c1[k] = (uint32_t)(uint16_t)o[8 + 2 * k] | ((uint32_t)o[9 + 2 * k] << 16);
+  for (int k = 0; k < 4; k++) {  // one v_perm per pair
+    c0[k] = pack_i16x2(o[2 * k], o[2 * k + 1]);
+    c1[k] = pack_i16x2(o[8 + 2 * k], o[9 + 2 * k]);
   }
-  *(u4v *)&st[lane][0] = c0;
-  *(u4v *)&st[lane][8] = c1;
+  // staged block-major (block b's 64 coefficients in zigzag order at st +
+  // 64 b): the AC loop below addresses coefficient z of its block directly
+  int16_t *stb = &st[0][0] + 64 * bcol + 16 * g;
+  *(u4v *)stb = c0;
+  *(u4v *)(stb + 8) = c1;
   // nonzero mask: min(half, 1) per packed int16 pair puts coefficient 2k's
   // flag at bit 2k and 2k+1's at bit 16+2k
   // (v_pk_min_u16 in asm: the compiler rewrites min(h, 1) into compares and
@@ -567,17 +572,21 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
   const auto r16 = __builtin_amdgcn_permlane16_swap(h, h, false, false);
   h = r16[0] | r16[1];
   const auto r32 = __builtin_amdgcn_permlane32_swap(h, h, false, false);
-  const unsigned long long M = ((unsigned long long)r32[1] << 32) | r32[0];
-  const int eob = !((M >> 63) & 1ull);
-  const int n = valid ? 1 + __popcll(M) + eob : 0;
+  const uint32_t Mlo = r32[0], Mhi = r32[1];
+  const int eob = !(Mhi >> 31);
+  const int n = valid ? 1 + __popc(Mlo) + __popc(Mhi) + eob : 0;
   // token offsets of the blocks inside their segment (chroma rows hold two
-  // 8-block segments: Cb | Cr)
+  // 8-block segments: Cb | Cr; a luma row is one 16-block segment, where the
+  // zero fill of row_shr already stops the scan at the row start)
   const int pos = chroma ? (bcol & 7) : bcol;
   uint32_t incl = (uint32_t)n;
-  incl += row_shr0<1>(incl) & (pos >= 1 ? ~0u : 0u);
-  incl += row_shr0<2>(incl) & (pos >= 2 ? ~0u : 0u);
-  incl += row_shr0<4>(incl) & (pos >= 4 ? ~0u : 0u);
-  if (!chroma) incl += row_shr0<8>(incl);
+  if (chroma) {
+    incl += row_shr0<1>(incl) & (pos >= 1 ? ~0u : 0u);
+    incl += row_shr0<2>(incl) & (pos >= 2 ? ~0u : 0u);
+    incl += row_shr0<4>(incl) & (pos >= 4 ? ~0u : 0u);
+  } else {
+    incl = row_scan16(incl);
+  }
   const int base = (int)incl - n;
   const int dc0 = o[0];
   const int prev = (int)row_shr0<1>((uint32_t)dc0);
@@ -602,23 +611,38 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
     const unsigned long long eobs = __ballot(g == 0 && valid && eob);
     if (lane == 0 && eobs) atomicAdd(&hAC[0x00], (unsigned)__popcll(eobs));
   }
-  if (valid && !(kflags & K1F_NO_ACLOOP)) {  // lane (g, b) takes the zigzag positions z == g (mod 4)
-    unsigned long long mm = M & (0x1111111111111111ull << g);
-    while (mm) {
-      const int z = __ffsll((long long)mm) - 1;
-      mm &= mm - 1ull;
-      const int cz = st[(z >> 4) * 16 + bcol][z & 15];
-      const unsigned long long before = M & ((1ull << z) - 1ull);
-      const int run = z - (63 - __clzll(before | 1ull)) - 1;
-      const int cls = mag_class(cz);
-      const int sym = ((run & 15) << 4) | cls;
-      if (!(kflags & K1F_NO_TOKSTORE))
-        segtok[base + 1 + __popcll(before)] =
-            (uint32_t)sym | ((uint32_t)(run >> 4) << 8) | TOK_AC | (mag_bits(cz, cls) << 16);
+  // AC tokens (encoder.c:448-460, ZRLs :490-494): lane (g, b) takes the
+  // zigzag positions z == g (mod 4) of block b, those below 32 first, then
+  // the rest, so the mask work is 32-bit: a token's index in the segment is
+  // base + 1 + the block's set bits below z, its run the distance to the
+  // highest of them (the DC at z = 0 when there is none).  Token word:
+  // (run << 4 | cls) is sym | ZRLs << 8 (run <= 62).
+  if (valid && !(kflags & K1F_NO_ACLOOP)) {
+    const int16_t *sl = &st[0][0] + 64 * bcol;
+    auto token = [&](int z, int rank, int zp) {
+      const int cz = sl[z];
+      const int run = z - zp - 1;
+      const uint32_t a = (uint32_t)max(cz, -cz);
+      const uint32_t cls = 32u - (uint32_t)__builtin_clz(a);  // a != 0
+      const uint32_t mag = __builtin_amdgcn_ubfe((uint32_t)(cz + (cz >> 31)), 0u, cls);
+      const uint32_t t = ((uint32_t)run << 4) | cls | TOK_AC;
+      if (!(kflags & K1F_NO_TOKSTORE)) segtok[(uint32_t)(base + 1 + rank)] = t | (mag << 16);
       if (!(kflags & K1F_NO_HIST)) {
-        atomicAdd(&hAC[sym], 1u);
+        atomicAdd(&hAC[t & 255u], 1u);
         if (run >= 16) atomicAdd(&hAC[0xF0], (unsigned)(run >> 4));
       }
+    };
+    const uint32_t cm = 0x11111111u << g;
+    for (uint32_t m = Mlo & cm; m; m &= m - 1u) {
+      const int z = __builtin_ctz(m);
+      const uint32_t bef = Mlo & ((1u << z) - 1u);
+      token(z, __popc(bef), 31 - __clz((int)(bef | 1u)));
+    }
+    const int rank_lo = __popc(Mlo), zp_lo = 31 - __clz((int)(Mlo | 1u));
+    for (uint32_t m = Mhi & cm; m; m &= m - 1u) {
+      const int zz = __builtin_ctz(m);
+      const uint32_t bef = Mhi & ((1u << zz) - 1u);
+      token(32 + zz, rank_lo + __popc(bef), bef ? 63 - __clz((int)bef) : zp_lo);
     }
   }
   wave_lds_sync();
@@ -1744,7 +1768,10 @@ constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = 
 // of each of a row's PACK_SEGS / 16 segments stay in registers from phase 1 to
 // phase 3 (tokens are read once unless a segment holds more than
 // 64 * LB_STEPS tokens)
-constexpr int LB_SEGS_PER_ROW = PACK_SEGS / 16;
+constexpr int LB_SEGS_PER_ROW = 4;
+constexpr int LB_ROWS = PACK_SEGS / LB_SEGS_PER_ROW;   // 16-lane rows per workgroup
+constexpr int LB_THREADS = 16 * LB_ROWS;
+constexpr int LB_VPL = PACK_SEGS / 64;                 // look-back scan: segments per lane
 #ifndef MIJ_LB_STEPS
 #define MIJ_LB_STEPS 1
 #endif
@@ -1752,7 +1779,7 @@ constexpr int LB_SEGS_PER_ROW = PACK_SEGS / 16;
 #define MIJ_LB_OCC 7
 #endif
 constexpr int LB_STEPS = MIJ_LB_STEPS;
-static_assert(PACK_SEGS % 16 == 0, "k_pack_lb: 16 lanes per segment");
+static_assert(PACK_SEGS % 64 == 0 && LB_THREADS <= 1024, "k_pack_lb: 4 segments per 16-lane row");
 
 // bits of a token (encoder.c:434-460, ZRLs :490-494); tab = [DC | AC][256]
 // len << 16 | code of this scan's tables
@@ -1773,7 +1800,7 @@ __device__ __forceinline__ void put_bits64(uint32_t *buf, uint32_t pos, unsigned
   if (off + len > 64) atomicOr(&buf[w + 2], __builtin_amdgcn_alignbit(lo, 0u, off));
 }
 
-__global__ __launch_bounds__(256, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
+__global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
   __shared__ uint32_t buf[PACK_WORDS];
   __shared__ uint32_t tab[2 * 256];
   __shared__ uint32_t s_bits[PACK_SEGS], s_off[PACK_SEGS];
@@ -1815,21 +1842,21 @@ __global__ __launch_bounds__(256, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
   int nt[LB_SEGS_PER_ROW];
 #pragma unroll
   for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
-    const int sl = row + 16 * k;
+    const int sl = row + LB_ROWS * k;
     nt[k] = sl < nsg ? min((int)a.seg_ntok[fs0 + sl], SEG_TOK) : 0;
   }
   u4v tq[LB_SEGS_PER_ROW][LB_STEPS];
 #pragma unroll
   for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
-    const uint32_t *tk = a.tok + (fs0 + row + 16 * k) * SEG_TOK;
+    const uint32_t *tk = a.tok + (fs0 + row + LB_ROWS * k) * SEG_TOK;
 #pragma unroll
     for (int st = 0; st < LB_STEPS; st++) {
       const int j = 64 * st + 4 * sub;
       tq[k][st] = j < nt[k] ? *(const u4v *)(tk + j) : u4v{0u, 0u, 0u, 0u};
     }
-    if (sub == 0 && nt[k] > 0) tq[k][0][0] = a.tok0[fs0 + row + 16 * k];  // token 0
+    if (sub == 0 && nt[k] > 0) tq[k][0][0] = a.tok0[fs0 + row + LB_ROWS * k];  // token 0
   }
-  for (int i = tid; i < 512; i += 256) tab[i] = a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + i];
+  for (int i = tid; i < 512; i += LB_THREADS) tab[i] = a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + i];
   __syncthreads();
   const uint32_t zac = tab[256 + 0xF0];
   const uint32_t Lz = zac >> 16, zcode = zac & 0xFFFFu;
@@ -1846,14 +1873,14 @@ __global__ __launch_bounds__(256, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
   };
   // steps past the registers (segments of more than 64 * LB_STEPS tokens)
   auto load_step = [&](int k, int i0) -> u4v {
-    const uint32_t *tk = a.tok + (fs0 + row + 16 * k) * SEG_TOK;
+    const uint32_t *tk = a.tok + (fs0 + row + LB_ROWS * k) * SEG_TOK;
     const int j = i0 + 4 * sub;
     return j < nt[k] ? *(const u4v *)(tk + j) : u4v{0u, 0u, 0u, 0u};
   };
   // ---- 1. bits of each segment ---------------------------------------------
 #pragma unroll
   for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
-    const int sl = row + 16 * k;
+    const int sl = row + LB_ROWS * k;
     if (sl >= nsg) break;  // row-uniform
     uint32_t b = 0;
 #pragma unroll
@@ -1866,9 +1893,19 @@ __global__ __launch_bounds__(256, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
   LB_STAMP(1);
   // ---- 2. offsets inside the group, group total, look-back -----------------
   if (wave == 0) {
-    const uint32_t v = lane < nsg ? s_bits[lane] : 0u;
+    uint32_t vv[LB_VPL], v = 0;
+#pragma unroll
+    for (int i = 0; i < LB_VPL; i++) {
+      vv[i] = lane * LB_VPL + i < nsg ? s_bits[lane * LB_VPL + i] : 0u;
+      v += vv[i];
+    }
     const uint32_t incl = wave_scan64(v);
-    if (lane < nsg) s_off[lane] = incl - v;
+    uint32_t run = incl - v;
+#pragma unroll
+    for (int i = 0; i < LB_VPL; i++) {
+      if (lane * LB_VPL + i < nsg) s_off[lane * LB_VPL + i] = run;
+      run += vv[i];
+    }
     const unsigned long long T = __shfl(incl, 63);
     const unsigned long long base = a.bit_base ? a.bit_base[f * 4 + comp] : 0u;
     unsigned long long *stt = a.pack_state;
@@ -1917,7 +1954,7 @@ __global__ __launch_bounds__(256, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
   for (uint32_t w0 = 0; w0 < nw; w0 += PACK_WORDS) {
     const uint32_t wn = min((uint32_t)PACK_WORDS, nw - w0);
     const uint32_t lo_bit = w0 * 32, hi_bit = (w0 + wn) * 32;
-    for (uint32_t i = tid; i < wn; i += 256) buf[i] = 0;
+    for (uint32_t i = tid; i < wn; i += LB_THREADS) buf[i] = 0;
     __syncthreads();
     // one window covers the group (all but near worst-case entropy): lanes
     // merge their 4 tokens in a 64-bit register and OR it in with <= 3 LDS
@@ -1964,7 +2001,7 @@ __global__ __launch_bounds__(256, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
     if (whole) {
 #pragma unroll
       for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
-        const int sl = row + 16 * k;
+        const int sl = row + LB_ROWS * k;
         if (sl >= nsg) break;  // row-uniform
         uint32_t pos0 = bit0 + s_off[sl];
 #pragma unroll
@@ -1977,7 +2014,7 @@ __global__ __launch_bounds__(256, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
     }
     if (__ballot(slow)) {  // second pass over this wave's rows, tokens reloaded
       for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
-        const int sl = row + 16 * k;
+        const int sl = row + LB_ROWS * k;
         if (sl >= nsg) break;  // row-uniform
         uint32_t pos0 = bit0 + s_off[sl];
         if (pos0 >= hi_bit || pos0 + s_bits[sl] <= lo_bit) continue;  // row-uniform
@@ -2006,7 +2043,7 @@ __global__ __launch_bounds__(256, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
     }
     __syncthreads();
     // the edge words may be shared with the neighbouring groups: OR (onto zero)
-    for (uint32_t i = tid; i < wn; i += 256) {
+    for (uint32_t i = tid; i < wn; i += LB_THREADS) {
       const uint32_t wi = w0 + i;
       if (wi == 0 || wi == nw - 1) atomicOr(&raw[wi], buf[i]);
       else raw[wi] = buf[i];
@@ -2360,8 +2397,10 @@ int k1_grid(int device, long long ntiles, int mode) {
     hipDeviceProp_t prop;
     cus = hipGetDeviceProperties(&prop, device) == hipSuccess ? prop.multiProcessorCount : 256;
   }
+  // MIJ_K1_GRID_MULT (A/B timing): workgroups per resident slot
+  static const int mult = getenv("MIJ_K1_GRID_MULT") ? atoi(getenv("MIJ_K1_GRID_MULT")) : 1;
   long long want = (ntiles + nw - 1) / nw;
-  long long cap = (long long)cus * per_cu;
+  long long cap = (long long)cus * per_cu * (mult > 0 ? mult : 1);
   return (int)(want < cap ? want : cap);
 }
 
@@ -2458,7 +2497,7 @@ hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s) {
   hipError_t e = hipMemsetAsync(a.pack_state, 0, sizeof(unsigned long long) * groups, s);
   if (e == hipSuccess) e = hipMemsetAsync(a.pack_ticket, 0, sizeof(unsigned), s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_pack_lb, dim3((unsigned)groups), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_pack_lb, dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_emit(const EntArgs &a, hipStream_t s) {
