@@ -410,23 +410,38 @@ __device__ __forceinline__ void convert4(uint32_t w0, uint32_t w1, uint32_t w2, 
 }
 
 // Rare path: the Y corrections of a run as a packed byte-wise subtrahend.
-// Only the pixel slots that hold an exact-integer Y in some lane pay for the
-// bitmap read (one wave-uniform branch per slot).
-template <bool RGB>
+// Only the pixel slots that hold an exact-integer Y in some lane pay for a
+// bitmap read (one wave-uniform branch per slot), and the read walks the
+// lanes that need it with scalar loads: a vector load's s_waitcnt vmcnt(0)
+// would also wait for every token store still in flight.
+// (GLOBAL_LUT false: the bitmap is in LDS, read per lane)
+template <bool RGB, bool GLOBAL_LUT>
 __device__ __forceinline__ uint32_t y_fix(uint32_t w0, uint32_t w1, uint32_t w2, const float (&fy)[4],
-                                          const uint32_t *__restrict__ lut) {
+                                          const uint32_t *__restrict__ lut, int lane) {
   const uint32_t Gv[4] = {(w0 >> 8) & 255, w1 & 255, w1 >> 24, (w2 >> 16) & 255};
   const uint32_t B0[4] = {w0 & 255, w0 >> 24, (w1 >> 16) & 255, (w2 >> 8) & 255};
   const uint32_t R0[4] = {(w0 >> 16) & 255, (w1 >> 8) & 255, w2 & 255, w2 >> 24};
   const uint32_t(&Rv)[4] = RGB ? B0 : R0;
+  typedef __attribute__((address_space(4))) const uint32_t cu32;  // uniform address: s_load
+  cu32 *slut = (cu32 *)lut;
   uint32_t corr = 0;
 #pragma unroll
   for (int p = 0; p < 4; p++) {
     const bool ey = fy[p] < 0.001f;
-    if (__ballot(ey)) {
+    unsigned long long m = __ballot(ey);
+    if (m && !GLOBAL_LUT) {
       const uint32_t i = (Rv[p] << 7) | (Gv[p] >> 1);  // integer Y needs R == G (mod 2)
       const uint32_t bit = (lut[i >> 5] >> (i & 31)) & 1u;
       corr |= (ey ? bit : 0u) << (8 * p);
+    } else if (m) {
+      const uint32_t i = (Rv[p] << 7) | (Gv[p] >> 1);
+      do {
+        const int l = __ffsll((long long)m) - 1;
+        m &= m - 1ull;
+        const uint32_t il = (uint32_t)__builtin_amdgcn_readlane((int)i, l);
+        const uint32_t bit = (slut[il >> 5] >> (il & 31)) & 1u;
+        if (lane == l) corr |= bit << (8 * p);
+      } while (m);
     }
   }
   return corr;
@@ -468,7 +483,7 @@ __device__ __forceinline__ uint32_t chroma_pair(const uint32_t (&r0)[4], const u
   return s0 | (s1 << 8);
 }
 
-template <bool RGB>
+template <bool RGB, bool GLOBAL_LUT>
 __device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int c4, int pr,
                                              const uint32_t *__restrict__ lut, bool use_lut) {
   // all 8 row pieces of this lane up front: the exception branches below
@@ -505,7 +520,8 @@ __device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int
 #pragma unroll
     for (int dy = 0; dy < 2; dy++)
       if (__ballot(r[dy].cy)) {
-        const uint32_t corr = y_fix<RGB>(w[it][dy][0], w[it][dy][1], w[it][dy][2], r[dy].fy, lut);
+        const uint32_t corr = y_fix<RGB, GLOBAL_LUT>(w[it][dy][0], w[it][dy][1], w[it][dy][2], r[dy].fy, lut,
+                                                     c4 | (pr << 5));
         if (corr) *Yd[dy] = py[dy] - corr;  // no borrows: a corrected Y is >= 1
       }
     if (__ballot(r[0].cc | r[1].cc)) {
@@ -820,7 +836,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
           dma_wait();
         else if (DEFER)
           dma_wait_behind_stores();
-        if (!(kflags & K1F_NO_COLOUR)) colour_stage<RGB>(raw, L, c4, pr, lut, !(kflags & K1F_NO_LUT));
+        if (!(kflags & K1F_NO_COLOUR)) colour_stage<RGB, !LUT_LDS>(raw, L, c4, pr, lut, !(kflags & K1F_NO_LUT));
         wave_lds_sync();
         // ---- stream the wave's next tile into the freed raw buffer -----------
         if (REG) skip_outside(tn);
