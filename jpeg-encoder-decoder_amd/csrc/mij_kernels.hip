@@ -447,25 +447,45 @@ __device__ __forceinline__ uint32_t y_fix(uint32_t w0, uint32_t w1, uint32_t w2,
   return corr;
 }
 
-// Rare path: Cb / Cr corrections (0/1 per pixel) of a run.
-template <bool RGB>
+// Rare path: Cb / Cr corrections (0/1 per pixel) of a run.  GLOBAL_LUT:
+// per pixel slot, only the lanes with an exact-integer candidate read the
+// bitmap, by scalar loads (as y_fix).
+template <bool RGB, bool GLOBAL_LUT>
 __device__ __forceinline__ void chroma_fix(uint32_t w0, uint32_t w1, uint32_t w2,
                                            const uint32_t *__restrict__ lut, uint32_t (&cbc)[4],
-                                           uint32_t (&crc)[4]) {
+                                           uint32_t (&crc)[4], int lane) {
   const uint32_t B0[4] = {w0 & 255, w0 >> 24, (w1 >> 16) & 255, (w2 >> 8) & 255};
   const uint32_t Gv[4] = {(w0 >> 8) & 255, w1 & 255, w1 >> 24, (w2 >> 16) & 255};
   const uint32_t R0[4] = {(w0 >> 16) & 255, (w1 >> 8) & 255, w2 & 255, w2 >> 24};
   const uint32_t(&Bv)[4] = RGB ? R0 : B0;
   const uint32_t(&Rv)[4] = RGB ? B0 : R0;
+  typedef __attribute__((address_space(4))) const uint32_t cu32;
+  cu32 *slut = (cu32 *)lut;
 #pragma unroll
   for (int p = 0; p < 4; p++) {
-    const uint32_t wb = lut[LUT_WORDS + ((Gv[p] << 2) | (Bv[p] >> 6))];
-    const uint32_t wr = lut[2 * LUT_WORDS + ((Gv[p] << 2) | (Rv[p] >> 6))];
     // bit (G<<7 | B>>1) of the Cb table; valid when R == G and B == G (mod 2)
     const bool eb = Rv[p] == Gv[p] && !((Bv[p] ^ Gv[p]) & 1);
     const bool er = Bv[p] == Gv[p] && !((Rv[p] ^ Gv[p]) & 1);
-    cbc[p] = (wb >> ((Bv[p] >> 1) & 31)) & (uint32_t)eb;
-    crc[p] = (wr >> ((Rv[p] >> 1) & 31)) & (uint32_t)er;
+    if (!GLOBAL_LUT) {
+      const uint32_t wb = lut[LUT_WORDS + ((Gv[p] << 2) | (Bv[p] >> 6))];
+      const uint32_t wr = lut[2 * LUT_WORDS + ((Gv[p] << 2) | (Rv[p] >> 6))];
+      cbc[p] = (wb >> ((Bv[p] >> 1) & 31)) & (uint32_t)eb;
+      crc[p] = (wr >> ((Rv[p] >> 1) & 31)) & (uint32_t)er;
+      continue;
+    }
+    cbc[p] = crc[p] = 0;
+    for (int t = 0; t < 2; t++) {
+      unsigned long long m = __ballot(t ? er : eb);
+      if (!m) continue;
+      const uint32_t i = (Gv[p] << 7) | ((t ? Rv[p] : Bv[p]) >> 1);
+      do {
+        const int l = __ffsll((long long)m) - 1;
+        m &= m - 1ull;
+        const uint32_t il = (uint32_t)__builtin_amdgcn_readlane((int)i, l);
+        const uint32_t bit = (slut[(1 + t) * LUT_WORDS + (il >> 5)] >> (il & 31)) & 1u;
+        if (lane == l) (t ? crc[p] : cbc[p]) = bit;
+      } while (m);
+    }
   }
 }
 
@@ -527,7 +547,8 @@ __device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int
     if (__ballot(r[0].cc | r[1].cc)) {
       uint32_t cbc[2][4], crc[2][4];
 #pragma unroll
-      for (int dy = 0; dy < 2; dy++) chroma_fix<RGB>(w[it][dy][0], w[it][dy][1], w[it][dy][2], lut, cbc[dy], crc[dy]);
+      for (int dy = 0; dy < 2; dy++)
+        chroma_fix<RGB, GLOBAL_LUT>(w[it][dy][0], w[it][dy][1], w[it][dy][2], lut, cbc[dy], crc[dy], c4 | (pr << 5));
       const uint32_t nb0 = cbc[0][0] + cbc[0][1] + cbc[1][0] + cbc[1][1];
       const uint32_t nb1 = cbc[0][2] + cbc[0][3] + cbc[1][2] + cbc[1][3];
       const uint32_t nr0 = crc[0][0] + crc[0][1] + crc[1][0] + crc[1][1];
