@@ -153,7 +153,8 @@ constexpr int K1F_NO_LUT = 1, K1F_NO_REPLAY = 2, K1F_NO_COLOUR = 4, K1F_NO_DCT =
               K1F_NO_STORE = 16, K1F_NO_QUANT = 32, K1F_NO_MFMA = 64,
               K1F_LINEAR_STORE = 128, K1F_PLAIN_STORE = 256,
               K1F_NO_HIST = 512, K1F_NO_TOKSTORE = 1024,
-              K1F_EXTRA_LDS = 2048, K1F_NO_EMIT = 4096, K1F_NO_ACLOOP = 8192;
+              K1F_EXTRA_LDS = 2048, K1F_NO_EMIT = 4096, K1F_NO_ACLOOP = 8192,
+              K1F_NO_DMAWAIT = 16384;
 
 struct EntArgs {
   Geom g;

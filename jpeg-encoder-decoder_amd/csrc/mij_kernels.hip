@@ -1091,7 +1091,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
           }
           // token variants: the next tile's DMA has landed before the first
           // store (their VMEM count per tile varies)
-          if (nt == 0 && !DEFER) dma_wait();
+          if (nt == 0 && !DEFER && !(kflags & K1F_NO_DMAWAIT)) dma_wait();
           finish(nt, o);
         }
       } else if (!PIX) {
