@@ -1783,28 +1783,32 @@ __global__ __launch_bounds__(256) void k_pack(EntArgs a) {
 // ===========================================================================
 // k_pack_lb: segment bits, scan offsets and bit packing in one pass.  Each
 // workgroup takes the next pack group of PACK_SEGS segments of one scan (a
-// ticket keeps groups claimed in scan order), sums its segments' token bits,
-// and finds the group's start bit by decoupled look-back over the groups
-// before it in the same scan (per group: aggregate, then inclusive prefix,
-// published in one 64-bit word).  Then it packs as k_pack does: 16 lanes (a
-// DPP row) per segment place their tokens by a row scan of token bits and OR
-// the pieces into an LDS window.
+// ticket keeps groups claimed in scan order), merges each lane's tokens into
+// bit strings and sums its segments' bits, publishes the group's aggregate,
+// packs the group into an LDS window relative to its own first bit (16 lanes
+// -- a DPP row -- per segment place their strings by a row scan of their
+// lengths), and only then finds its start bit by decoupled look-back over the
+// groups before it in the same scan (per group: aggregate, then inclusive
+// prefix, published in one 64-bit word) -- by then those groups have
+// published, so the look-back rarely waits -- and stores the window shifted
+// into place.  Groups wider than one window (near worst-case entropy) take
+// the look-back first and pack window by window at absolute offsets.
 //
 // The scan buffers are all-zero when this kernel starts (k_emit_write zeroes
 // every word it consumes; the host clears them after the band paths), so a
 // group ORs its first and last word, which it may share with a neighbour
 // group, and stores its interior words plainly: no ordering between groups
-// beyond the prefix itself.  (Measured against this two-read form: staging a
-// group's tokens in LDS to read them once ran 1.72 ms instead of 1.31 ms per
-// config-3 step -- the 48 KB staging cut residency from 8 to 3 groups per CU,
-// and the kernel is latency-bound.)
+// beyond the prefix itself.  (Measured: staging a group's tokens in LDS to
+// read them once ran 1.72 ms instead of 1.31 ms per config-3 step -- the
+// 48 KB staging cut residency from 8 to 3 groups per CU, and the kernel is
+// latency-bound; look-back before packing: 0.94-0.97 ms against 0.92 here.)
 // ===========================================================================
 constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1;
 // k_pack_lb: a lane takes 4 consecutive tokens of a segment (one 16-byte
 // load), 16 lanes a segment, 64 tokens per row step; the first LB_STEPS steps
-// of each of a row's PACK_SEGS / 16 segments stay in registers from phase 1 to
-// phase 3 (tokens are read once unless a segment holds more than
-// 64 * LB_STEPS tokens)
+// of each of a row's PACK_SEGS / 16 segments are merged once in phase 1 and
+// kept in registers, as (64-bit string, length), until phase 3 places them
+// (measured: LB_STEPS = 2 spills; occupancy 6 beats 7 by 0.03 ms)
 constexpr int LB_SEGS_PER_ROW = 4;
 constexpr int LB_ROWS = PACK_SEGS / LB_SEGS_PER_ROW;   // 16-lane rows per workgroup
 constexpr int LB_THREADS = 16 * LB_ROWS;
@@ -1813,7 +1817,7 @@ constexpr int LB_VPL = PACK_SEGS / 64;                 // look-back scan: segmen
 #define MIJ_LB_STEPS 1
 #endif
 #ifndef MIJ_LB_OCC
-#define MIJ_LB_OCC 7
+#define MIJ_LB_OCC 6
 #endif
 constexpr int LB_STEPS = MIJ_LB_STEPS;
 static_assert(PACK_SEGS % 64 == 0 && LB_THREADS <= 1024, "k_pack_lb: 4 segments per 16-lane row");
@@ -1842,6 +1846,7 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
   __shared__ uint32_t tab[2 * 256];
   __shared__ uint32_t s_bits[PACK_SEGS], s_off[PACK_SEGS];
   __shared__ unsigned long long s_prefix;
+  __shared__ uint32_t s_total;
   __shared__ int s_ticket;
   const Geom &G = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1874,24 +1879,20 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
   const int s0 = q * PACK_SEGS, s1 = min(ns, s0 + PACK_SEGS), nsg = s1 - s0;
   const long long fs0 = (long long)f * G.nseg + sbase + s0;  // the group's first segment
   const int sub = tid & 15, row = tid >> 4;
-  // ---- 0. this row's segments: token counts, then their first LB_STEPS
-  // 64-token steps into registers (the loads overlap the table fill) --------
+  // ---- 0. this row's segments: token counts and their first 64-token step.
+  // The step-0 loads do not wait for the counts (a slot holds SEG_TOK tokens,
+  // so reading past a short segment stays inside it; lim masks the excess):
+  // one memory round trip instead of two before the tables are ready --------
   int nt[LB_SEGS_PER_ROW];
+  u4v tq[LB_SEGS_PER_ROW];
+  uint32_t t0w[LB_SEGS_PER_ROW];
 #pragma unroll
   for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
     const int sl = row + LB_ROWS * k;
-    nt[k] = sl < nsg ? min((int)a.seg_ntok[fs0 + sl], SEG_TOK) : 0;
-  }
-  u4v tq[LB_SEGS_PER_ROW][LB_STEPS];
-#pragma unroll
-  for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
-    const uint32_t *tk = a.tok + (fs0 + row + LB_ROWS * k) * SEG_TOK;
-#pragma unroll
-    for (int st = 0; st < LB_STEPS; st++) {
-      const int j = 64 * st + 4 * sub;
-      tq[k][st] = j < nt[k] ? *(const u4v *)(tk + j) : u4v{0u, 0u, 0u, 0u};
-    }
-    if (sub == 0 && nt[k] > 0) tq[k][0][0] = a.tok0[fs0 + row + LB_ROWS * k];  // token 0
+    const bool in = sl < nsg;  // row-uniform; no slot past the group's last segment
+    nt[k] = in ? (int)a.seg_ntok[fs0 + sl] : 0;
+    tq[k] = in ? *(const u4v *)(a.tok + (fs0 + sl) * SEG_TOK + 4 * sub) : u4v{0u, 0u, 0u, 0u};
+    t0w[k] = in && sub == 0 ? a.tok0[fs0 + sl] : 0u;  // token 0 (dense array)
   }
   for (int i = tid; i < 512; i += LB_THREADS) tab[i] = a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + i];
   __syncthreads();
@@ -1914,21 +1915,62 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
     const int j = i0 + 4 * sub;
     return j < nt[k] ? *(const u4v *)(tk + j) : u4v{0u, 0u, 0u, 0u};
   };
-  // ---- 1. bits of each segment ---------------------------------------------
+  // a step's 4 tokens merged into one left-growing bit string (ZRLs first,
+  // encoder.c:490-494), and its length; garbage but flagged when > 64 bits
+  auto merge_step = [&](const u4v &t, int lim, unsigned long long &acc) -> uint32_t {
+    uint32_t nb = 0;
+    acc = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      uint32_t code;
+      uint32_t L = lb_tok_code(tab, t[e], code);
+      uint32_t nzr = (t[e] >> 8) & 3u;
+      if (e >= lim) L = nzr = code = 0u;
+      for (uint32_t z = nzr; z; z--) acc = (acc << Lz) | zcode;
+      acc = (acc << L) | code;
+      nb += L + nzr * Lz;
+    }
+    return nb;
+  };
+  // ---- 1. bits of each segment.  The register steps are merged here, once
+  // (phase 3 only places them): step 0 of the four segments, then step 1,
+  // whose loads go out once the counts are known -------------------------------
+  unsigned long long pacc[LB_SEGS_PER_ROW][LB_STEPS];
+  uint32_t pnb[LB_SEGS_PER_ROW][LB_STEPS];
+  uint32_t bsum[LB_SEGS_PER_ROW];
+#pragma unroll
+  for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
+    nt[k] = min(nt[k], SEG_TOK);
+    if (sub == 0 && nt[k] > 0) tq[k][0] = t0w[k];
+    pnb[k][0] = merge_step(tq[k], nt[k] - 4 * sub, pacc[k][0]);
+    bsum[k] = pnb[k][0];
+  }
+#pragma unroll
+  for (int st = 1; st < LB_STEPS; st++) {
+    // (compiler fence: the loads must not be hoisted above the step-0 merges,
+    // or both steps' tokens are live at once)
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < LB_SEGS_PER_ROW; k++) tq[k] = load_step(k, 64 * st);
+#pragma unroll
+    for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
+      pnb[k][st] = merge_step(tq[k], nt[k] - 64 * st - 4 * sub, pacc[k][st]);
+      bsum[k] += pnb[k][st];
+    }
+  }
 #pragma unroll
   for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
     const int sl = row + LB_ROWS * k;
     if (sl >= nsg) break;  // row-uniform
-    uint32_t b = 0;
-#pragma unroll
-    for (int st = 0; st < LB_STEPS; st++) b += step_bits(tq[k][st], nt[k] - 64 * st - 4 * sub);
+    uint32_t b = bsum[k];
     for (int i0 = 64 * LB_STEPS; i0 < nt[k]; i0 += 64) b += step_bits(load_step(k, i0), nt[k] - i0 - 4 * sub);
     b = row_scan16(b);
     if (sub == 15) s_bits[sl] = b;
   }
   __syncthreads();
   LB_STAMP(1);
-  // ---- 2. offsets inside the group, group total, look-back -----------------
+  // ---- 2. offsets inside the group and its total; the aggregate goes out
+  // at once, so later groups' look-backs need not wait for this one's packing
   if (wave == 0) {
     uint32_t vv[LB_VPL], v = 0;
 #pragma unroll
@@ -1943,12 +1985,22 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
       if (lane * LB_VPL + i < nsg) s_off[lane * LB_VPL + i] = run;
       run += vv[i];
     }
-    const unsigned long long T = __shfl(incl, 63);
+    const uint32_t T = __shfl(incl, 63);
+    if (lane == 0) {
+      s_total = T;
+      if (q > 0) __hip_atomic_store(&a.pack_state[gid], LB_AGG | T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  const uint32_t gbits = s_total;
+  // the group's first bit in its scan: decoupled look-back over the groups
+  // before it (wave 0; publishes this group's inclusive prefix)
+  auto look_back = [&]() {
+    if (wave != 0) return;
     const unsigned long long base = a.bit_base ? a.bit_base[f * 4 + comp] : 0u;
     unsigned long long *stt = a.pack_state;
     unsigned long long prefix = base;
     if (q > 0) {
-      if (lane == 0) __hip_atomic_store(&stt[gid], LB_AGG | T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       prefix = 0;
       long long j = gid - 1;
       while (true) {
@@ -1970,40 +2022,47 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
       }
     }
     if (lane == 0) {
-      __hip_atomic_store(&stt[gid], LB_INC | (prefix + T), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (q == nq - 1) a.scan_bits[f * 3 + comp] = prefix + T;
+      __hip_atomic_store(&stt[gid], LB_INC | (prefix + gbits), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (q == nq - 1) a.scan_bits[f * 3 + comp] = prefix + gbits;
       s_prefix = prefix;
     }
+  };
+  // ---- 3. pack the group's tokens.  A group that fits one LDS window (all
+  // but near worst-case entropy) is placed relative to its own first bit and
+  // shifted into place as it is stored, so its look-back runs after the
+  // packing, when the groups before it have long published; a wider group
+  // takes its start bit first and packs window by window at absolute offsets.
+  uint32_t *raw_scan = a.raw + (long long)f * G.raw_fs +
+                       (comp == 0 ? 0 : G.raw_words[0] + (comp == 2 ? G.raw_words[1] : 0));
+  const bool rel = ((gbits + 31) >> 5) + 1 <= (uint32_t)PACK_WORDS;
+  // the group's words in the scan: [first, first + n)
+  auto group_words = [&](unsigned long long gbase, uint32_t &n) -> unsigned long long {
+    n = (uint32_t)(((gbase & 31) + gbits + 31) >> 5);
+    if ((gbase >> 5) + n + 1 > (unsigned long long)G.raw_words[comp]) {  // cannot happen for valid
+      if (tid == 0) a.err[f] = 2;                                         // tokens; never write OOB
+      n = 0;
+    }
+    return gbase >> 5;
+  };
+  uint32_t boff = 0, nw = ((gbits + 31) >> 5) + 1;  // relative: one spare word for the shift
+  unsigned long long gw = 0;
+  if (!rel) {
+    look_back();
+    __syncthreads();
+    boff = (uint32_t)(s_prefix & 31);
+    gw = group_words(s_prefix, nw);
   }
-  __syncthreads();
   LB_STAMP(2);
-  // ---- 3. pack the group's tokens ------------------------------------------
-  const unsigned long long gbase = s_prefix;
-  const uint32_t bit0 = (uint32_t)(gbase & 31);
-  const unsigned long long gbits = (unsigned long long)(nsg ? s_off[nsg - 1] + s_bits[nsg - 1] : 0u);
-  uint32_t nw = (uint32_t)((bit0 + gbits + 31) >> 5);  // words of the group
-  if ((gbase >> 5) + nw + 1 > (unsigned long long)G.raw_words[comp]) {  // cannot happen for valid
-    if (tid == 0) a.err[f] = 2;                                          // tokens; never write OOB
-    nw = 0;
-  }
-  uint32_t *raw = a.raw + (long long)f * G.raw_fs +
-                  (comp == 0 ? 0 : G.raw_words[0] + (comp == 2 ? G.raw_words[1] : 0)) + (gbase >> 5);
   for (uint32_t w0 = 0; w0 < nw; w0 += PACK_WORDS) {
     const uint32_t wn = min((uint32_t)PACK_WORDS, nw - w0);
     const uint32_t lo_bit = w0 * 32, hi_bit = (w0 + wn) * 32;
     for (uint32_t i = tid; i < wn; i += LB_THREADS) buf[i] = 0;
     __syncthreads();
-    // one window covers the group (all but near worst-case entropy): lanes
-    // merge their 4 tokens in a 64-bit register and OR it in with <= 3 LDS
-    // atomics.  A smaller window, or a lane whose 4 tokens exceed 64 bits,
-    // goes token by token in a second pass that reloads the tokens.
+    // lanes merged their 4 tokens of a register step into a 64-bit string in
+    // phase 1 and OR it in with <= 3 LDS atomics.  A narrower window, or a
+    // lane whose 4 tokens exceed 64 bits, goes token by token in a second
+    // pass that reloads the tokens.
     const bool whole = w0 == 0 && wn == nw;
-    // (tokens opaque here: otherwise the compiler hoists their per-token table
-    // addresses and masks out of the window loop and keeps them all live)
-#pragma unroll
-    for (int k = 0; k < LB_SEGS_PER_ROW; k++)
-#pragma unroll
-      for (int st = 0; st < LB_STEPS; st++) asm volatile("" : "+v"(tq[k][st]));
     auto decode = [&](const u4v &t, int lim, uint32_t (&L)[4], uint32_t (&code)[4], uint32_t (&nzr)[4]) {
       uint32_t nb = 0;
 #pragma unroll
@@ -2016,7 +2075,8 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
       return nb;
     };
     bool slow = !whole;
-    // one 64-token step of a row: positions, then the lane's merged bits
+    // one 64-token step of a row past the registers: positions, then the
+    // lane's merged bits
     auto fast_step = [&](const u4v &t, int lim, uint32_t &pos0) {
       uint32_t L[4], code[4], nzr[4];
       const uint32_t nb = decode(t, lim, L, code, nzr);
@@ -2035,16 +2095,24 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
         put_bits64(buf, pos, acc << (64 - nb), nb);
       }
     };
+    // the same for a step merged in phase 1
+    auto placed_step = [&](unsigned long long acc, uint32_t nb, uint32_t &pos0) {
+      const uint32_t x = row_scan16(nb);
+      const uint32_t pos = pos0 + x - nb;
+      pos0 += row_last(x);
+      if (nb > 64) slow = true;
+      else if (nb) put_bits64(buf, pos, acc << (64 - nb), nb);
+    };
     if (whole) {
 #pragma unroll
       for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
         const int sl = row + LB_ROWS * k;
         if (sl >= nsg) break;  // row-uniform
-        uint32_t pos0 = bit0 + s_off[sl];
+        uint32_t pos0 = boff + s_off[sl];
 #pragma unroll
         for (int st = 0; st < LB_STEPS; st++) {
           if (64 * st >= nt[k]) break;  // row-uniform
-          fast_step(tq[k][st], nt[k] - 64 * st - 4 * sub, pos0);
+          placed_step(pacc[k][st], pnb[k][st], pos0);
         }
         for (int i0 = 64 * LB_STEPS; i0 < nt[k]; i0 += 64) fast_step(load_step(k, i0), nt[k] - i0 - 4 * sub, pos0);
       }
@@ -2053,7 +2121,7 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
       for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
         const int sl = row + LB_ROWS * k;
         if (sl >= nsg) break;  // row-uniform
-        uint32_t pos0 = bit0 + s_off[sl];
+        uint32_t pos0 = boff + s_off[sl];
         if (pos0 >= hi_bit || pos0 + s_bits[sl] <= lo_bit) continue;  // row-uniform
         const uint32_t *tk = a.tok + (fs0 + sl) * SEG_TOK;
         for (int i0 = 0; i0 < nt[k]; i0 += 64) {
@@ -2078,12 +2146,27 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
         }
       }
     }
-    __syncthreads();
-    // the edge words may be shared with the neighbouring groups: OR (onto zero)
-    for (uint32_t i = tid; i < wn; i += LB_THREADS) {
-      const uint32_t wi = w0 + i;
-      if (wi == 0 || wi == nw - 1) atomicOr(&raw[wi], buf[i]);
-      else raw[wi] = buf[i];
+    if (rel) {  // the start bit now, then the words shifted into place
+      look_back();
+      __syncthreads();
+      uint32_t n;
+      gw = group_words(s_prefix, n);
+      const uint32_t sh = (uint32_t)(s_prefix & 31);
+      uint32_t *raw = raw_scan + gw;
+      // the edge words may be shared with the neighbouring groups: OR (onto zero)
+      for (uint32_t i = tid; i < n; i += LB_THREADS) {
+        const uint32_t v = __builtin_amdgcn_alignbit(i ? buf[i - 1] : 0u, buf[i], sh);
+        if (i == 0 || i == n - 1) atomicOr(&raw[i], v);
+        else raw[i] = v;
+      }
+    } else {
+      __syncthreads();
+      uint32_t *raw = raw_scan + gw;
+      for (uint32_t i = tid; i < wn; i += LB_THREADS) {
+        const uint32_t wi = w0 + i;
+        if (wi == 0 || wi == nw - 1) atomicOr(&raw[wi], buf[i]);
+        else raw[wi] = buf[i];
+      }
     }
     __syncthreads();
   }
