@@ -139,7 +139,7 @@ def run_config4(args, world, rank, local, dist):
     verified = 0
     if rank == 0 and args.verify:
         import oracle as O
-        for f in range(min(args.verify, n)):
+        for f in range(n if args.verify < 0 else min(args.verify, n)):
             if full.output(f) != O.cref_encode(frames[f % distinct], args.quality):
                 raise SystemExit(f"bench config4: frame {f} differs from the oracle")
             verified += 1

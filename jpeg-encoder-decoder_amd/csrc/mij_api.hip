@@ -32,6 +32,8 @@ hipError_t launch_pack(const EntArgs &a, hipStream_t s);
 hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s);
 hipError_t launch_emit(const EntArgs &a, hipStream_t s);
 hipError_t launch_or_words(uint32_t *dst, const uint32_t *src, long long n, hipStream_t s);
+hipError_t launch_move_pieces(uint32_t *raw, const Geom &g, uint32_t *dst,
+                              const unsigned long long *d_pieces, int npieces, long long max_words, hipStream_t s);
 hipError_t launch_or_pieces(uint32_t *raw, const Geom &g, const uint32_t *src,
                             const unsigned long long *d_pieces, int npieces, long long max_words, hipStream_t s);
 hipError_t launch_gather_regions(uint8_t *dst, long long slot_bytes, int pitch, const uint8_t *src,
@@ -356,7 +358,7 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
     HIP_TRY(dalloc(&b->d_seg_off, F * g.nseg));
     HIP_TRY(dalloc(&b->d_fix, F * g.nblk));
     HIP_TRY(dalloc(&b->d_pack_state, F * ((g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((g.nsc + PACK_SEGS - 1) / PACK_SEGS))));
-    HIP_TRY(dalloc(&b->d_pack_ticket, 1));
+    HIP_TRY(dalloc(&b->d_pack_ticket, F * 3));  // one per scan
     HIP_TRY(dalloc(&b->d_fix_count, 1));
     HIP_TRY(dalloc(&b->d_regions, F));
   }
@@ -1177,13 +1179,16 @@ extern "C" int mij_band_analyze(mij_batch *b, int n, int16_t *last_dc) {
   if (!last_dc) return fail(MIJ_EINVAL, "band_analyze: null last_dc");
   HIP_TRY(hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * n * 4 * 257, b->stream));
   HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * n, b->stream));
-  if (run_k1(b, n, 1) || run_k1(b, n, 6, 0)) return g_err;
+  // the fused K1: tokens and histograms straight from the pixels; each
+  // segment's first DC token waits for mij_band_histograms (k_seg_dc), which
+  // knows the band's predictors by then
+  if (run_k1(b, n, 2)) return g_err;
   const Geom &g = b->g;
   const long long last[3] = {g.nY - 1, g.nY + g.nC - 1, g.nY + 2LL * g.nC - 1};
-  for (int f = 0; f < n; f++)
-    for (int c = 0; c < 3; c++)
-      HIP_TRY(hipMemcpyAsync(last_dc + f * 3 + c, b->d_dc + (long long)f * g.nblk + last[c],
-                             sizeof(int16_t), hipMemcpyDeviceToHost, b->stream));
+  // every frame's last raw DC of a component: one strided copy per component
+  for (int c = 0; c < 3; c++)
+    HIP_TRY(hipMemcpy2DAsync(last_dc + c, 3 * sizeof(int16_t), b->d_dc + last[c], sizeof(int16_t) * g.nblk,
+                             sizeof(int16_t), n, hipMemcpyDeviceToHost, b->stream));
   HIP_TRY(hipStreamSynchronize(b->stream));
   return MIJ_OK;
 }
@@ -1241,9 +1246,11 @@ extern "C" int mij_band_pack(mij_batch *b, int n, const unsigned long long *bit_
   HIP_TRY(hipMemcpyAsync(b->d_bitbase, base.data(), sizeof(uint32_t) * n * 4, hipMemcpyHostToDevice,
                          b->stream));
   EntArgs a = ent_args(b, n);
-  b->raw_dirty = true;  // the band words stay in the scan buffers (no emit)
-  HIP_TRY(launch_scan(a, b->stream));
-  HIP_TRY(launch_pack(a, b->stream));
+  // k_pack_lb needs all-zero scan buffers: mij_band_words_all moves the band
+  // words out and zeroes them; a band packed but never moved leaves them dirty
+  if (b->raw_dirty) HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->cap * b->g.raw_fs, b->stream));
+  b->raw_dirty = true;
+  HIP_TRY(launch_pack_lb(a, b->stream));
   std::vector<unsigned long long> tot((size_t)n * 3);
   HIP_TRY(hipMemcpyAsync(tot.data(), b->d_scan_bits, sizeof(uint64_t) * n * 3,
                          hipMemcpyDeviceToHost, b->stream));
@@ -1281,17 +1288,46 @@ extern "C" int mij_band_words_all(mij_batch *b, int n, void *dst, size_t cap_wor
   unsigned long long total = 0;
   for (int i = 0; i < 3 * n; i++) total += b->band_words[i];
   if (cap_words < total) return fail(MIJ_ENOSPC, "band_words_all: need %llu words", total);
-  // (frame, comp) order, one stream-ordered copy each, one synchronisation
-  uint8_t *d = (uint8_t *)dst;
-  for (int f = 0; f < n; f++)
-    for (int c = 0; c < 3; c++) {
-      const unsigned long long nw = b->band_words[f * 3 + c];
-      if (nw)
-        HIP_TRY(hipMemcpyAsync(d, scan_words(b, f, c), nw * 4,
-                               dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, b->stream));
-      d += nw * 4;
+  // (frame, comp) order, moved (and zeroed behind) in one launch, then one
+  // copy to a host destination, one synchronisation
+  HIP_TRY(hipSetDevice(b->dev));
+  std::vector<unsigned long long> pcs;
+  long long max_words = 0;
+  unsigned long long at = 0;
+  for (int i = 0; i < 3 * n; i++) {
+    const unsigned long long nw = b->band_words[i];
+    if (nw) pcs.insert(pcs.end(), {(unsigned long long)i, nw, at});
+    max_words = std::max(max_words, (long long)nw);
+    at += nw;
+  }
+  const int np = (int)(pcs.size() / 3);
+  uint32_t *d = (uint32_t *)dst;
+  if (!dst_on_device && total) {
+    if (b->stage_words < total) {
+      if (b->d_stage) HIP_TRY(hipFree(b->d_stage));
+      b->d_stage = nullptr;
+      HIP_TRY(dalloc(&b->d_stage, total));
+      b->stage_words = total;
     }
+    d = b->d_stage;
+  }
+  if (np) {
+    if (b->pieces_cap < (size_t)np) {
+      if (b->d_pieces) HIP_TRY(hipFree(b->d_pieces));
+      b->d_pieces = nullptr;
+      HIP_TRY(dalloc(&b->d_pieces, (size_t)np * 4));
+      b->pieces_cap = (size_t)np;
+    }
+    HIP_TRY(hipMemcpyAsync(b->d_pieces, pcs.data(), sizeof(unsigned long long) * pcs.size(), hipMemcpyHostToDevice,
+                           b->stream));
+    HIP_TRY(launch_move_pieces(b->d_raw, b->g, d, b->d_pieces, np, max_words, b->stream));
+  }
+  if (!dst_on_device && total)
+    HIP_TRY(hipMemcpyAsync(dst, d, total * 4, hipMemcpyDeviceToHost, b->stream));
   HIP_TRY(hipStreamSynchronize(b->stream));
+  // every word mij_band_pack wrote has left the buffers (a scan's words,
+  // its in-word start offset included, are its band_words)
+  b->raw_dirty = false;
   return MIJ_OK;
 }
 

@@ -181,7 +181,7 @@ struct EntArgs {
   uint32_t *ffc;            // per frame [3][emit_chunks]: 0xFF bytes per EMIT_CH chunk
   uint32_t *choff;          // per frame [3][emit_chunks]: output offset of each chunk
   unsigned long long *pack_state;  // k_pack_lb: per pack group, flag << 62 | bits
-  unsigned int *pack_ticket;       // k_pack_lb: next group to claim
+  unsigned int *pack_ticket;       // k_pack_lb: next group to claim, per scan
   unsigned long long *dbg;         // diagnostics only (MIJ_PACK_TIME, diag build)
   const int2 *fdims;               // per-frame image size (region batches), null: the canvas
   int seg_dc;                      // k_tables: compute the segment-first DC tokens first (k_seg_dc)

@@ -1808,7 +1808,9 @@ constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = 
 // load), 16 lanes a segment, 64 tokens per row step; the first LB_STEPS steps
 // of each of a row's PACK_SEGS / 16 segments are merged once in phase 1 and
 // kept in registers, as (64-bit string, length), until phase 3 places them
-// (measured: LB_STEPS = 2 spills; occupancy 6 beats 7 by 0.03 ms)
+// (measured on config 3, where luma segments hold ~138 tokens and chroma ones
+// ~16: LB_STEPS = 3 at occupancy 4 or 5, 0.96 ms, and 2 at 5, 0.92, against
+// 1 at occupancy 6, 0.92; occupancy 6 beats 7 by 0.03 ms)
 constexpr int LB_SEGS_PER_ROW = 4;
 constexpr int LB_ROWS = PACK_SEGS / LB_SEGS_PER_ROW;   // 16-lane rows per workgroup
 constexpr int LB_THREADS = 16 * LB_ROWS;
@@ -1816,10 +1818,14 @@ constexpr int LB_VPL = PACK_SEGS / 64;                 // look-back scan: segmen
 #ifndef MIJ_LB_STEPS
 #define MIJ_LB_STEPS 1
 #endif
+#ifndef MIJ_LB_STEPS_C
+#define MIJ_LB_STEPS_C 1
+#endif
 #ifndef MIJ_LB_OCC
 #define MIJ_LB_OCC 6
 #endif
-constexpr int LB_STEPS = MIJ_LB_STEPS;
+constexpr int LB_STEPS = MIJ_LB_STEPS, LB_STEPS_C = MIJ_LB_STEPS_C;
+static_assert(LB_STEPS_C <= LB_STEPS && 64 * LB_STEPS <= SEG_TOK, "k_pack_lb: register steps inside a slot");
 static_assert(PACK_SEGS % 64 == 0 && LB_THREADS <= 1024, "k_pack_lb: 4 segments per 16-lane row");
 
 // bits of a token (encoder.c:434-460, ZRLs :490-494); tab = [DC | AC][256]
@@ -1857,47 +1863,32 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
 #define LB_STAMP(k)
 #endif
   LB_STAMP(0);
-  if (tid == 0) s_ticket = (int)atomicAdd(a.pack_ticket, 1u);
-  __syncthreads();
-  const int gid = s_ticket;  // groups in (frame, scan, q) order
   const int gy = (G.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (G.nsc + PACK_SEGS - 1) / PACK_SEGS;
   const int gpf = gy + 2 * gc;
-  const int f = gid / gpf;
-  int q = gid - f * gpf, comp, sbase, ns;
-  if (q < gy) {
-    comp = 0; sbase = 0; ns = G.nsy;
-  } else {
-    q -= gy;
-    comp = 1 + (q >= gc);
-    if (q >= gc) q -= gc;
-    sbase = comp == 1 ? G.nsy : G.nsy + G.nsc;
-    ns = G.nsc;
-  }
+  // The workgroup's scan follows from its index; its group inside the scan
+  // from the scan's own ticket, so that groups are claimed in scan order (a
+  // group's look-back only waits on groups that have started) without one
+  // counter for the whole launch.  (Measured: one launch-wide ticket 0.92 ms,
+  // per-scan tickets 0.89, dispatch order without a ticket 0.84 -- not safe
+  // by the ISA's guarantees; loading the group dispatch order suggests while
+  // the ticket is in flight: the tickets of a scan arrive out of dispatch
+  // order across the XCDs, so most groups redid their loads, 1.08 ms.)
+  const int f = blockIdx.x / gpf, bq = blockIdx.x - f * gpf;
+  const int comp = bq < gy ? 0 : (bq < gy + gc ? 1 : 2);
+  const int sbase = comp == 0 ? 0 : (comp == 1 ? G.nsy : G.nsy + G.nsc), ns = comp == 0 ? G.nsy : G.nsc;
+  const int gscan0 = f * gpf + (comp == 0 ? 0 : gy + (comp == 2 ? gc : 0));  // the scan's first group
   const int nq = comp == 0 ? gy : gc;
-  const int gscan0 = gid - q;  // ticket of the scan's first group
-  const int chroma = comp != 0;
-  const int s0 = q * PACK_SEGS, s1 = min(ns, s0 + PACK_SEGS), nsg = s1 - s0;
-  const long long fs0 = (long long)f * G.nseg + sbase + s0;  // the group's first segment
-  const int sub = tid & 15, row = tid >> 4;
-  // ---- 0. this row's segments: token counts and their first 64-token step.
-  // The step-0 loads do not wait for the counts (a slot holds SEG_TOK tokens,
-  // so reading past a short segment stays inside it; lim masks the excess):
-  // one memory round trip instead of two before the tables are ready --------
-  int nt[LB_SEGS_PER_ROW];
-  u4v tq[LB_SEGS_PER_ROW];
-  uint32_t t0w[LB_SEGS_PER_ROW];
-#pragma unroll
-  for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
-    const int sl = row + LB_ROWS * k;
-    const bool in = sl < nsg;  // row-uniform; no slot past the group's last segment
-    nt[k] = in ? (int)a.seg_ntok[fs0 + sl] : 0;
-    tq[k] = in ? *(const u4v *)(a.tok + (fs0 + sl) * SEG_TOK + 4 * sub) : u4v{0u, 0u, 0u, 0u};
-    t0w[k] = in && sub == 0 ? a.tok0[fs0 + sl] : 0u;  // token 0 (dense array)
-  }
-  for (int i = tid; i < 512; i += LB_THREADS) tab[i] = a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + i];
+  if (tid == 0) s_ticket = (int)atomicAdd(&a.pack_ticket[f * 3 + comp], 1u);
   __syncthreads();
-  const uint32_t zac = tab[256 + 0xF0];
-  const uint32_t Lz = zac >> 16, zcode = zac & 0xFFFFu;
+  const int q = s_ticket;
+  const int gid = gscan0 + q;
+  const int chroma = comp != 0;
+  const int sub = tid & 15, row = tid >> 4;
+  const int nst = chroma ? LB_STEPS_C : LB_STEPS;  // register steps of this scan
+  const int s0 = q * PACK_SEGS, nsg = min(ns, s0 + PACK_SEGS) - s0;
+  const long long fs0 = (long long)f * G.nseg + sbase + s0;  // the group's first segment
+  int nt[LB_SEGS_PER_ROW];
+  uint32_t Lz = 0, zcode = 0;
   // a step's 4 tokens (those below lim = tokens left - 4 * sub): bits, ZRLs included
   auto step_bits = [&](const u4v &t, int lim) -> uint32_t {
     uint32_t b = 0;
@@ -1932,40 +1923,52 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
     }
     return nb;
   };
-  // ---- 1. bits of each segment.  The register steps are merged here, once
-  // (phase 3 only places them): step 0 of the four segments, then step 1,
-  // whose loads go out once the counts are known -------------------------------
   unsigned long long pacc[LB_SEGS_PER_ROW][LB_STEPS];
   uint32_t pnb[LB_SEGS_PER_ROW][LB_STEPS];
-  uint32_t bsum[LB_SEGS_PER_ROW];
-#pragma unroll
-  for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
-    nt[k] = min(nt[k], SEG_TOK);
-    if (sub == 0 && nt[k] > 0) tq[k][0] = t0w[k];
-    pnb[k][0] = merge_step(tq[k], nt[k] - 4 * sub, pacc[k][0]);
-    bsum[k] = pnb[k][0];
-  }
-#pragma unroll
-  for (int st = 1; st < LB_STEPS; st++) {
-    // (compiler fence: the loads must not be hoisted above the step-0 merges,
-    // or both steps' tokens are live at once)
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int k = 0; k < LB_SEGS_PER_ROW; k++) tq[k] = load_step(k, 64 * st);
-#pragma unroll
-    for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
-      pnb[k][st] = merge_step(tq[k], nt[k] - 64 * st - 4 * sub, pacc[k][st]);
-      bsum[k] += pnb[k][st];
-    }
-  }
+  // ---- 0. this row's segments: token counts and their first register steps
+  // (LB_STEPS 64-token steps of a luma segment, LB_STEPS_C of a chroma one),
+  // all loads at once: none waits for the counts (a slot holds SEG_TOK
+  // tokens, so reading past a short segment stays inside it; lim masks the
+  // excess) -- one memory round trip before the tables are ready ------------
+  u4v tq[LB_SEGS_PER_ROW][LB_STEPS];
+  uint32_t t0w[LB_SEGS_PER_ROW];
 #pragma unroll
   for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
     const int sl = row + LB_ROWS * k;
-    if (sl >= nsg) break;  // row-uniform
-    uint32_t b = bsum[k];
-    for (int i0 = 64 * LB_STEPS; i0 < nt[k]; i0 += 64) b += step_bits(load_step(k, i0), nt[k] - i0 - 4 * sub);
-    b = row_scan16(b);
-    if (sub == 15) s_bits[sl] = b;
+    const bool in = sl < nsg;  // row-uniform; no slot past the group's last segment
+    nt[k] = in ? (int)a.seg_ntok[fs0 + sl] : 0;
+#pragma unroll
+    for (int st = 0; st < LB_STEPS; st++)
+      tq[k][st] = in && st < nst ? *(const u4v *)(a.tok + (fs0 + sl) * SEG_TOK + 64 * st + 4 * sub)
+                                 : u4v{0u, 0u, 0u, 0u};
+    t0w[k] = in && sub == 0 ? a.tok0[fs0 + sl] : 0u;  // token 0 (dense array)
+  }
+  for (int i = tid; i < 512; i += LB_THREADS) tab[i] = a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + i];
+  __syncthreads();
+  {
+    const uint32_t zac = tab[256 + 0xF0];
+    Lz = zac >> 16;
+    zcode = zac & 0xFFFFu;
+  }
+  // ---- 1. bits of each segment.  The register steps are merged here, once
+  // (phase 3 only places them); steps past them are read twice ---------------
+#pragma unroll
+  for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
+    nt[k] = min(nt[k], SEG_TOK);
+    if (sub == 0 && nt[k] > 0) tq[k][0][0] = t0w[k];
+    uint32_t b = 0;
+#pragma unroll
+    for (int st = 0; st < LB_STEPS; st++) {
+      pacc[k][st] = 0;
+      pnb[k][st] = st < nst ? merge_step(tq[k][st], nt[k] - 64 * st - 4 * sub, pacc[k][st]) : 0u;
+      b += pnb[k][st];
+    }
+    const int sl = row + LB_ROWS * k;
+    if (sl < nsg) {  // row-uniform
+      for (int i0 = 64 * nst; i0 < nt[k]; i0 += 64) b += step_bits(load_step(k, i0), nt[k] - i0 - 4 * sub);
+      b = row_scan16(b);
+      if (sub == 15) s_bits[sl] = b;
+    }
   }
   __syncthreads();
   LB_STAMP(1);
@@ -2111,10 +2114,10 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
         uint32_t pos0 = boff + s_off[sl];
 #pragma unroll
         for (int st = 0; st < LB_STEPS; st++) {
-          if (64 * st >= nt[k]) break;  // row-uniform
+          if (st >= nst || 64 * st >= nt[k]) break;  // row-uniform
           placed_step(pacc[k][st], pnb[k][st], pos0);
         }
-        for (int i0 = 64 * LB_STEPS; i0 < nt[k]; i0 += 64) fast_step(load_step(k, i0), nt[k] - i0 - 4 * sub, pos0);
+        for (int i0 = 64 * nst; i0 < nt[k]; i0 += 64) fast_step(load_step(k, i0), nt[k] - i0 - 4 * sub, pos0);
       }
     }
     if (__ballot(slow)) {  // second pass over this wave's rows, tokens reloaded
@@ -2261,36 +2264,48 @@ __global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
   uint8_t *out = a.out + (long long)f * a.g.out_cap;
   const HuffCode *hc = a.hc + (long long)f * 4;
   const long long nchmax = emit_chunks(a.g);
-  if (tid == 0) {
-    unsigned long long p = 0;
-    const uint8_t app0[20] = {0xFF, 0xD8, 0xFF, 0xE0, 0x00, 0x10, 0x4A, 0x46, 0x49, 0x46,
-                              0x00, 0x01, 0x01, 0x00, 0x00, 0x48, 0x00, 0x48, 0x00, 0x00};
-    for (int i = 0; i < 20; i++) out[p++] = app0[i];
-    for (int t = 0; t < 2; t++) {
-      out[p++] = 0xFF; out[p++] = 0xDB; out[p++] = 0x00; out[p++] = 0x43; out[p++] = (uint8_t)t;
-      for (int i = 0; i < 64; i++) out[p++] = (uint8_t)a.tab->dqt[t][i];
-    }
-    const int tcth[4] = {0x00, 0x10, 0x01, 0x11};
-    for (int t = 0; t < 4; t++) {
-      int n = 0;
-      for (int i = 1; i <= 16; i++) n += hc[t].code_len_freq[i];
-      const int len = 19 + n;
-      out[p++] = 0xFF; out[p++] = 0xC4;
-      out[p++] = (uint8_t)(len >> 8); out[p++] = (uint8_t)len;
-      out[p++] = (uint8_t)tcth[t];
-      for (int i = 1; i <= 16; i++) out[p++] = (uint8_t)hc[t].code_len_freq[i];
-      for (int i = 0; i < n; i++) out[p++] = (uint8_t)hc[t].sym_sorted[i];
-    }
+  // headers, one byte per thread (a single thread's byte loop is a chain of
+  // dependent loads and stores: 40 us per launch): APP0 20 + DQT 2 x 69 +
+  // DHT 4 x (21 + n_t) + SOF0 19
+  __shared__ int s_n[4];
+  {
+    int hn = tid < 64 ? hc[tid >> 4].code_len_freq[1 + (tid & 15)] : 0;
+    for (int o = 8; o; o >>= 1) hn += __shfl_xor(hn, o);  // sums over 16 lanes
+    if (tid < 64 && (tid & 15) == 0) s_n[tid >> 4] = hn;
+  }
+  __syncthreads();
+  int doff[5];  // DHT t starts at doff[t]; SOF0 at doff[4]
+  doff[0] = 20 + 2 * 69;
+  for (int t = 0; t < 4; t++) doff[t + 1] = doff[t] + 21 + s_n[t];
+  const int hlen = doff[4] + 19;
+  {
     const FGeom fg = frame_geom(a.g, a.fdims, f);
     const int W = fg.w, H = fg.h;
-    const uint8_t sof[19] = {0xFF, 0xC0, 0x00, 0x11, 0x08, (uint8_t)(H >> 8), (uint8_t)H,
-                             (uint8_t)(W >> 8), (uint8_t)W, 0x03, 0x01, 0x22, 0x00,
-                             0x02, 0x11, 0x01, 0x03, 0x11, 0x01};
-    for (int i = 0; i < 19; i++) out[p++] = sof[i];
+    for (int i = tid; i < hlen; i += 256) {
+      uint8_t v;
+      if (i < 20) {
+        const uint8_t app0[20] = {0xFF, 0xD8, 0xFF, 0xE0, 0x00, 0x10, 0x4A, 0x46, 0x49, 0x46,
+                                  0x00, 0x01, 0x01, 0x00, 0x00, 0x48, 0x00, 0x48, 0x00, 0x00};
+        v = app0[i];
+      } else if (i < doff[0]) {  // DQT (encoder.c:559-571)
+        const int t = (i - 20) / 69, k = (i - 20) - 69 * t;
+        const uint8_t m[5] = {0xFF, 0xDB, 0x00, 0x43, (uint8_t)t};
+        v = k < 5 ? m[k] : (uint8_t)a.tab->dqt[t][k - 5];
+      } else if (i < doff[4]) {  // DHT (encoder.c:504-532)
+        const int t = i >= doff[3] ? 3 : i >= doff[2] ? 2 : i >= doff[1] ? 1 : 0;
+        const int k = i - doff[t], len = 19 + s_n[t];
+        const uint8_t m[5] = {0xFF, 0xC4, (uint8_t)(len >> 8), (uint8_t)len, (uint8_t)((t & 1) << 4 | (t >> 1))};
+        v = k < 5 ? m[k] : k < 21 ? (uint8_t)hc[t].code_len_freq[k - 4] : (uint8_t)hc[t].sym_sorted[k - 21];
+      } else {  // SOF0 (encoder.c:573-600)
+        const uint8_t sof[19] = {0xFF, 0xC0, 0x00, 0x11, 0x08, (uint8_t)(H >> 8), (uint8_t)H,
+                                 (uint8_t)(W >> 8), (uint8_t)W, 0x03, 0x01, 0x22, 0x00,
+                                 0x02, 0x11, 0x01, 0x03, 0x11, 0x01};
+        v = sof[i - doff[4]];
+      }
+      out[i] = v;
+    }
   }
-  // header length: APP0 20 + DQT 2 x 69 + DHT 4 x (21 + n) + SOF0 19
-  int hn = tid < 64 ? hc[tid >> 4].code_len_freq[1 + (tid & 15)] : 0;
-  unsigned long long pos = 20 + 2 * 69 + 19 + 4 * 21 + (unsigned long long)block_sum256(hn, red);
+  unsigned long long pos = (unsigned long long)hlen;
   for (int comp = 0; comp < 3; comp++) {
     if (tid == 0) {  // SOS (encoder.c:601-620)
       const uint8_t sos[10] = {0xFF, 0xDA, 0x00, 0x08, 0x01, (uint8_t)(comp + 1),
@@ -2474,6 +2489,21 @@ __global__ void k_or_pieces(uint32_t *raw, long long raw_fs, long long rw0, long
 }
 
 // ---- tiny self-test used by the test-suite: exact i8 MFMA layout check ----
+// Band words out of the scan buffers, zeroed behind them (k_pack_lb needs
+// all-zero buffers): piece blockIdx.y = {frame * 3 + scan, words, first
+// destination word}, from the start of the scan.
+__global__ void k_move_pieces(uint32_t *raw, long long raw_fs, long long rw0, long long rw1,
+                              uint32_t *dst, const unsigned long long *pieces) {
+  const unsigned long long *pc = pieces + 3 * (long long)blockIdx.y;
+  const long long fc = (long long)pc[0], n = (long long)pc[1];
+  const long long f = fc / 3, c = fc - 3 * f;
+  uint32_t *src = raw + f * raw_fs + (c == 0 ? 0 : rw0 + (c == 2 ? rw1 : 0));
+  uint32_t *dp = dst + (long long)pc[2];
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    dp[i] = src[i];
+    src[i] = 0u;
+  }
+}
 __global__ void k_mfma_probe(const int4 *A, const int4 *B, int4 *D) {
   const int lane = threadIdx.x;
   const int4 a4 = A[lane], b4 = B[lane];
@@ -2606,6 +2636,15 @@ hipError_t launch_or_pieces(uint32_t *raw, const Geom &g, const uint32_t *src,
   return hipGetLastError();
 }
 
+hipError_t launch_move_pieces(uint32_t *raw, const Geom &g, uint32_t *dst,
+                              const unsigned long long *d_pieces, int npieces, long long max_words, hipStream_t s) {
+  if (npieces <= 0 || max_words <= 0) return hipSuccess;
+  const long long chunks = (max_words + 1023) / 1024;
+  hipLaunchKernelGGL(k_move_pieces, dim3((unsigned)(chunks < 64 ? chunks : 64), (unsigned)npieces), dim3(256), 0, s,
+                     raw, g.raw_fs, g.raw_words[0], g.raw_words[1], dst, d_pieces);
+  return hipGetLastError();
+}
+
 hipError_t launch_pack(const EntArgs &a, hipStream_t s) {
   const int gy = (a.g.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (a.g.nsc + PACK_SEGS - 1) / PACK_SEGS;
   hipLaunchKernelGGL(k_pack, dim3(a.nframes * (gy + 2 * gc)), dim3(256), 0, s, a);
@@ -2615,7 +2654,7 @@ hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s) {
   const int gy = (a.g.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (a.g.nsc + PACK_SEGS - 1) / PACK_SEGS;
   const long long groups = (long long)a.nframes * (gy + 2 * gc);
   hipError_t e = hipMemsetAsync(a.pack_state, 0, sizeof(unsigned long long) * groups, s);
-  if (e == hipSuccess) e = hipMemsetAsync(a.pack_ticket, 0, sizeof(unsigned), s);
+  if (e == hipSuccess) e = hipMemsetAsync(a.pack_ticket, 0, sizeof(unsigned) * 3 * a.nframes, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_pack_lb, dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
   return hipGetLastError();
