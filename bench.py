@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1),
                     help="processes for the frame-parallel CPU baseline (the GPU box's CPU "
                          "share is 16 cores per GPU); 1 disables it")
+    ap.add_argument("--overlap", type=int, default=int(os.environ.get("MIJ_OVERLAP", "1")),
+                    help="fused pipeline in this many sub-batches, the entropy stages of one "
+                         "on a second stream beside K1 of the next (1: off)")
     ap.add_argument("--split", action="store_true",
                     help="split pipeline: K1 writes coefficient planes and a second pass "
                          "tokenizes them (default: fused, K1 emits the symbol tokens itself)")
@@ -619,6 +622,8 @@ def main():
     gpu = 0 if dist is not None and dist.get_backend() != "nccl" else local
     batch = mijpeg.Batch(W, H, F, args.quality, device=gpu)
     batch.set_split(args.split)
+    if args.overlap > 1:
+        batch.set_overlap(args.overlap)
     for i in range(F):
         batch.upload(frames[i % len(frames)], first=i)
     run = batch.encode if args.mode == "encode" else batch.dct

@@ -123,6 +123,11 @@ int mij_batch_encode(mij_batch *b, int nframes);     /* full path, async */
  * zigzag coefficient planes and a second pass tokenizes them.  Same output
  * bytes either way. */
 int mij_batch_set_split(mij_batch *b, int on);
+/* fused pipeline: encode in nsub sub-batches (1 = off, at most 16), the
+ * entropy stages of sub-batch k on a second stream behind K1 of sub-batch k,
+ * concurrent with K1 of sub-batch k + 1.  Same output bytes; stage timing
+ * then reports K1 over all sub-batches ([0]) and the whole encode ([7]). */
+int mij_batch_set_overlap(mij_batch *b, int nsub);
 /* input frames in R, G, B byte order (PPM files, brain.c:25-42) instead of the
  * encoder's B, G, R (encoder.c:133); the channels are swapped inside K1, at no
  * cost.  Both pipelines. */

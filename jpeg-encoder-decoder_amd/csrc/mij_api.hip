@@ -283,6 +283,10 @@ struct mij_batch {
   bool rgb = false;         // input frames in R, G, B byte order (PPM) instead of B, G, R
   bool split = false;       // true: K1 writes coefficients, a second pass tokenizes;
                             // false (default): K1 emits the tokens itself
+  // sub-batch overlap (mij_batch_set_overlap): entropy stages on stream2
+  int overlap = 1;
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ov_k1[16] = {}, ov_done = nullptr;
   bool timing = false;
   static constexpr int HIST = 64;
   hipEvent_t evh[HIST][MIJ_NSTAGES] = {};  // per-step events while timing is on
@@ -310,6 +314,13 @@ static void batch_free(mij_batch *b) {
   for (auto &row : b->evh)
     for (auto &e : row)
       if (e) hipEventDestroy(e);
+  for (auto &e : b->ov_k1)
+    if (e) hipEventDestroy(e);
+  if (b->ov_done) hipEventDestroy(b->ov_done);
+  if (b->stream2) {
+    hipStreamSynchronize(b->stream2);
+    hipStreamDestroy(b->stream2);
+  }
   if (b->stream) hipStreamDestroy(b->stream);
   delete b;
 }
@@ -461,7 +472,7 @@ extern "C" int mij_batch_set_input(mij_batch *b, const void *d_bgr, long long fr
   return MIJ_OK;
 }
 
-static EntArgs ent_args(mij_batch *b, int nframes) {
+static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0) {
   EntArgs a;
   memset(&a, 0, sizeof(a));
   a.g = b->g;
@@ -489,12 +500,39 @@ static EntArgs ent_args(mij_batch *b, int nframes) {
   a.pack_state = b->d_pack_state;
   a.pack_ticket = b->d_pack_ticket;
   a.fdims = b->use_fdims ? b->d_fdims : nullptr;
+  if (f0) {  // sub-batch: frames f0.. of the batch (every per-frame array shifted)
+    const Geom &g = b->g;
+    const long long F = f0, gpf = (g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((g.nsc + PACK_SEGS - 1) / PACK_SEGS);
+    a.coef += F * g.coef_fs;
+    a.dc += F * g.nblk;
+    a.hist += F * 4 * 257;
+    a.ehuf += F * 4 * 256;
+    a.tok += F * g.nseg * SEG_TOK;
+    a.tok0 += F * g.nseg;
+    a.seg_ntok += F * g.nseg;
+    a.seg_bits += F * g.nseg;
+    a.seg_off += F * g.nseg;
+    a.scan_bits += F * 3;
+    a.raw += F * g.raw_fs;
+    a.hc += F * 4;
+    a.out += F * g.out_cap;
+    a.out_len += F;
+    a.err += F;
+    a.dc_pred += F * 4;
+    a.bit_base += F * 4;
+    a.ffc += F * 3 * emit_chunks(g);
+    a.choff += F * 3 * emit_chunks(g);
+    a.pack_state += F * gpf;
+    a.pack_ticket += F * 3;
+    if (a.fdims) a.fdims += F;
+  }
   return a;
 }
 
 // mode: K1 mode bits (1 coefficient planes out, 2 tokens + histograms out,
 // 4 coefficient planes in)
-static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int seg_dc_inline = 0) {
+static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int seg_dc_inline = 0, int f0 = 0,
+                  bool stage_events = true) {
   K1Args k;
   memset(&k, 0, sizeof(k));
   k.in = b->d_in;
@@ -514,6 +552,18 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int se
   k.fix_count = b->d_fix_count;
   k.rgb = b->rgb && (mode & 4) == 0;  // pixel-input variants
   k.fdims = b->use_fdims ? b->d_fdims : nullptr;
+  if (f0) {  // sub-batch: frames f0.. (per-frame arrays shifted; mode 2 only)
+    const Geom &g = b->g;
+    const long long F = f0;
+    k.in += F * b->in_fs;
+    k.coef += F * g.coef_fs;
+    k.dc += F * g.nblk;
+    k.tok += F * g.nseg * SEG_TOK;
+    k.tok0 += F * g.nseg;
+    k.seg_ntok += F * g.nseg;
+    k.hist += F * 4 * 257;
+    if (k.fdims) k.fdims += F;
+  }
   static const int k1_flags = getenv("MIJ_K1_FLAGS") ? atoi(getenv("MIJ_K1_FLAGS")) : 0;
   k.flags = k1_flags;
   const long long ntiles = (long long)nframes * b->g.tiles_per_frame;
@@ -559,9 +609,9 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int se
     fprintf(stderr, "K1 waves %lld tiles %lld: span %.1f us, first end %.1f us, wave life mean %.1f min %.1f max %.1f us\n",
             n, tiles, (e1 - s0) / 100.0, (e0 - s0) / 100.0, sum / n / 100.0, smin / 100.0, smax / 100.0);
   }
-  if (b->timing && mode != 6) HIP_TRY(hipEventRecord(b->ev[1], b->stream));
+  if (b->timing && mode != 6 && stage_events) HIP_TRY(hipEventRecord(b->ev[1], b->stream));
   if (mode == 1) HIP_TRY(launch_fix_blocks(k, b->stream));
-  if (b->timing && mode != 6) HIP_TRY(hipEventRecord(b->ev[2], b->stream));
+  if (b->timing && mode != 6 && stage_events) HIP_TRY(hipEventRecord(b->ev[2], b->stream));
   return MIJ_OK;
 }
 
@@ -569,20 +619,22 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int se
 // must have been zeroed before K1).  dc_fix: the segments' first DC tokens
 // are still to compute (K1 from pixels); tables_given: the caller's huff_code
 // structs are already in d_hc and d_ehuf (drop-in write_jpg).
-static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given) {
-  EntArgs a = ent_args(b, nframes);
-  const bool t = b->timing;
+static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given, int f0 = 0,
+                       hipStream_t st = nullptr) {
+  EntArgs a = ent_args(b, nframes, f0);
+  const bool t = b->timing && !st;  // (sub-batches: no stage events)
+  if (!st) st = b->stream;
   // segment-first DC tokens: inside k_tables (its DC-table waves), or on
   // their own when the caller's tables are given
   static const int segdc_dbg = getenv("MIJ_SEGDC_DBG") ? atoi(getenv("MIJ_SEGDC_DBG")) : 0;  // diag build
   a.seg_dc = dc_fix && !tables_given ? 1 | segdc_dbg : 0;
-  if (dc_fix && tables_given) HIP_TRY(launch_seg_dc(a, b->stream));
-  if (t) HIP_TRY(hipEventRecord(b->ev[4], b->stream));
-  if (!tables_given) HIP_TRY(launch_tables(a, b->stream));
-  if (t) HIP_TRY(hipEventRecord(b->ev[5], b->stream));
+  if (dc_fix && tables_given) HIP_TRY(launch_seg_dc(a, st));
+  if (t) HIP_TRY(hipEventRecord(b->ev[4], st));
+  if (!tables_given) HIP_TRY(launch_tables(a, st));
+  if (t) HIP_TRY(hipEventRecord(b->ev[5], st));
   // segment bits, scan offsets and packing in one look-back pass
   if (b->raw_dirty) {
-    HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->cap * b->g.raw_fs, b->stream));
+    HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->cap * b->g.raw_fs, st));
     b->raw_dirty = false;
   }
   // diagnostics (MIJ_PACK_TIME with the diag build): per-group phase times of k_pack_lb
@@ -591,13 +643,13 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
                                                   2 * ((b->g.nsc + PACK_SEGS - 1) / PACK_SEGS));
   if (ptime) {
     HIP_TRY(hipMalloc(&a.dbg, sizeof(unsigned long long) * 4 * ngroups));
-    HIP_TRY(hipMemsetAsync(a.dbg, 0, sizeof(unsigned long long) * 4 * ngroups, b->stream));
+    HIP_TRY(hipMemsetAsync(a.dbg, 0, sizeof(unsigned long long) * 4 * ngroups, st));
   }
-  HIP_TRY(launch_pack_lb(a, b->stream));
+  HIP_TRY(launch_pack_lb(a, st));
   if (ptime) {
     std::vector<unsigned long long> h(4 * ngroups);
-    HIP_TRY(hipMemcpyAsync(h.data(), a.dbg, sizeof(unsigned long long) * 4 * ngroups, hipMemcpyDeviceToHost, b->stream));
-    HIP_TRY(hipStreamSynchronize(b->stream));
+    HIP_TRY(hipMemcpyAsync(h.data(), a.dbg, sizeof(unsigned long long) * 4 * ngroups, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
     HIP_TRY(hipFree(a.dbg));
     a.dbg = nullptr;
     double ph[3] = {0};
@@ -612,9 +664,9 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
     fprintf(stderr, "pack groups %lld: span %.1f us, per group: ticket+bits %.2f us, look-back %.2f us, pack %.2f us\n",
             ngroups, (t1 - t0) / 100.0, ph[0] / ngroups / 100.0, ph[1] / ngroups / 100.0, ph[2] / ngroups / 100.0);
   }
-  if (t) HIP_TRY(hipEventRecord(b->ev[6], b->stream));
-  HIP_TRY(launch_emit(a, b->stream));
-  if (t) HIP_TRY(hipEventRecord(b->ev[7], b->stream));
+  if (t) HIP_TRY(hipEventRecord(b->ev[6], st));
+  HIP_TRY(launch_emit(a, st));
+  if (t) HIP_TRY(hipEventRecord(b->ev[7], st));
   return MIJ_OK;
 }
 
@@ -627,6 +679,27 @@ static int encode_frames(mij_batch *b, int nframes) {
     HIP_TRY(hipMemsetAsync(b->d_seg_ntok, 0, sizeof(uint32_t) * nframes * b->g.nseg, b->stream));
   HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * nframes, b->stream));
   if (b->timing) HIP_TRY(hipEventRecord(b->ev[0], b->stream));
+  const int nsub = std::min(b->overlap, nframes);
+  if (!b->split && !b->keep_coefs && nsub > 1) {
+    // sub-batches: K1 of sub-batch k on the batch stream, its entropy stages
+    // on stream2 behind it, concurrent with K1 of sub-batch k + 1; the batch
+    // stream then waits for stream2, so syncing it covers the whole encode
+    const int per = (nframes + nsub - 1) / nsub;
+    for (int k = 0, f0 = 0; f0 < nframes; k++, f0 += per) {
+      const int nk = std::min(per, nframes - f0);
+      if (run_k1(b, nk, 2, 0, 0, f0, false)) return g_err;
+      HIP_TRY(hipEventRecord(b->ov_k1[k], b->stream));
+      HIP_TRY(hipStreamWaitEvent(b->stream2, b->ov_k1[k], 0));
+      if (run_entropy(b, nk, true, false, f0, b->stream2)) return g_err;
+    }
+    if (b->timing)
+      for (int e = 1; e <= 3; e++) HIP_TRY(hipEventRecord(b->ev[e], b->stream));  // K1 over all sub-batches
+    HIP_TRY(hipEventRecord(b->ov_done, b->stream2));
+    HIP_TRY(hipStreamWaitEvent(b->stream, b->ov_done, 0));
+    if (b->timing)
+      for (int e = 4; e < MIJ_NSTAGES; e++) HIP_TRY(hipEventRecord(b->ev[e], b->stream));
+    return MIJ_OK;
+  }
   if (b->split) {
     if (run_k1(b, nframes, 1)) return g_err;  // records events 1 and 2 around the fixer
     if (run_k1(b, nframes, 6, 0, 1)) return g_err;  // segment-first DCs inline: no k_seg_dc
@@ -775,6 +848,19 @@ int mij_batch_output_async(mij_batch *b, int frame, uint8_t *dst, size_t n) {
 extern "C" int mij_batch_set_split(mij_batch *b, int on) {
   if (!b) return fail(MIJ_EINVAL, "set_split: null batch");
   b->split = on != 0;
+  return MIJ_OK;
+}
+
+extern "C" int mij_batch_set_overlap(mij_batch *b, int nsub) {
+  if (pipe_check(b, "set_overlap")) return g_err;
+  if (nsub < 1 || nsub > 16) return fail(MIJ_EINVAL, "set_overlap: 1..16 sub-batches");
+  HIP_TRY(hipSetDevice(b->dev));
+  if (nsub > 1 && !b->stream2) {
+    HIP_TRY(hipStreamCreateWithFlags(&b->stream2, hipStreamNonBlocking));
+    for (auto &e : b->ov_k1) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&b->ov_done, hipEventDisableTiming));
+  }
+  b->overlap = nsub;
   return MIJ_OK;
 }
 

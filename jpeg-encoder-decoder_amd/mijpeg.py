@@ -22,7 +22,7 @@ EXPORTS = [
     "mij_set_input_stride", "mij_set_quality", "mij_last_error", "mij_strerror",
     "mij_max_jpg_bytes", "mij_encode",
     "mij_batch_create", "mij_batch_destroy", "mij_batch_upload", "mij_batch_set_input",
-    "mij_batch_encode", "mij_batch_keep_coefs", "mij_batch_set_split", "mij_batch_dct", "mij_batch_sync", "mij_batch_output",
+    "mij_batch_encode", "mij_batch_keep_coefs", "mij_batch_set_split", "mij_batch_set_overlap", "mij_batch_dct", "mij_batch_sync", "mij_batch_output",
     "mij_batch_lengths", "mij_batch_coefs", "mij_batch_tables", "mij_batch_set_timing",
     "mij_batch_stage_ms", "mij_batch_stage_history", "mij_batch_token_count", "mij_batch_geometry", "mij_batch_replays", "mij_batch_stream",
     "mij_band_analyze", "mij_band_histograms", "mij_band_tables", "mij_band_pack", "mij_band_words",
@@ -101,6 +101,7 @@ def load() -> C.CDLL:
     lib.mij_batch_encode.argtypes = [p, i]
     lib.mij_batch_keep_coefs.argtypes = [p, i]
     lib.mij_batch_set_split.argtypes = [p, i]
+    lib.mij_batch_set_overlap.argtypes = [p, i]
     lib.mij_batch_dct.argtypes = [p, i]
     lib.mij_batch_sync.argtypes = [p]
     lib.mij_batch_output.argtypes = [p, i, p, sz, C.POINTER(sz)]
@@ -318,6 +319,10 @@ class Batch:
 
     def set_split(self, on: bool) -> None:
         _check(self.lib.mij_batch_set_split(self.h_, int(on)), "set_split")
+
+    def set_overlap(self, nsub: int) -> None:
+        """fused pipeline in nsub sub-batches, entropy of one beside K1 of the next"""
+        _check(self.lib.mij_batch_set_overlap(self.h_, int(nsub)), "set_overlap")
 
     def set_rgb(self, on: bool) -> None:
         """frames in R, G, B byte order (PPM) instead of the encoder's B, G, R"""

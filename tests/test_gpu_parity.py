@@ -300,3 +300,19 @@ def test_pack_staged_and_unstaged_groups_in_one_scan(q):
         got, ref = b.output(i), O.cref_encode(frames[i], q)
         assert got == ref, f"frame {i} q{q}: first diff {first_diff(got, ref)}"
     b.close()
+
+
+@pytest.mark.parametrize("nsub", [2, 3])
+def test_overlapped_sub_batches_same_bytes(nsub):
+    """mij_batch_set_overlap: sub-batches whose entropy stages run on a second
+    stream beside the next sub-batch's K1 give the reference's JFIF, also
+    when the frame count does not divide evenly, and across repeated encodes."""
+    frames = np.stack([recipes.config3_frame(i, 272, 480) for i in range(4)] + [recipes.noise(272, 480, 5)])
+    b = mijpeg.Batch(480, 272, 5)
+    b.set_overlap(nsub)
+    b.upload(frames)
+    for _ in range(2):
+        b.encode(5)
+        for i in range(5):
+            assert b.output(i) == O.cref_encode(frames[i])
+    b.close()
