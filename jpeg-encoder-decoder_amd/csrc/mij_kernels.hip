@@ -586,10 +586,14 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
     c1[k] = pack_i16x2(o[8 + 2 * k], o[9 + 2 * k]);
   }
   // staged block-major (block b's 64 coefficients in zigzag order at st +
-  // 64 b): the AC loop below addresses coefficient z of its block directly
-  int16_t *stb = &st[0][0] + 64 * bcol + 16 * g;
-  *(u4v *)stb = c0;
-  *(u4v *)(stb + 8) = c1;
+  // 64 b), its 16-byte chunks XOR-swizzled by b & 7 (coefficient z at
+  // 64 b + (z ^ 8 (b & 7))): the 8 lanes of a ds_write_b128 group store to 8
+  // different bank quads instead of one (blocks are 128 B = 32 banks apart:
+  // 8-way conflicts), and the AC loop's reads of one z spread over the banks
+  const int zsw = 8 * (bcol & 7);
+  int16_t *stb = &st[0][0] + 64 * bcol;
+  *(u4v *)(stb + ((16 * g) ^ zsw)) = c0;
+  *(u4v *)(stb + ((16 * g + 8) ^ zsw)) = c1;
   // nonzero mask: min(half, 1) per packed int16 pair puts coefficient 2k's
   // flag at bit 2k and 2k+1's at bit 16+2k
   // (v_pk_min_u16 in asm: the compiler rewrites min(h, 1) into compares and
@@ -657,7 +661,7 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
   if (valid && !(kflags & K1F_NO_ACLOOP)) {
     const int16_t *sl = &st[0][0] + 64 * bcol;
     auto token = [&](int z, int rank, int zp) {
-      const int cz = sl[z];
+      const int cz = sl[z ^ zsw];
       const int run = z - zp - 1;
       const uint32_t a = (uint32_t)max(cz, -cz);
       const uint32_t cls = 32u - (uint32_t)__builtin_clz(a);  // a != 0
