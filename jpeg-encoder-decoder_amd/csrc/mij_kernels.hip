@@ -1932,7 +1932,7 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
     return nb;
   };
   unsigned long long pacc[LB_SEGS_PER_ROW][LB_STEPS];
-  uint32_t pnb[LB_SEGS_PER_ROW][LB_STEPS];
+  uint32_t pnb[LB_SEGS_PER_ROW][LB_STEPS], bk[LB_SEGS_PER_ROW];
   // ---- 0. this row's segments: token counts and their first register steps
   // (LB_STEPS 64-token steps of a luma segment, LB_STEPS_C of a chroma one),
   // all loads at once: none waits for the counts (a slot holds SEG_TOK
@@ -1971,10 +1971,25 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
       pnb[k][st] = st < nst ? merge_step(tq[k][st], nt[k] - 64 * st - 4 * sub, pacc[k][st]) : 0u;
       b += pnb[k][st];
     }
+    bk[k] = b;
+  }
+  // steps past the registers, in rounds: one step of every segment of the
+  // row per round, their loads issued together (one memory round trip per
+  // round, not per segment and step)
+  const int ntmax = max(max(nt[0], nt[1]), max(nt[2], nt[3]));  // row-uniform
+  for (int i0 = 64 * nst; i0 < ntmax; i0 += 64) {
+    u4v tr[LB_SEGS_PER_ROW];
+#pragma unroll
+    for (int k = 0; k < LB_SEGS_PER_ROW; k++) tr[k] = load_step(k, i0);
+#pragma unroll
+    for (int k = 0; k < LB_SEGS_PER_ROW; k++)
+      if (i0 < nt[k]) bk[k] += step_bits(tr[k], nt[k] - i0 - 4 * sub);
+  }
+#pragma unroll
+  for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
     const int sl = row + LB_ROWS * k;
     if (sl < nsg) {  // row-uniform
-      for (int i0 = 64 * nst; i0 < nt[k]; i0 += 64) b += step_bits(load_step(k, i0), nt[k] - i0 - 4 * sub);
-      b = row_scan16(b);
+      const uint32_t b = row_scan16(bk[k]);
       if (sub == 15) s_bits[sl] = b;
     }
   }
@@ -2115,17 +2130,27 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
       else if (nb) put_bits64(buf, pos, acc << (64 - nb), nb);
     };
     if (whole) {
+      uint32_t pos0[LB_SEGS_PER_ROW];
 #pragma unroll
       for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
         const int sl = row + LB_ROWS * k;
         if (sl >= nsg) break;  // row-uniform
-        uint32_t pos0 = boff + s_off[sl];
+        pos0[k] = boff + s_off[sl];
 #pragma unroll
         for (int st = 0; st < LB_STEPS; st++) {
           if (st >= nst || 64 * st >= nt[k]) break;  // row-uniform
-          placed_step(pacc[k][st], pnb[k][st], pos0);
+          placed_step(pacc[k][st], pnb[k][st], pos0[k]);
         }
-        for (int i0 = 64 * nst; i0 < nt[k]; i0 += 64) fast_step(load_step(k, i0), nt[k] - i0 - 4 * sub, pos0);
+      }
+      // the steps past the registers again in rounds (segments beyond the
+      // group have nt = 0)
+      for (int i0 = 64 * nst; i0 < ntmax; i0 += 64) {
+        u4v tr[LB_SEGS_PER_ROW];
+#pragma unroll
+        for (int k = 0; k < LB_SEGS_PER_ROW; k++) tr[k] = load_step(k, i0);
+#pragma unroll
+        for (int k = 0; k < LB_SEGS_PER_ROW; k++)
+          if (i0 < nt[k]) fast_step(tr[k], nt[k] - i0 - 4 * sub, pos0[k]);
       }
     }
     if (__ballot(slow)) {  // second pass over this wave's rows, tokens reloaded
