@@ -172,10 +172,13 @@ __device__ __forceinline__ int dc_tie(int d, const uint32_t *bits) {
 
 // One AC coefficient replayed exactly as encoder.c:87-109 computes it
 // (column pass summed from 0 in y order, row pass in x order, FP64, no FMA).
-// C = the 64 cosines (LDS), blk = the block's 64 staged pixels (LDS).  The
-// eight column sums are independent chains, evaluated side by side.
-__device__ __forceinline__ int ac_exact(const uint8_t *blk, int z, int q, const double *C) {
-  const int rz = c_zigzag[z];
+// C = the 64 cosines (LDS), blk = the block's 64 staged pixels (LDS), zz =
+// the zigzag table (LDS: a global load here would wait, vmcnt(0), for every
+// token store and the next tile's DMA still in flight -- it made the replays
+// 10x dearer).  The eight column sums are independent chains, evaluated side
+// by side.
+__device__ __forceinline__ int ac_exact(const uint8_t *blk, int z, int q, const double *C, const uint8_t *zz) {
+  const int rz = zz[z];
   const int v = rz >> 3, u = rz & 7;
   double inner[8];
 #pragma unroll
@@ -741,6 +744,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   constexpr bool LUT_LDS = PIX && !(TOK && NW >= 8);
   __shared__ uint32_t s_lut[LUT_LDS ? 3 * LUT_WORDS : 1];
   __shared__ double s_cos[64];
+  __shared__ uint8_t s_zz[64];
   __shared__ int s_qint[2][64];
   __shared__ __attribute__((aligned(16))) int16_t s_st[TOK ? NW : 1][64][16];  // token staging
   // per-frame histograms of this workgroup: [frame slot][luma, chroma][copy][symbol];
@@ -762,7 +766,10 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
 #else
   constexpr int kflags = 0;
 #endif
-  if (threadIdx.x < 64) s_cos[threadIdx.x] = T->cosd[threadIdx.x];
+  if (threadIdx.x < 64) {
+    s_cos[threadIdx.x] = T->cosd[threadIdx.x];
+    s_zz[threadIdx.x] = (uint8_t)c_zigzag[threadIdx.x];
+  }
   if (TOK) {
     for (int i = threadIdx.x; i < 2 * 2 * HREP * 256; i += NT) (&s_hac[0][0][0][0])[i] = 0;
     for (int i = threadIdx.x; i < 2 * 2 * HREP * 16; i += NT) (&s_hdc[0][0][0][0])[i] = 0;
@@ -814,6 +821,11 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   const unsigned long long w_t0 = __builtin_amdgcn_s_memrealtime();
   int w_ntiles = 0;
 #endif
+  // coefficients this lane replayed in FP64 (or listed for k_fix_blocks):
+  // summed over the wave and added once at the end (an atomic per replaying
+  // lane on the one counter cost 12 ms per launch at Q=90, where 2.7 M
+  // coefficients are replayed: 17.5 -> 5.3 ms)
+  uint32_t nrep = 0;
   if (t < tend) {
     uint8_t *raw = s_raw[PIX ? wave : 0];
     TilePos p = tpos(t);
@@ -1063,7 +1075,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
                 uint32_t base = 0;
                 if (lane == 0) {
                   base = atomicAdd(a.fix_count, (unsigned)__popc(m16));
-                  atomicAdd(a.replays, (unsigned)__popc(m16));
+                  nrep += (uint32_t)__popc(m16);
                 }
                 base = __builtin_amdgcn_readfirstlane(base);
                 if (g == 0 && ((m16 >> bcol) & 1u))
@@ -1086,16 +1098,15 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
                 const float tv = fmaf(fa, lc, 1.0e-6f);
                 mm |= (uint32_t)((int)fmaf(nf, fa, -tv) != (int)fmaf(nf, fa, tv)) << k;
               }
-            const uint32_t hm = mm;
+            nrep += (uint32_t)__popc(mm);
             while (mm) {
               const int k = __ffs(mm) - 1;
               mm &= mm - 1u;
               const int z = 16 * g + k;
-              const int v = ac_exact(Pb, z, s_qint[comp][z], s_cos);
+              const int v = ac_exact(Pb, z, s_qint[comp][z], s_cos, s_zz);
 #pragma unroll
               for (int j = 0; j < 16; j++) o[j] = j == k ? v : o[j];
             }
-            if (hm) atomicAdd(a.replays, (unsigned)__popc(hm));
           }
           // token variants: the next tile's DMA has landed before the first
           // store (their VMEM count per tile varies)
@@ -1118,6 +1129,10 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
       t = tn;
       first = false;
     }
+  }
+  if (__ballot(nrep != 0)) {
+    const uint32_t tot = wave_scan64(nrep);
+    if (lane == 63) atomicAdd(a.replays, tot);
   }
 #ifdef MIJ_K1_DIAG
   if (a.wtime && lane == 0) {
