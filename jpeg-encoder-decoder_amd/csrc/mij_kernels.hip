@@ -1870,6 +1870,18 @@ __device__ __forceinline__ void put_bits64(uint32_t *buf, uint32_t pos, unsigned
   if (off + len > 64) atomicOr(&buf[w + 2], __builtin_amdgcn_alignbit(lo, 0u, off));
 }
 
+// put_bits64 into the window [lo_bit, hi_bit) of the group's bits only
+// (buf holds the window's words)
+__device__ __forceinline__ void put_bits64_win(uint32_t *buf, uint32_t pos, unsigned long long v, uint32_t len,
+                                               uint32_t lo_bit, uint32_t hi_bit) {
+  if (pos + len <= lo_bit || pos >= hi_bit) return;
+  const uint32_t w = pos >> 5, off = pos & 31u, wl = lo_bit >> 5, wh = hi_bit >> 5;
+  const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+  if (w >= wl && w < wh) atomicOr(&buf[w - wl], hi >> off);
+  if (off + len > 32 && w + 1 >= wl && w + 1 < wh) atomicOr(&buf[w + 1 - wl], __builtin_amdgcn_alignbit(hi, lo, off));
+  if (off + len > 64 && w + 2 >= wl && w + 2 < wh) atomicOr(&buf[w + 2 - wl], __builtin_amdgcn_alignbit(lo, 0u, off));
+}
+
 __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
   __shared__ uint32_t buf[PACK_WORDS];
   __shared__ uint32_t tab[2 * 256];
@@ -2115,7 +2127,8 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
       }
       return nb;
     };
-    bool slow = !whole;
+    // (a window of a wider group: the same merged strings, clipped to it)
+    bool slow = false;
     // one 64-token step of a row past the registers: positions, then the
     // lane's merged bits
     auto fast_step = [&](const u4v &t, int lim, uint32_t &pos0) {
@@ -2133,7 +2146,8 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
           for (uint32_t z = nzr[e]; z; z--) acc = (acc << Lz) | zcode;  // encoder.c:490-494 ZRL
           acc = (acc << L[e]) | code[e];
         }
-        put_bits64(buf, pos, acc << (64 - nb), nb);
+        if (whole) put_bits64(buf, pos, acc << (64 - nb), nb);
+        else put_bits64_win(buf, pos, acc << (64 - nb), nb, lo_bit, hi_bit);
       }
     };
     // the same for a step merged in phase 1
@@ -2142,9 +2156,10 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
       const uint32_t pos = pos0 + x - nb;
       pos0 += row_last(x);
       if (nb > 64) slow = true;
-      else if (nb) put_bits64(buf, pos, acc << (64 - nb), nb);
+      else if (nb && whole) put_bits64(buf, pos, acc << (64 - nb), nb);
+      else if (nb) put_bits64_win(buf, pos, acc << (64 - nb), nb, lo_bit, hi_bit);
     };
-    if (whole) {
+    {
       uint32_t pos0[LB_SEGS_PER_ROW];
 #pragma unroll
       for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
@@ -2185,7 +2200,7 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
           uint32_t pos = pos0 + x - nb;
           pos0 += row_last(x);
           // the first pass placed the steps of lanes within 64 bits
-          if (whole && nb <= 64) continue;
+          if (nb <= 64) continue;
           for (int e = 0; e < 4; e++) {
             for (uint32_t z = nzr[e]; z; z--) {  // encoder.c:490-494 ZRL
               if (pos < hi_bit && pos + Lz > lo_bit) put_bits_window(buf, pos, lo_bit, hi_bit, zcode, (int)Lz);
