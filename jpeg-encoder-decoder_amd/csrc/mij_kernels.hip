@@ -567,6 +567,11 @@ __device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int
 // Bit length = code length + (symbol & 15) + ZRLs * ZRL code length for
 // every token kind (DC: symbol = class <= 11; EOB: symbol 0x00).
 constexpr uint32_t TOK_AC = 1u << 10;
+// N-tile of the token K1 before whose stores the next tile's DMA is awaited
+// (A/B: 0, 1 and 2 measured equal, 3.36-3.39 ms)
+#ifndef MIJ_K1_DMAWAIT_NT
+#define MIJ_K1_DMAWAIT_NT 0
+#endif
 
 // One N-tile of coefficients -> compacted token stream of its segment(s).
 // o[k] = zigzag coefficient 16g+k of block bcol (DC raw in o[0] of g == 0,
@@ -1110,7 +1115,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
           }
           // token variants: the next tile's DMA has landed before the first
           // store (their VMEM count per tile varies)
-          if (nt == 0 && !DEFER && !(kflags & K1F_NO_DMAWAIT)) dma_wait();
+          if (nt == MIJ_K1_DMAWAIT_NT && !DEFER && !(kflags & K1F_NO_DMAWAIT)) dma_wait();
           finish(nt, o);
         }
       } else if (!PIX) {
