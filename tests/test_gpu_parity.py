@@ -316,3 +316,21 @@ def test_overlapped_sub_batches_same_bytes(nsub):
         for i in range(5):
             assert b.output(i) == O.cref_encode(frames[i])
     b.close()
+
+
+@pytest.mark.parametrize("q", [75, 90])
+@pytest.mark.parametrize("split", [False, True])
+def test_high_quality_replays_both_pipelines(q, split):
+    """At high Q most N-tiles carry a straddling coefficient (~10^4 FP64
+    replays per 4K frame at Q=90): the in-place replays of the fused K1 and
+    k_fix_blocks of the split pipeline both give the reference's bytes, and
+    the replay counter counts them."""
+    frames = np.stack([recipes.config3_frame(i, 256, 512) for i in range(3)])
+    b = mijpeg.Batch(512, 256, 3, q)
+    b.set_split(split)
+    b.upload(frames)
+    b.encode(3)
+    for i in range(3):
+        assert b.output(i) == O.cref_encode(frames[i], q)
+    assert b.replays() > 0
+    b.close()
