@@ -569,6 +569,10 @@ __device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int
 constexpr uint32_t TOK_AC = 1u << 10;
 // N-tile of the token K1 before whose stores the next tile's DMA is awaited
 // (A/B: 0, 1 and 2 measured equal, 3.36-3.39 ms)
+// AC-token loop over both 32-bit mask halves at once (A/B knob)
+#ifndef MIJ_K1_ACMERGE
+#define MIJ_K1_ACMERGE 0
+#endif
 #ifndef MIJ_K1_DMAWAIT_NT
 #define MIJ_K1_DMAWAIT_NT 0
 #endif
@@ -686,17 +690,33 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
       }
     };
     const uint32_t cm = 0x11111111u << g;
+    const int rank_lo = __popc(Mlo), zp_lo = 31 - __clz((int)(Mlo | 1u));
+#if MIJ_K1_ACMERGE
+    // one loop over both halves: the wave runs max(lo + hi) iterations
+    // instead of max(lo) + max(hi), at a few selects per iteration
+    uint32_t mlo = Mlo & cm, mhi = Mhi & cm;
+    while (mlo | mhi) {
+      const bool lo = mlo != 0;
+      const uint32_t m = lo ? mlo : mhi, M = lo ? Mlo : Mhi;
+      const int zz = __builtin_ctz(m);
+      const uint32_t bef = M & ((1u << zz) - 1u);
+      const int h = lo ? 0 : 32;
+      token(h + zz, (lo ? 0 : rank_lo) + __popc(bef), bef ? h + 31 - __clz((int)bef) : (lo ? 0 : zp_lo));
+      if (lo) mlo &= mlo - 1u;
+      else mhi &= mhi - 1u;
+    }
+#else
     for (uint32_t m = Mlo & cm; m; m &= m - 1u) {
       const int z = __builtin_ctz(m);
       const uint32_t bef = Mlo & ((1u << z) - 1u);
       token(z, __popc(bef), 31 - __clz((int)(bef | 1u)));
     }
-    const int rank_lo = __popc(Mlo), zp_lo = 31 - __clz((int)(Mlo | 1u));
     for (uint32_t m = Mhi & cm; m; m &= m - 1u) {
       const int zz = __builtin_ctz(m);
       const uint32_t bef = Mhi & ((1u << zz) - 1u);
       token(32 + zz, rank_lo + __popc(bef), bef ? 63 - __clz((int)bef) : zp_lo);
     }
+#endif
   }
   wave_lds_sync();
 }
@@ -949,19 +969,20 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
       // ---- 3-4. quantize, replay, store, emit -----------------------------------
       // block (index inside the frame's coefficient space) of this lane's
       // column in N-tile nt; false for columns beyond the frame edge
-      auto block_of = [&](const int nt, int &blk) -> bool {
+      auto block_at = [&](const int nt, const int col, int &blk) -> bool {
         const FGeom fg = frame_geom(G, fdims, p.f);  // REG only
         const int bwf = REG ? fg.bw : bw, mwf = REG ? fg.mw : mw;
         const int nYf = REG ? fg.nY : G.nY, nCf = REG ? fg.nC : G.nC;
         if (nt < 2) {
-          const int bx = p.tx * 16 + bcol;
+          const int bx = p.tx * 16 + col;
           blk = (2 * p.ty + nt) * bwf + bx;
           return bx < bwf;
         }
-        const int mx = p.tx * 8 + (bcol & 7);
-        blk = nYf + (bcol >= 8 ? nCf : 0) + p.ty * mwf + mx;
+        const int mx = p.tx * 8 + (col & 7);
+        blk = nYf + (col >= 8 ? nCf : 0) + p.ty * mwf + mx;
         return mx < mwf;
       };
+      auto block_of = [&](const int nt, int &blk) -> bool { return block_at(nt, bcol, blk); };
       auto finish = [&](const int nt, int (&o)[16]) {
         const int comp = nt == 2 ? 1 : 0;
         int blk;
@@ -979,25 +1000,55 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
             o[9 + 2 * k] = (int16_t)(c1[k] >> 16);
           }
         }
-        if ((MODE & K1M_COEF_OUT) && valid && !(kflags & K1F_NO_STORE)) {
-          int16_t *dst = a.coef + (long long)p.f * G.coef_fs + (long long)blk * 64 + 16 * g;
+        if ((MODE & K1M_COEF_OUT) && !(kflags & K1F_NO_STORE)) {
           u4v s0, s1;
 #pragma unroll
           for (int k = 0; k < 4; k++) {
             s0[k] = pack_i16x2(o[2 * k], o[2 * k + 1]);
             s1[k] = pack_i16x2(o[8 + 2 * k], o[9 + 2 * k]);
           }
-          if (kflags & K1F_LINEAR_STORE) {  // diagnostics: timing of fully contiguous stores
-            const long long b0 = nt < 2 ? blk - bcol : G.nY + (long long)p.ty * mw + p.tx * 8;
-            int16_t *lin = a.coef + (long long)p.f * G.coef_fs + b0 * 64 + 8 * lane;
-            __builtin_nontemporal_store(s0, (u4v *)lin);
-            __builtin_nontemporal_store(s1, (u4v *)(lin + 512));
-          } else if (kflags & K1F_PLAIN_STORE) {  // diagnostics: default cache policy
-            *(u4v *)dst = s0;
-            *(u4v *)(dst + 8) = s1;
+          int16_t *const fcoef = a.coef + (long long)p.f * G.coef_fs;
+          if (kflags & (K1F_LINEAR_STORE | K1F_PLAIN_STORE)) {
+            int16_t *dst = fcoef + (long long)blk * 64 + 16 * g;
+            if (!valid) {
+            } else if (kflags & K1F_LINEAR_STORE) {  // diagnostics: timing of fully contiguous stores
+              const long long b0 = nt < 2 ? blk - bcol : G.nY + (long long)p.ty * mw + p.tx * 8;
+              int16_t *lin = fcoef + b0 * 64 + 8 * lane;
+              __builtin_nontemporal_store(s0, (u4v *)lin);
+              __builtin_nontemporal_store(s1, (u4v *)(lin + 512));
+            } else {  // diagnostics: the lane-owned halves with the default cache policy
+              *(u4v *)dst = s0;
+              *(u4v *)(dst + 8) = s1;
+            }
           } else {
-            __builtin_nontemporal_store(s0, (u4v *)dst);
-            __builtin_nontemporal_store(s1, (u4v *)(dst + 8));
+            // Whole block lines per store instruction.  Lane (g, b) holds
+            // chunks (b, 2g) = s0 and (b, 2g+1) = s1 of the 16-byte chunks of
+            // its block; stored as they are, each instruction would cover one
+            // half of every block's 128-byte line (written in two partial
+            // halves: 1.16x write traffic).  Lanes b and b^8 (one DPP row
+            // rotate by 8) trade: the first store writes blocks 0-7 whole
+            // (b < 8 its own s0, b >= 8 the s1 of block b-8), the second
+            // blocks 8-15 (b < 8 the s0 of block b+8, b >= 8 its own s1).
+            // Blocks 0-7 and 8-15 are each 1 KB contiguous (a luma block row
+            // of the tile; the tile's Cb and Cr blocks).
+            u4v d1, d2;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+              d1[k] = (uint32_t)__builtin_amdgcn_update_dpp((int)s0[k], (int)s1[k], 0x128, 0xF, 0xC, false);
+              d2[k] = (uint32_t)__builtin_amdgcn_update_dpp((int)s1[k], (int)s0[k], 0x128, 0xF, 0x3, false);
+            }
+            const int off = 16 * g + 8 * (bcol >> 3);
+            int b1, b2;
+            const bool v1 = block_at(nt, bcol & 7, b1), v2 = block_at(nt, bcol | 8, b2);
+            // The DEFER variant's counted DMA wait needs both store
+            // instructions issued on every N-tile: column 0's lanes are always
+            // valid for the first, and a lane whose second block lies beyond
+            // the frame edge repeats its first store (same bytes, same
+            // address) instead of dropping out, so the second never runs on
+            // an empty exec mask either.
+            int16_t *const p1 = fcoef + (long long)b1 * 64 + off;
+            if (v1) __builtin_nontemporal_store(d1, (u4v *)p1);
+            if (v1 || v2) __builtin_nontemporal_store(v2 ? d2 : d1, (u4v *)(v2 ? fcoef + (long long)b2 * 64 + off : p1));
           }
         }
         if (PIX && valid && g == 0) a.dc[(long long)p.f * G.nblk + blk] = (int16_t)o[0];
