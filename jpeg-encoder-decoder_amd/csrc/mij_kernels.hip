@@ -567,12 +567,13 @@ __device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int
 // Bit length = code length + (symbol & 15) + ZRLs * ZRL code length for
 // every token kind (DC: symbol = class <= 11; EOB: symbol 0x00).
 constexpr uint32_t TOK_AC = 1u << 10;
-// N-tile of the token K1 before whose stores the next tile's DMA is awaited
-// (A/B: 0, 1 and 2 measured equal, 3.36-3.39 ms)
-// AC-token loop over both 32-bit mask halves at once (A/B knob)
+// AC-token loop over both 32-bit mask halves at once (A/B knob; measured:
+// token K1 3.39 -> 3.49 ms, the selects cost more than the saved iterations)
 #ifndef MIJ_K1_ACMERGE
 #define MIJ_K1_ACMERGE 0
 #endif
+// N-tile of the token K1 before whose stores the next tile's DMA is awaited
+// (A/B: 0, 1 and 2 measured equal, 3.36-3.39 ms)
 #ifndef MIJ_K1_DMAWAIT_NT
 #define MIJ_K1_DMAWAIT_NT 0
 #endif
