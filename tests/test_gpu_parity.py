@@ -334,3 +334,22 @@ def test_high_quality_replays_both_pipelines(q, split):
         assert b.output(i) == O.cref_encode(frames[i], q)
     assert b.replays() > 0
     b.close()
+
+
+@pytest.mark.parametrize("W", [144, 160, 176, 192, 208, 224, 240])
+def test_coefficient_k1_partial_last_tile(W):
+    """The coefficient K1 stores whole block lines by trading chunks between
+    lanes b and b^8; in the last 128-px tile of a row only some block
+    columns exist (here 2..14 luma, 1..7 chroma), so the second store's lanes
+    fall back to repeating their first.  Split pipeline (coefficient planes
+    -> tokenize) against the reference's bytes, natural and noise content."""
+    H = 48
+    frames = np.stack([recipes.config3_frame(1, H, W), recipes.noise(H, W, W)])
+    b = mijpeg.Batch(W, H, 2)
+    b.set_split(True)
+    b.upload(frames)
+    b.encode(2)
+    for i in range(2):
+        got, ref = b.output(i), O.cref_encode(frames[i])
+        assert got == ref, f"W={W} frame {i}: first diff {first_diff(got, ref)}"
+    b.close()
