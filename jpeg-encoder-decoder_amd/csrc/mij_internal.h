@@ -39,9 +39,14 @@ constexpr int PACK_WORDS = 4096;
 // k_pack_lb: tokens per lane loaded in one batch (16 lanes per segment)
 constexpr int PACK_BATCH = 16;
 // JFIF assembly: scans are written in EMIT_CH-byte chunks by EMIT_SLOTS
-// workgroups per scan
+// workgroups per scan (A/B on config 3, emit = count + scan + write:
+// 8 slots 0.260 ms, 16 0.232, 32 0.243, 64 0.247, 128 0.269, 256 0.321;
+// profiles/r02/emit_slots_ab.txt)
 constexpr int EMIT_CH = 4096;
-constexpr int EMIT_SLOTS = 64;
+#ifndef MIJ_EMIT_SLOTS
+#define MIJ_EMIT_SLOTS 16
+#endif
+constexpr int EMIT_SLOTS = MIJ_EMIT_SLOTS;
 
 // Layout-identical to the reference huff_code (include/structs.h:5-13).
 struct HuffCode {
