@@ -42,7 +42,10 @@ constexpr int PACK_BATCH = 16;
 // workgroups per scan (A/B on config 3, emit = count + scan + write:
 // 8 slots 0.260 ms, 16 0.232, 32 0.243, 64 0.247, 128 0.269, 256 0.321;
 // profiles/r02/emit_slots_ab.txt)
-constexpr int EMIT_CH = 4096;
+#ifndef MIJ_EMIT_CH
+#define MIJ_EMIT_CH 4096
+#endif
+constexpr int EMIT_CH = MIJ_EMIT_CH;
 #ifndef MIJ_EMIT_SLOTS
 #define MIJ_EMIT_SLOTS 16
 #endif
