@@ -38,16 +38,16 @@ constexpr int MAX_BLOCK_BITS = 1729;              // 28 DC + 63 * 27 AC bits
 constexpr int PACK_WORDS = 4096;
 // k_pack_lb: tokens per lane loaded in one batch (16 lanes per segment)
 constexpr int PACK_BATCH = 16;
-// JFIF assembly: scans are written in EMIT_CH-byte chunks by EMIT_SLOTS
-// workgroups per scan (A/B on config 3, emit = count + scan + write:
-// 8 slots 0.260 ms, 16 0.232, 32 0.243, 64 0.247, 128 0.269, 256 0.321;
-// profiles/r02/emit_slots_ab.txt)
+// JFIF assembly: scans are written in EMIT_CH-byte chunks by EntArgs::
+// emit_slots workgroups per scan, EMIT_SLOTS when unset (A/B on config 3,
+// emit = count + scan + write: 8 slots 0.260 ms, 16 0.232, 32 0.243,
+// 64 0.247, 128 0.269, 256 0.321; profiles/r02/emit_slots_ab.txt)
 #ifndef MIJ_EMIT_CH
 #define MIJ_EMIT_CH 4096
 #endif
 constexpr int EMIT_CH = MIJ_EMIT_CH;
 #ifndef MIJ_EMIT_SLOTS
-#define MIJ_EMIT_SLOTS 16
+#define MIJ_EMIT_SLOTS 64
 #endif
 constexpr int EMIT_SLOTS = MIJ_EMIT_SLOTS;
 
@@ -192,6 +192,7 @@ struct EntArgs {
   unsigned int *pack_ticket;       // k_pack_lb: next group to claim, per scan
   unsigned long long *dbg;         // diagnostics only (MIJ_PACK_TIME, diag build)
   const int2 *fdims;               // per-frame image size (region batches), null: the canvas
+  int emit_slots;                  // k_emit_count / k_emit_write workgroups per scan (0: EMIT_SLOTS)
   int seg_dc;                      // k_tables: compute the segment-first DC tokens first (k_seg_dc)
 };
 

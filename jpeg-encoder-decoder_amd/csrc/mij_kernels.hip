@@ -2311,7 +2311,7 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
 // bytes of every chunk; k_emit_write then knows every chunk's output offset
 // (header + earlier scans + earlier chunks' stuffing) and writes the chunks
 // independently: the stuffed bytes are laid out in LDS and leave in
-// coalesced stores.  Workgroup (frame, comp, j) takes chunks j, j+EMIT_SLOTS..
+// coalesced stores.  Workgroup (frame, comp, j) takes chunks j, j+a.emit_slots..
 // ===========================================================================
 __device__ __forceinline__ bool emit_frame_ok(const EntArgs &a, int f) {
   unsigned long long need = 1024;  // headers, markers, pads
@@ -2346,14 +2346,14 @@ __device__ __forceinline__ int block_sum256(int v, int *red) {
 
 __global__ __launch_bounds__(256) void k_emit_count(EntArgs a) {
   __shared__ int red[4];
-  const int slot = blockIdx.x % EMIT_SLOTS, fc = blockIdx.x / EMIT_SLOTS;
+  const int slot = blockIdx.x % a.emit_slots, fc = blockIdx.x / a.emit_slots;
   const int f = fc / 3, comp = fc - f * 3;
   const unsigned long long nbytes = a.scan_bits[f * 3 + comp] >> 3;
   if (nbytes > 4ull * a.g.raw_words[comp]) return;  // k_emit_write drops the frame
   const uint32_t *raw = scan_raw(a, f, comp);
   const long long nch = (long long)((nbytes + EMIT_CH - 1) / EMIT_CH);
   uint32_t *ffc = a.ffc + (long long)fc * emit_chunks(a.g);
-  for (long long c = slot; c < nch; c += EMIT_SLOTS) {
+  for (long long c = slot; c < nch; c += a.emit_slots) {
     const unsigned long long b0 = (unsigned long long)c * EMIT_CH + threadIdx.x * (EMIT_CH / 256);
     int cnt = 0;
 #pragma unroll
@@ -2477,14 +2477,14 @@ __global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
 __global__ __launch_bounds__(256) void k_emit_write(EntArgs a) {
   __shared__ uint8_t s_out[2 * EMIT_CH];
   __shared__ int red[4];
-  const int slot = blockIdx.x % EMIT_SLOTS, fc = blockIdx.x / EMIT_SLOTS;
+  const int slot = blockIdx.x % a.emit_slots, fc = blockIdx.x / a.emit_slots;
   const int f = fc / 3, comp = fc - f * 3;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // every scan-buffer word read here is zeroed after use: k_pack_lb needs
   // all-zero buffers (a failed frame's buffers are cleared whole)
   uint32_t *raw = (uint32_t *)scan_raw(a, f, comp);
   if (!emit_frame_ok(a, f)) {
-    for (long long i = (long long)slot * 256 + tid; i < a.g.raw_words[comp]; i += EMIT_SLOTS * 256) raw[i] = 0;
+    for (long long i = (long long)slot * 256 + tid; i < a.g.raw_words[comp]; i += a.emit_slots * 256) raw[i] = 0;
     return;
   }
   uint8_t *out = a.out + (long long)f * a.g.out_cap;
@@ -2498,7 +2498,7 @@ __global__ __launch_bounds__(256) void k_emit_write(EntArgs a) {
   const uint32_t *cnt = a.ffc + (long long)fc * nchmax;
   const uint32_t *offs = a.choff + (long long)fc * nchmax;
   constexpr int WPW = EMIT_CH / 16;  // stream words per wave
-  for (long long c = slot; c < nch; c += EMIT_SLOTS) {
+  for (long long c = slot; c < nch; c += a.emit_slots) {
     const unsigned long long cb = (unsigned long long)c * EMIT_CH;
     const unsigned long long o0 = offs[c];
     const int tot = (int)cnt[c];
@@ -2779,10 +2779,12 @@ hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s) {
   hipLaunchKernelGGL(k_pack_lb, dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
   return hipGetLastError();
 }
-hipError_t launch_emit(const EntArgs &a, hipStream_t s) {
-  hipLaunchKernelGGL(k_emit_count, dim3(a.nframes * 3 * EMIT_SLOTS), dim3(256), 0, s, a);
+hipError_t launch_emit(const EntArgs &a0, hipStream_t s) {
+  EntArgs a = a0;
+  if (a.emit_slots < 1) a.emit_slots = EMIT_SLOTS;
+  hipLaunchKernelGGL(k_emit_count, dim3(a.nframes * 3 * a.emit_slots), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_emit_scan, dim3(a.nframes), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_emit_write, dim3(a.nframes * 3 * EMIT_SLOTS), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_emit_write, dim3(a.nframes * 3 * a.emit_slots), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_gather_regions(uint8_t *dst, long long slot_bytes, int pitch, const uint8_t *src,
