@@ -1444,6 +1444,53 @@ __device__ __forceinline__ void top2(unsigned long long &k1, unsigned long long 
   k2 = hi < m2 ? hi : m2;
 }
 
+// One butterfly step of the wave's top-2 reduction with DPP instead of
+// ds_bpermute (__shfl_xor): each step exchanges the 64-bit keys with a lane of
+// a disjoint group (quad_perm [1,0,3,2], [2,3,0,1]; row_half_mirror,
+// row_mirror; then permlane16/32 swaps across rows), so after six steps every
+// lane holds the wave's two smallest keys.  VALU-latency steps instead of LDS
+// round trips on the merge loop's critical path (~160 iterations per AC table).
+#ifndef MIJ_TAB_DPP
+#define MIJ_TAB_DPP 1
+#endif
+template <int CTRL>
+__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, false);
+  return ((unsigned long long)hi << 32) | lo;
+}
+template <int CTRL>
+__device__ __forceinline__ void top2_dpp(unsigned long long &k1, unsigned long long &k2) {
+  const unsigned long long o1 = dpp_u64<CTRL>(k1), o2 = dpp_u64<CTRL>(k2);
+  top2(k1, k2, o1, o2);
+}
+// permlane16/32 swap of a 64-bit value: (a, b) = one lane's own value and its
+// partner's (which is which depends on the row; the merge is symmetric)
+template <int W>
+__device__ __forceinline__ void swap_u64(unsigned long long x, unsigned long long &a, unsigned long long &b) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  if constexpr (W == 16) {
+    const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    a = ((unsigned long long)rh[0] << 32) | rl[0];
+    b = ((unsigned long long)rh[1] << 32) | rl[1];
+  } else {
+    const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    a = ((unsigned long long)rh[0] << 32) | rl[0];
+    b = ((unsigned long long)rh[1] << 32) | rl[1];
+  }
+}
+template <int W>
+__device__ __forceinline__ void top2_swap(unsigned long long &k1, unsigned long long &k2) {
+  unsigned long long a1, b1, a2, b2;
+  swap_u64<W>(k1, a1, b1);
+  swap_u64<W>(k2, a2, b2);
+  k1 = a1;
+  k2 = a2;
+  top2(k1, k2, b1, b2);
+}
+
 // extra: DC class counts the caller adds to hist (the segment-first DCs), or null
 __device__ void build_table_wave(const uint32_t *hist, const uint32_t *extra, HuffCode *hc, uint32_t *ehuf,
                                  TabScratch *S, int lane, int *err) {
@@ -1473,12 +1520,21 @@ __device__ void build_table_wave(const uint32_t *hist, const uint32_t *extra, Hu
         top2(k1, k2, key, ~0ull);
       }
     }
+#if MIJ_TAB_DPP
+    top2_dpp<0xB1>(k1, k2);   // quad_perm [1,0,3,2]
+    top2_dpp<0x4E>(k1, k2);   // quad_perm [2,3,0,1]
+    top2_dpp<0x141>(k1, k2);  // row_half_mirror
+    top2_dpp<0x140>(k1, k2);  // row_mirror
+    top2_swap<16>(k1, k2);
+    top2_swap<32>(k1, k2);
+#else
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
       const unsigned long long o1 = __shfl_xor(k1, off);
       const unsigned long long o2 = __shfl_xor(k2, off);
       top2(k1, k2, o1, o2);
     }
+#endif
     if (k2 == ~0ull) break;
     const int v1 = 256 - (int)(k1 & 511), v2 = 256 - (int)(k2 & 511);
     const uint32_t fs = (uint32_t)(k1 >> 9) + (uint32_t)(k2 >> 9);
@@ -1492,6 +1548,9 @@ __device__ void build_table_wave(const uint32_t *hist, const uint32_t *extra, Hu
         gr[i] = v1;
       }
     }
+    // (Measured and dropped: chain tails kept in registers and read with
+    // readlane instead of this LDS round trip + wave sync: 0.066 -> 0.088 ms
+    // per config-3 launch, the VALU->SGPR hand-offs cost more than the LDS.)
     if (lane == 0) {
       const int t1 = S->tail[v1];
       S->next[t1] = v2;

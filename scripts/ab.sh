@@ -6,6 +6,6 @@ mkdir -p gpurun_out
 for r in $(seq ${ROUNDS:-3}); do
   for lib in $LIBS; do
     MIJ_LIB=$PWD/$lib timeout -k 10 300 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --verify 0 ${ARGS:-} > gpurun_out/ab.log 2>&1 || { echo "$lib failed"; tail -5 gpurun_out/ab.log; exit 1; }
-    python3 -c "import json,sys;d=json.loads(open('gpurun_out/ab.log').read().strip().splitlines()[-1]);s=d['stages_ms'];print(sys.argv[1], round(d['ms_per_step'],3), 'k1', s['k1_colour_dct_quant'], 'tok', s.get('tokenize'), 'pack', s.get('pack'), 'emit', s.get('emit'))" $lib
+    python3 -c "import json,sys;d=json.loads(open('gpurun_out/ab.log').read().strip().splitlines()[-1]);s=d['stages_ms'];print(sys.argv[1], round(d['ms_per_step'],3), 'k1', s['k1_colour_dct_quant'], 'tok', s.get('tokenize'), 'pack', s.get('pack'), 'emit', s.get('emit'), 'tables', s.get('tables'))" $lib
   done
 done
