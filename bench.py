@@ -494,22 +494,45 @@ def verify_batch(batch, frames, F, args, rank):
     return n, pinned
 
 
-def util_counters(kernel_sym):
+UTIL_KEYS = ("width", "height", "frames_per_gpu", "quality", "mode", "pipeline")
+
+
+def util_counters(kernel_sym, config):
     """VALU / MFMA utilisation of `kernel_sym` from the newest profiles/rNN/util.json
-    (scripts/pmc_util.sh + scripts/util.py: rocprofv3 PMC passes of this bench's
-    default workload).  mfma_util = matrix-pipe busy cycles / (1024 SIMDs x
-    cycles) -- 1.0 is the dense i8 peak at the clock held; valu_util = VALU
-    issue slots used (2 cycles per wave64 instruction) / available."""
+    (scripts/pmc_util.sh + scripts/util.py: rocprofv3 PMC passes of a bench
+    run) whose recorded workload matches `config` (size, frames, quality,
+    mode, pipeline); (None, None) when none does.  mfma_util = matrix-pipe
+    busy cycles / (1024 SIMDs x cycles) -- 1.0 is the dense i8 peak at the
+    clock held; valu_util = VALU issue slots used (2 cycles per wave64
+    instruction) / available.  Everything attached comes from that one
+    profiled run (its counters and its own launch time)."""
     import glob
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "util.json")), reverse=True):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
+        if any(d.get("config", {}).get(k) != config.get(k) for k in UTIL_KEYS):
+            continue
         for name, v in d.get("kernels", {}).items():
             if kernel_sym in name:
                 return v, os.path.relpath(path, REPO)
     return None, None
+
+
+def util_fields(u, src):
+    """The roofline fields of one util.json kernel entry (util_counters)."""
+    r = {"mfma_util": u.get("mfma_util"), "valu_util": u.get("valu_util"),
+         "util_source": f"{src} (rocprofv3 PMC: SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU, "
+                        f"GRBM_GUI_ACTIVE; same workload)"}
+    if u.get("SQ_INSTS_MFMA") and u.get("launch_us"):
+        # v_mfma_i32_16x16x64_i8: 16*16*64 MACs = 32768 int8 ops each; dense
+        # i8 peak 5 POP/s (MI355X_MICROARCH.md, 2x bf16's 2.5 PF); counts and
+        # time both from the profiled run
+        tops = u["SQ_INSTS_MFMA"] * 32768 / (u["launch_us"] * 1e-6) / 1e12
+        r["mfma_i8_TOPs"] = round(tops, 1)
+        r["mfma_frac_of_i8_peak"] = round(tops / 5000.0, 4)
+    return r
 
 
 # rocprofv3 symbol of each K1 variant (for the PMC traffic lookup)
@@ -719,7 +742,10 @@ def main():
                      "achieved": round(k1_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(k1_gbs / HBM_PEAK_GBS, 4), "traffic": None,
                      "ms_per_launch": round(dom_ms, 4),
-                     "algorithmic_bytes_per_launch": int(k1_bytes)},
+                     "algorithmic_bytes_per_launch": int(k1_bytes),
+                     # SURVEY §8(d)'s unit: 6 B per image pixel (3 B BGR in +
+                     # 3 B int16 coefficients out), whatever the kernel moves
+                     "frac_8d_6Bpx": round(6 * px_step / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "kernels": {k: {"ms": round(v[1], 4), "algorithmic_GB": round(v[0] / 1e9, 3),
                         "GB_per_s": round(v[0] / (v[1] * 1e-3) / 1e9, 1)}
                     for k, v in kernels.items()},
@@ -739,22 +765,12 @@ def main():
             "frac": round(cb / (coef_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "ms_per_launch": round(coef_ms, 4), "algorithmic_bytes_per_launch": int(cb),
             "launches": args.coef_launches}
-        u1, usrc1 = util_counters("k_mcu_dct<1>")
+        u1, usrc1 = util_counters("k_mcu_dct<1>", res["config"])
         if u1 is not None:
-            res["roofline_k1_coefficient_variant"].update(
-                mfma_util=u1.get("mfma_util"), valu_util=u1.get("valu_util"), util_source=usrc1)
-    u, usrc = util_counters(K1_SYMBOL.get(dom, dom))
+            res["roofline_k1_coefficient_variant"].update(util_fields(u1, usrc1))
+    u, usrc = util_counters(K1_SYMBOL.get(dom, dom), res["config"])
     if u is not None:
-        res["roofline"]["mfma_util"] = u.get("mfma_util")
-        res["roofline"]["valu_util"] = u.get("valu_util")
-        res["roofline"]["util_source"] = (f"{usrc} (rocprofv3 PMC: SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU, "
-                                          f"GRBM_GUI_ACTIVE; same workload)")
-        if u.get("SQ_INSTS_MFMA"):
-            # v_mfma_i32_16x16x64_i8: 16*16*64 MACs = 32768 int8 ops each;
-            # dense i8 peak 5 POP/s (MI355X_MICROARCH.md, 2x bf16's 2.5 PF)
-            tops = u["SQ_INSTS_MFMA"] * 32768 / (dom_ms * 1e-3) / 1e12
-            res["roofline"]["mfma_i8_TOPs"] = round(tops, 1)
-            res["roofline"]["mfma_frac_of_i8_peak"] = round(tops / 5000.0, 4)
+        res["roofline"].update(util_fields(u, usrc))
     traffic, src = pmc_traffic(dom, res["config"])
     if traffic is not None:
         res["roofline"]["traffic"] = traffic

@@ -28,7 +28,6 @@ hipError_t launch_tables(const EntArgs &a, hipStream_t s);
 hipError_t launch_ehuf_struct(const HuffCode *hc, uint32_t *ehuf, hipStream_t s);
 hipError_t launch_bits(const EntArgs &a, hipStream_t s);
 hipError_t launch_scan(const EntArgs &a, hipStream_t s);
-hipError_t launch_pack(const EntArgs &a, hipStream_t s);
 hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s);
 hipError_t launch_emit(const EntArgs &a, hipStream_t s);
 hipError_t launch_or_words(uint32_t *dst, const uint32_t *src, long long n, hipStream_t s);
@@ -277,8 +276,10 @@ struct mij_batch {
   uint8_t *d_frame = nullptr;
   size_t frame_cap = 0;
   // k_pack_lb needs all-zero scan buffers; k_emit_write leaves them so, the
-  // band paths (k_scan + k_pack, no emit) do not
-  bool raw_dirty = false;
+  // band paths (k_scan + k_pack_lb, no emit) and the assembler's ORed words
+  // before mij_assemble_end do not.  raw_dirty = frames 0..raw_dirty-1 may
+  // hold words (0: every scan buffer is zero)
+  int raw_dirty = 0;
   bool keep_coefs = false;  // encode also writes coefficient planes
   bool rgb = false;         // input frames in R, G, B byte order (PPM) instead of B, G, R
   bool split = false;       // true: K1 writes coefficients, a second pass tokenizes;
@@ -442,13 +443,33 @@ extern "C" void mij_batch_destroy(mij_batch *b) { batch_free(b); }
 
 extern "C" void *mij_batch_stream(mij_batch *b) { return b ? (void *)b->stream : nullptr; }
 
+// slots first..first+n-1 hold canvas-sized frames again; a region batch
+// whose slots are then all canvas-sized is a plain batch
+static int canvas_frames(mij_batch *b, int first, int n) {
+  if (!b->use_fdims) return MIJ_OK;
+  const int2 cv = make_int2(b->g.w, b->g.h);
+  for (int i = first; i < first + n; i++) b->h_fdims[i] = cv;
+  bool all = true;
+  for (const int2 &d : b->h_fdims) all = all && d.x == cv.x && d.y == cv.y;
+  if (all) {
+    b->use_fdims = false;
+    return MIJ_OK;
+  }
+  HIP_TRY(hipMemcpyAsync(b->d_fdims + first, b->h_fdims.data() + first, sizeof(int2) * n,
+                         hipMemcpyHostToDevice, b->stream));
+  HIP_TRY(hipStreamSynchronize(b->stream));  // pageable source
+  return MIJ_OK;
+}
+
 extern "C" int mij_batch_upload(mij_batch *b, const uint8_t *bgr, int first, int nframes) {
   if (pipe_check(b, "upload")) return g_err;
   if (!bgr || first < 0 || nframes < 1 || first + nframes > b->cap)
     return fail(MIJ_EINVAL, "upload: bad args");
   if (!b->own_in) return fail(MIJ_EINVAL, "upload: batch reads external device input");
   HIP_TRY(hipSetDevice(b->dev));
-  b->use_fdims = false;  // full frames: the batch geometry again (set_frame_dims after, if wanted)
+  // full frames: the uploaded slots are canvas-sized again (set_frame_dims
+  // after, if wanted); the other slots keep their sizes
+  if (canvas_frames(b, first, nframes)) return g_err;
   HIP_TRY(hipMemcpyAsync(b->d_in + (long long)first * b->in_fs, bgr, (size_t)nframes * b->in_fs,
                          hipMemcpyHostToDevice, b->stream));
   HIP_TRY(hipStreamSynchronize(b->stream));
@@ -639,8 +660,8 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   if (t) HIP_TRY(hipEventRecord(b->ev[5], st));
   // segment bits, scan offsets and packing in one look-back pass
   if (b->raw_dirty) {
-    HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->cap * b->g.raw_fs, st));
-    b->raw_dirty = false;
+    HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->raw_dirty * b->g.raw_fs, st));
+    b->raw_dirty = 0;
   }
   // diagnostics (MIJ_PACK_TIME with the diag build): per-group phase times of k_pack_lb
   static const bool ptime = getenv("MIJ_PACK_TIME") != nullptr;
@@ -730,13 +751,13 @@ extern "C" int mij_batch_encode(mij_batch *b, int nframes) {
 }
 
 extern "C" int mij_batch_keep_coefs(mij_batch *b, int on) {
-  if (!b) return fail(MIJ_EINVAL, "keep_coefs: null batch");
+  if (pipe_check(b, "keep_coefs")) return g_err;
   b->keep_coefs = on != 0;
   return MIJ_OK;
 }
 
 extern "C" int mij_batch_set_rgb(mij_batch *b, int on) {
-  if (!b) return fail(MIJ_EINVAL, "set_rgb: null batch");
+  if (pipe_check(b, "set_rgb")) return g_err;
   b->rgb = on != 0;
   return MIJ_OK;
 }
@@ -804,14 +825,16 @@ static int gather_regions(mij_batch *b, const uint8_t *d_src, long long src_pitc
 
 extern "C" int mij_batch_gather_regions(mij_batch *b, const void *d_frame, long long pitch, int frame_w,
                                         int frame_h, const area_t *regions, int n) {
-  if (!b || !d_frame || pitch < 3LL * frame_w) return fail(MIJ_EINVAL, "gather_regions: bad args");
+  if (pipe_check(b, "gather_regions")) return g_err;
+  if (!d_frame || pitch < 3LL * frame_w) return fail(MIJ_EINVAL, "gather_regions: bad args");
   HIP_TRY(hipSetDevice(b->dev));
   return gather_regions(b, (const uint8_t *)d_frame, pitch, frame_w, frame_h, regions, n);
 }
 
 extern "C" int mij_batch_upload_regions(mij_batch *b, const uint8_t *bgr, int stride_px, int frame_h,
                                         const area_t *regions, int n) {
-  if (!b || !bgr || stride_px < 16 || frame_h < 16) return fail(MIJ_EINVAL, "upload_regions: bad args");
+  if (pipe_check(b, "upload_regions")) return g_err;
+  if (!bgr || stride_px < 16 || frame_h < 16) return fail(MIJ_EINVAL, "upload_regions: bad args");
   HIP_TRY(hipSetDevice(b->dev));
   const size_t bytes = (size_t)stride_px * frame_h * 3;
   if (bytes > b->frame_cap) {
@@ -828,10 +851,11 @@ extern "C" int mij_batch_upload_regions(mij_batch *b, const uint8_t *bgr, int st
 // ---- asynchronous host transfers for the streaming engine (mij_stream.hip):
 // queued on the batch stream, no synchronisation
 int mij_batch_upload_async(mij_batch *b, const uint8_t *host, int nframes) {
-  if (!b || !host || nframes < 1 || nframes > b->cap || !b->own_in)
+  if (pipe_check(b, "upload_async")) return g_err;
+  if (!host || nframes < 1 || nframes > b->cap || !b->own_in)
     return fail(MIJ_EINVAL, "upload_async: bad args");
   HIP_TRY(hipSetDevice(b->dev));
-  b->use_fdims = false;
+  if (canvas_frames(b, 0, nframes)) return g_err;
   HIP_TRY(hipMemcpyAsync(b->d_in, host, (size_t)nframes * b->in_fs, hipMemcpyHostToDevice, b->stream));
   return MIJ_OK;
 }
@@ -851,7 +875,7 @@ int mij_batch_output_async(mij_batch *b, int frame, uint8_t *dst, size_t n) {
 }
 
 extern "C" int mij_batch_set_split(mij_batch *b, int on) {
-  if (!b) return fail(MIJ_EINVAL, "set_split: null batch");
+  if (pipe_check(b, "set_split")) return g_err;
   b->split = on != 0;
   return MIJ_OK;
 }
@@ -988,7 +1012,8 @@ extern "C" int mij_batch_output(mij_batch *b, int frame, uint8_t *dst, size_t ca
 
 extern "C" int mij_batch_coefs(mij_batch *b, int frame, int16_t *Y, int16_t *Cb, int16_t *Cr,
                                int diffed) {
-  if (!b || frame < 0 || frame >= b->cap) return fail(MIJ_EINVAL, "coefs: bad frame");
+  if (pipe_check(b, "coefs")) return g_err;
+  if (frame < 0 || frame >= b->cap) return fail(MIJ_EINVAL, "coefs: bad frame");
   HIP_TRY(hipSetDevice(b->dev));
   const Geom &g0 = b->g;
   // the frame's own planes (region batches: its w x h, not the canvas)
@@ -1339,8 +1364,8 @@ extern "C" int mij_band_pack(mij_batch *b, int n, const unsigned long long *bit_
   EntArgs a = ent_args(b, n);
   // k_pack_lb needs all-zero scan buffers: mij_band_words_all moves the band
   // words out and zeroes them; a band packed but never moved leaves them dirty
-  if (b->raw_dirty) HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->cap * b->g.raw_fs, b->stream));
-  b->raw_dirty = true;
+  if (b->raw_dirty) HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->raw_dirty * b->g.raw_fs, b->stream));
+  b->raw_dirty = n;
   HIP_TRY(launch_pack_lb(a, b->stream));
   std::vector<unsigned long long> tot((size_t)n * 3);
   HIP_TRY(hipMemcpyAsync(tot.data(), b->d_scan_bits, sizeof(uint64_t) * n * 3,
@@ -1416,9 +1441,10 @@ extern "C" int mij_band_words_all(mij_batch *b, int n, void *dst, size_t cap_wor
   if (!dst_on_device && total)
     HIP_TRY(hipMemcpyAsync(dst, d, total * 4, hipMemcpyDeviceToHost, b->stream));
   HIP_TRY(hipStreamSynchronize(b->stream));
-  // every word mij_band_pack wrote has left the buffers (a scan's words,
-  // its in-word start offset included, are its band_words)
-  b->raw_dirty = false;
+  // the words of frames 0..n-1 have left the buffers (a scan's words, its
+  // in-word start offset included, are its band_words); frames a wider
+  // mij_band_pack covered beyond n still hold theirs
+  if (n >= b->raw_dirty) b->raw_dirty = 0;
   return MIJ_OK;
 }
 
@@ -1466,6 +1492,8 @@ extern "C" int mij_assemble_begin(mij_batch *b, int n, const uint32_t *hist) {
   if (band_check(b, n, "assemble_begin", true)) return g_err;
   if (!hist) return fail(MIJ_EINVAL, "assemble_begin: null hist");
   HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * n * b->g.raw_fs, b->stream));
+  // the words ORed in before mij_assemble_end leave frames 0..n-1 dirty
+  b->raw_dirty = std::max(b->raw_dirty, n);
   return upload_hist_tables(b, n, hist);
 }
 
@@ -1499,7 +1527,8 @@ extern "C" int mij_assemble_end(mij_batch *b, int n, const unsigned long long *t
   HIP_TRY(hipMemcpyAsync(b->d_scan_bits, total_bits, sizeof(uint64_t) * n * 3,
                          hipMemcpyHostToDevice, b->stream));
   EntArgs a = ent_args(b, n);
-  HIP_TRY(launch_emit(a, b->stream));
+  HIP_TRY(launch_emit(a, b->stream));  // k_emit_write zeroes the words it reads
+  if (n >= b->raw_dirty) b->raw_dirty = 0;
   b->last_frames = n;
   return MIJ_OK;
 }

@@ -13,7 +13,7 @@
 //   k_ehuf_struct  code tables from caller-owned huff_code structs
 //   k_seg_bits     bits per segment
 //   k_scan         per-scan offsets of each segment
-//   k_pack         bit packing of segment groups in LDS (:434-502)
+//   k_pack_lb      segment bits + look-back offsets + bit packing (:434-502)
 //   k_emit         JFIF assembly + 0xFF stuffing + pad quirks (:383-432,
 //                  :504-644)
 //
@@ -1766,7 +1766,7 @@ __global__ __launch_bounds__(256) void k_seg_bits(EntArgs a) {
 // ===========================================================================
 // k_scan: per scan (frame, component) exclusive scan of segment bits; zeroes
 // the first/last word of every pack group (shared with neighbour groups and
-// OR-combined by k_pack).  One wave per scan.
+// OR-combined by k_pack_lb).  One wave per scan.
 // ===========================================================================
 __global__ void k_scan(EntArgs a) {
   const int sid = blockIdx.x;  // frame * 3 + comp
@@ -1799,11 +1799,7 @@ __global__ void k_scan(EntArgs a) {
 }
 
 // ===========================================================================
-// k_pack: bit-pack a group of PACK_SEGS consecutive segments of one scan in
-// LDS, then store it.  A wave takes a segment; lanes take its tokens, place
-// them at the segment offset + a wave-wide exclusive scan of token bits, and
-// OR the pieces into LDS words (big-endian bit order).  Interior words are
-// stored plainly, the group's first/last word atomically (k_scan zeroed them).
+// Bit placement helpers of k_pack_lb's window paths (big-endian bit order).
 // ===========================================================================
 __device__ __forceinline__ void put_bits(uint32_t *buf, uint32_t pos, uint32_t val, int len) {
   // len in 1..28, val < 2^len
@@ -1827,95 +1823,6 @@ __device__ __forceinline__ void put_bits_window(uint32_t *buf, uint32_t pos, uin
   } else {
     if (w >= wl && w < wh) atomicOr(&buf[w - wl], val >> (-sh));
     if (w + 1 >= wl && w + 1 < wh) atomicOr(&buf[w + 1 - wl], val << (32 + sh));
-  }
-}
-
-__global__ __launch_bounds__(256) void k_pack(EntArgs a) {
-  __shared__ uint32_t buf[PACK_WORDS];
-  __shared__ uint32_t tab[2][256];  // this component's DC and AC codes
-  const Geom &G = a.g;
-  const int gy = (G.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (G.nsc + PACK_SEGS - 1) / PACK_SEGS;
-  const int gpf = gy + 2 * gc;
-  const int f = blockIdx.x / gpf;
-  int q = blockIdx.x - f * gpf, comp, sbase, ns;
-  if (q < gy) {
-    comp = 0; sbase = 0; ns = G.nsy;
-  } else {
-    q -= gy;
-    comp = 1 + (q >= gc);
-    if (q >= gc) q -= gc;
-    sbase = comp == 1 ? G.nsy : G.nsy + G.nsc;
-    ns = G.nsc;
-  }
-  const int chroma = comp != 0;
-  const int s0 = q * PACK_SEGS, s1 = min(ns, s0 + PACK_SEGS);
-  const long long fs0 = (long long)f * G.nseg + sbase;
-  for (int i = threadIdx.x; i < 512; i += 256)
-    tab[i >> 8][i & 255] = a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + i];
-  const unsigned long long gbase = a.seg_off[fs0 + s0];
-  const unsigned long long gend = a.seg_off[fs0 + s1 - 1] + a.seg_bits[fs0 + s1 - 1];
-  const uint32_t bit0 = (uint32_t)(gbase & 31);
-  uint32_t nw = (uint32_t)((bit0 + (gend - gbase) + 31) >> 5);  // words of the group
-  if ((gbase >> 5) + nw + 1 > (unsigned long long)G.raw_words[comp]) {  // cannot happen for valid
-    if (threadIdx.x == 0) a.err[f] = 2;                                 // tokens; never write OOB
-    nw = 0;
-  }
-  uint32_t *raw = a.raw + (long long)f * G.raw_fs +
-                  (comp == 0 ? 0 : G.raw_words[0] + (comp == 2 ? G.raw_words[1] : 0)) +
-                  (gbase >> 5);
-  // 16 lanes (one DPP row) per segment, 16 segments in flight per workgroup
-  const int sub = threadIdx.x & 15, row = threadIdx.x >> 4;
-  __syncthreads();
-  const uint32_t zac = tab[1][0xF0];
-  const int Lz = (int)(zac >> 16);
-  // window [w0, w0 + PACK_WORDS) of the group's words per pass
-  for (uint32_t w0 = 0; w0 < nw; w0 += PACK_WORDS) {
-    const uint32_t wn = min((uint32_t)PACK_WORDS, nw - w0);
-    const uint32_t lo_bit = w0 * 32, hi_bit = (w0 + wn) * 32;
-    for (uint32_t i = threadIdx.x; i < wn; i += 256) buf[i] = 0;
-    __syncthreads();
-    for (int s = s0 + row; s < s1; s += 16) {
-      const long long fs = fs0 + s;
-      const uint32_t sb = bit0 + (uint32_t)(a.seg_off[fs] - gbase);
-      if (sb >= hi_bit || sb + a.seg_bits[fs] <= lo_bit) continue;  // row-uniform
-      const int n = min((int)a.seg_ntok[fs], SEG_TOK);
-      const uint32_t *tk = a.tok + fs * SEG_TOK;
-      uint32_t pos0 = sb;
-      uint32_t tq[4];  // tokens of the next 64, loaded ahead (latency-bound loop)
-#pragma unroll
-      for (int u = 0; u < 4; u++) tq[u] = 16 * u + sub < n ? tk[16 * u + sub] : 0u;
-      if (sub == 0) tq[0] = a.tok0[fs];  // token 0
-      for (int i0 = 0; i0 < n; i0 += 16) {
-        const int i = i0 + sub;
-        const uint32_t t = tq[0];
-        tq[0] = tq[1];
-        tq[1] = tq[2];
-        tq[2] = tq[3];
-        tq[3] = i + 64 < n ? tk[i + 64] : 0u;
-        const uint32_t sym = t & 255u, cls = sym & 15u;
-        const uint32_t e = i < n ? tab[(t & TOK_AC) ? 1 : 0][sym] : 0u;
-        const uint32_t nz = (t >> 8) & 3u;
-        const uint32_t L = (e >> 16) + cls;
-        const uint32_t nb = i < n ? L + nz * (uint32_t)Lz : 0u;
-        const uint32_t x = row_scan16(nb);
-        uint32_t pos = pos0 + x - nb;
-        if (nb && pos < hi_bit && pos + nb > lo_bit) {
-          for (uint32_t k = nz; k; k--) {  // encoder.c:490-494 ZRL
-            put_bits_window(buf, pos, lo_bit, hi_bit, zac & 0xFFFFu, Lz);
-            pos += Lz;
-          }
-          if (L) put_bits_window(buf, pos, lo_bit, hi_bit, ((e & 0xFFFFu) << cls) | (t >> 16), (int)L);
-        }
-        pos0 += __shfl(x, 15, 16);
-      }
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < wn; i += 256) {
-      const uint32_t wi = w0 + i;
-      if (wi == 0 || wi == nw - 1) atomicOr(&raw[wi], buf[i]);
-      else raw[wi] = buf[i];
-    }
-    __syncthreads();
   }
 }
 
@@ -2667,7 +2574,6 @@ __global__ void k_or_pieces(uint32_t *raw, long long raw_fs, long long rw0, long
   }
 }
 
-// ---- tiny self-test used by the test-suite: exact i8 MFMA layout check ----
 // Band words out of the scan buffers, zeroed behind them (k_pack_lb needs
 // all-zero buffers): piece blockIdx.y = {frame * 3 + scan, words, first
 // destination word}, from the start of the scan.
@@ -2683,6 +2589,7 @@ __global__ void k_move_pieces(uint32_t *raw, long long raw_fs, long long rw0, lo
     src[i] = 0u;
   }
 }
+// ---- tiny self-test used by the test-suite: exact i8 MFMA layout check ----
 __global__ void k_mfma_probe(const int4 *A, const int4 *B, int4 *D) {
   const int lane = threadIdx.x;
   const int4 a4 = A[lane], b4 = B[lane];
@@ -2824,11 +2731,6 @@ hipError_t launch_move_pieces(uint32_t *raw, const Geom &g, uint32_t *dst,
   return hipGetLastError();
 }
 
-hipError_t launch_pack(const EntArgs &a, hipStream_t s) {
-  const int gy = (a.g.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (a.g.nsc + PACK_SEGS - 1) / PACK_SEGS;
-  hipLaunchKernelGGL(k_pack, dim3(a.nframes * (gy + 2 * gc)), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
 hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s) {
   const int gy = (a.g.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (a.g.nsc + PACK_SEGS - 1) / PACK_SEGS;
   const long long groups = (long long)a.nframes * (gy + 2 * gc);

@@ -354,7 +354,12 @@ class Batch:
         frames_bgr = np.ascontiguousarray(frames_bgr, np.uint8)
         n = frames_bgr.shape[0] if frames_bgr.ndim == 4 else 1
         _check(self.lib.mij_batch_upload(self.h_, _ptr(frames_bgr), first, n), "upload")
-        self.fdims = None  # full frames: the library restored the batch geometry
+        # full frames: the uploaded slots are canvas-sized again, the others
+        # keep their region sizes (as the library does)
+        if self.fdims is not None:
+            dims = list(self.fdims) + [(self.w, self.h)] * max(0, self.max_frames - len(self.fdims))
+            dims[first:first + n] = [(self.w, self.h)] * n
+            self.fdims = None if all(d == (self.w, self.h) for d in dims) else dims
 
     def set_input(self, dev_ptr: int, frame_stride: int, pitch: int) -> None:
         _check(self.lib.mij_batch_set_input(self.h_, dev_ptr, frame_stride, pitch), "set_input")

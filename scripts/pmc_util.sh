@@ -23,4 +23,7 @@ done <<'G'
 GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE
 GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES
 G
+python3 -c "
+import json; d=json.loads(open('$out/p1.log').read().strip().splitlines()[-1])
+json.dump(d['config'], open('$out/config.json','w'))"
 python3 scripts/util.py "$out" "$out/util.json"

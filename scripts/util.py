@@ -69,7 +69,14 @@ for k, cs in acc.items():
                 e[name] = round(m[c] / wc, 4)
     res[k] = e
 
-json.dump({"method": __doc__.strip(), "kernels": res}, open(out, "w"), indent=1)
+# the profiled bench run's workload (scripts/pmc_util.sh writes it from the
+# first pass's bench line): bench.py attaches these numbers only to a run of
+# the same workload
+meta = {}
+mf = os.path.join(d, "config.json")
+if os.path.exists(mf):
+    meta = json.load(open(mf))
+json.dump({"config": meta, "method": __doc__.strip(), "kernels": res}, open(out, "w"), indent=1)
 for k, e in sorted(res.items(), key=lambda kv: -kv[1]["launch_us"])[:10]:
     print(f"{k[:44]:44s} {e['launch_us']:9.1f} us  mfma {e.get('mfma_util', float('nan')):.3f}  "
           f"valu {e.get('valu_util', float('nan')):.3f}  busy {e.get('valu_busy', float('nan')):.3f}  "

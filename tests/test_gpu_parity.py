@@ -281,19 +281,57 @@ def test_fused_pipeline_keep_coefs_golden(manifest):
     b.close()
 
 
+def _luma_group_bits(Y, tabs, W, H, group, tiles_x):
+    """Exact bits of luma pack group `group` (PACK_SEGS = 64 segments; a
+    segment is 16 blocks of one block row inside one 128-px tile column),
+    from the oracle's differenced coefficients and tables (encoder.c:434-502)."""
+    dc, ac = tabs[0], tabs[1]
+    bw, bh = W // 8, H // 8
+    Yb = Y.reshape(bh * bw, 64)
+    bits = 0
+    for s in range(64 * group, min(64 * (group + 1), bh * tiles_x)):
+        r, tx = divmod(s, tiles_x)
+        for bx in range(16 * tx, min(16 * tx + 16, bw)):
+            blk = Yb[r * bw + bx]
+            d = int(blk[0])
+            c = abs(d).bit_length()
+            bits += dc.sym_code_len[c] + c
+            nz = np.flatnonzero(blk[1:]) + 1
+            prev = 0
+            for z in nz:
+                run = int(z) - prev - 1
+                c = abs(int(blk[z])).bit_length()
+                bits += (run >> 4) * ac.sym_code_len[0xF0] + ac.sym_code_len[((run & 15) << 4) | c] + c
+                prev = int(z)
+            if blk[63] == 0:
+                bits += ac.sym_code_len[0x00]
+    return bits
+
+
 @pytest.mark.parametrize("q", [50, 100])
-def test_pack_staged_and_unstaged_groups_in_one_scan(q):
-    """k_pack_lb stages a pack group's tokens in LDS when they fit and packs
-    from HBM otherwise: noise rows (thousands of tokens per group at high Q)
-    next to natural rows and flat rows in one scan, so both kinds of groups
-    and the seams between them land in the same bitstream."""
+def test_pack_window_paths_in_one_scan(q):
+    """k_pack_lb's two placement paths in one scan (both at Q=100, the
+    single-window one alone at Q=50): a pack group whose bits fit one LDS
+    window (PACK_WORDS = 4096 words) is placed relative to its own
+    first bit and stored after the look-back; a wider one (noise rows: its
+    bits are asserted to exceed the window) takes the look-back first and is
+    packed window by window at absolute offsets (put_bits64_win, tokens
+    reloaded per window).  Natural and flat rows follow in the same scan, so
+    the seams between both kinds of groups land in one bitstream."""
     rng = np.random.default_rng(q)
     W, H = 1920, 96
     nat = ppm.rgb_to_bgr(np.tile(recipes.sample("sample_640x640"), (1, 3, 1))[:32, :W])
     img = np.concatenate([rng.integers(0, 256, (32, W, 3), dtype=np.uint8), nat,
                           np.full((32, W, 3), 77, np.uint8)])
-    b = mijpeg.Batch(W, H, 2, q)
     frames = np.stack([img, img[::-1].copy()])
+    # frame 0's first luma group (noise) is wider than one window at Q=100
+    # (516k bits) and fits one at Q=50 (124k); frame 1's first (flat) fits
+    Y, _, _, tabs, _ = O.cref_stages(frames[0], q)
+    wide = _luma_group_bits(Y, tabs, W, H, 0, (W + 127) // 128) > 4096 * 32
+    assert wide == (q == 100)
+    Y1, _, _, tabs1, _ = O.cref_stages(frames[1], q)
+    assert _luma_group_bits(Y1, tabs1, W, H, 0, (W + 127) // 128) < 4096 * 32
+    b = mijpeg.Batch(W, H, 2, q)
     b.upload(frames)
     b.encode(2)
     for i in range(2):
