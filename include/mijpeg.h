@@ -88,6 +88,9 @@ enum {
 };
 int mij_last_error(void);
 const char *mij_strerror(int code);
+/* Text of the calling thread's last failure ("" before any): what was wrong
+ * with which argument, beyond the code mij_last_error returns. */
+const char *mij_last_message(void);
 
 /* Worst-case size of an encoded w x h frame (all 63 AC coefficients coded at
  * 27 bits, every byte stuffed). */
@@ -284,6 +287,12 @@ int mij_probe_mfma(const int8_t *A, const int8_t *B, int32_t *D);
  * (R<<7 | G>>1) of table 0 (Y), (G<<7 | B>>1) of table 1 (Cb, R == G),
  * (G<<7 | R>>1) of table 2 (Cr, B == G); see DESIGN.md */
 int mij_colour_lut(uint32_t *out);
+/* Tests: runs the coefficient K1 (as mij_batch_dct) on frames 0..n-1 of a
+ * plain B, G, R batch through its audit variant and copies out every
+ * block's fast-path decisions: masks[(f * nblk + blk) * 4 + g] bit k set =
+ * zigzag coefficient 16 g + k straddled a truncation boundary (replayed in
+ * FP64), blocks in the batch's coefficient order (Y, Cb, Cr). */
+int mij_batch_audit(mij_batch *b, int nframes, uint16_t *masks);
 /* name of the code object target the library was built for ("gfx950") */
 const char *mij_build_target(void);
 

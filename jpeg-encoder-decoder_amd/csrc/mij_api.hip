@@ -48,11 +48,14 @@ using namespace mij;
 // ---------------------------------------------------------------------------
 static thread_local int g_err = MIJ_OK;
 
+static thread_local char g_msg[256];  // text of this thread's last failure
 static int vfail(int code, const char *fmt, va_list ap) {
   g_err = code;
-  fprintf(stderr, "mijpeg: ");
-  vfprintf(stderr, fmt, ap);
-  fprintf(stderr, "\n");
+  va_list aq;
+  va_copy(aq, ap);
+  vsnprintf(g_msg, sizeof g_msg, fmt, aq);
+  va_end(aq);
+  fprintf(stderr, "mijpeg: %s\n", g_msg);
   return code;
 }
 static int fail(int code, const char *fmt, ...) {
@@ -80,6 +83,8 @@ void mij_clear_error() { g_err = MIJ_OK; }
   } while (0)
 
 extern "C" int mij_last_error(void) { return g_err; }
+
+extern "C" const char *mij_last_message(void) { return g_msg; }
 
 extern "C" const char *mij_strerror(int code) {
   switch (code) {
@@ -254,8 +259,10 @@ struct mij_batch {
   uint32_t *d_choff = nullptr;    // k_emit_scan: output offset per scan chunk
   unsigned long long *d_pack_state = nullptr;  // k_pack_lb look-back words, per pack group
   unsigned *d_pack_ticket = nullptr;
-  uint32_t *d_fix = nullptr;      // K1 fix list (frame * nblk + block), worst case every block
-  unsigned *d_fix_count = nullptr;
+  uint16_t *d_fixmask = nullptr;  // K1 fix masks: per N-tile (tile * 3 + nt), zero between launches
+  uint16_t *d_audit = nullptr;    // mij_batch_audit: per frame, block, lane group 16 straddle bits
+  size_t audit_cap = 0;
+  bool audit = false;             // the next coefficient K1 launch is the audit variant
   // bands of one large frame (mij_band_*, mij_assemble_*): per frame [4]
   int16_t *d_dcpred = nullptr;
   uint32_t *d_bitbase = nullptr;
@@ -308,7 +315,7 @@ static void batch_free(mij_batch *b) {
   void *ptrs[] = {b->d_tab, b->own_in ? b->d_in : nullptr, b->d_coef, b->d_dc, b->d_hist,
                   b->d_ehuf, b->d_raw, b->d_tok, b->d_tok0, b->d_seg_ntok, b->d_seg_bits, b->d_seg_off,
                   b->d_scan_bits, b->d_out_len, b->d_hc, b->d_out, b->d_err, b->d_replays,
-                  b->d_dcpred, b->d_bitbase, b->d_stage, b->d_fix, b->d_fix_count, b->d_ffc, b->d_choff,
+                  b->d_dcpred, b->d_bitbase, b->d_stage, b->d_fixmask, b->d_audit, b->d_ffc, b->d_choff,
                   b->d_pack_state, b->d_pack_ticket, b->d_fdims, b->d_frame, b->d_regions, b->d_pieces};
   for (void *p : ptrs)
     if (p) hipFree(p);
@@ -368,10 +375,10 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
     HIP_TRY(dalloc(&b->d_seg_ntok, F * g.nseg));
     HIP_TRY(dalloc(&b->d_seg_bits, F * g.nseg));
     HIP_TRY(dalloc(&b->d_seg_off, F * g.nseg));
-    HIP_TRY(dalloc(&b->d_fix, F * g.nblk));
+    HIP_TRY(dalloc(&b->d_fixmask, F * g.tiles_per_frame * 3));
+    HIP_TRY(hipMemsetAsync(b->d_fixmask, 0, sizeof(uint16_t) * F * g.tiles_per_frame * 3, b->stream));
     HIP_TRY(dalloc(&b->d_pack_state, F * ((g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((g.nsc + PACK_SEGS - 1) / PACK_SEGS))));
     HIP_TRY(dalloc(&b->d_pack_ticket, F * 3));  // one per scan
-    HIP_TRY(dalloc(&b->d_fix_count, 1));
     HIP_TRY(dalloc(&b->d_regions, F));
   }
   HIP_TRY(dalloc(&b->d_hist, F * 4 * 257));
@@ -493,7 +500,10 @@ extern "C" int mij_batch_set_input(mij_batch *b, const void *d_bgr, long long fr
   return MIJ_OK;
 }
 
-static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0) {
+// band: the mij_band_* calls, whose per-frame DC predictors and in-word scan
+// start bits live in d_dcpred / d_bitbase; every other pipeline reads both as
+// 0 (null), so a band call leaves no state behind for the next encode
+static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0, bool band = false) {
   EntArgs a;
   memset(&a, 0, sizeof(a));
   a.g = b->g;
@@ -514,8 +524,8 @@ static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0) {
   a.out = b->d_out;
   a.out_len = b->d_out_len;
   a.err = b->d_err;
-  a.dc_pred = b->d_dcpred;
-  a.bit_base = b->d_bitbase;
+  a.dc_pred = band ? b->d_dcpred : nullptr;
+  a.bit_base = band ? b->d_bitbase : nullptr;
   a.ffc = b->d_ffc;
   a.choff = b->d_choff;
   a.pack_state = b->d_pack_state;
@@ -544,8 +554,8 @@ static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0) {
     a.out += F * g.out_cap;
     a.out_len += F;
     a.err += F;
-    a.dc_pred += F * 4;
-    a.bit_base += F * 4;
+    if (a.dc_pred) a.dc_pred += F * 4;
+    if (a.bit_base) a.bit_base += F * 4;
     a.ffc += F * 3 * emit_chunks(g);
     a.choff += F * 3 * emit_chunks(g);
     a.pack_state += F * gpf;
@@ -574,8 +584,8 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int se
   k.tok0 = b->d_tok0;
   k.seg_ntok = b->d_seg_ntok;
   k.hist = b->d_hist;
-  k.fix_list = b->d_fix;
-  k.fix_count = b->d_fix_count;
+  k.fix_mask = b->d_fixmask;
+  k.audit = b->audit && mode == 1 ? b->d_audit : nullptr;
   k.rgb = b->rgb && (mode & 4) == 0;  // pixel-input variants
   k.fdims = b->use_fdims ? b->d_fdims : nullptr;
   if (f0) {  // sub-batch: frames f0.. (per-frame arrays shifted; mode 2 only)
@@ -600,40 +610,44 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int se
   k.per_wg = (int)per_wg;
   k.dc_diffed = dc_diffed;
   k.seg_dc_inline = seg_dc_inline;
-  // the coefficient variant lists hazard blocks; k_fix_blocks recomputes
-  // them in FP64 right after it, on the same stream
-  if (mode == 1) HIP_TRY(hipMemsetAsync(b->d_fix_count, 0, sizeof(unsigned), b->stream));
+  // the coefficient variant marks hazard blocks in the fix masks;
+  // k_fix_blocks recomputes them in FP64 right after it, on the same stream
   // diagnostics (MIJ_K1_WTIME with the diag build): per-wave lifetimes of K1
   static const bool wtime = getenv("MIJ_K1_WTIME") != nullptr;
   unsigned long long *d_wt = nullptr;
   const long long nw = grid * 16;
   if (wtime && (mode == 1 || mode == 2)) {
-    HIP_TRY(hipMalloc(&d_wt, sizeof(unsigned long long) * 3 * nw));
-    HIP_TRY(hipMemsetAsync(d_wt, 0, sizeof(unsigned long long) * 3 * nw, b->stream));
+    HIP_TRY(hipMalloc(&d_wt, sizeof(unsigned long long) * K1_WTIME_WORDS * nw));
+    HIP_TRY(hipMemsetAsync(d_wt, 0, sizeof(unsigned long long) * K1_WTIME_WORDS * nw, b->stream));
     k.wtime = d_wt;
   }
   HIP_TRY(launch_k1(k, (int)grid, mode, b->stream));
   if (d_wt) {
-    std::vector<unsigned long long> h(3 * nw);
-    HIP_TRY(hipMemcpyAsync(h.data(), d_wt, sizeof(unsigned long long) * 3 * nw, hipMemcpyDeviceToHost, b->stream));
+    const int WW = K1_WTIME_WORDS;
+    std::vector<unsigned long long> h(WW * nw);
+    HIP_TRY(hipMemcpyAsync(h.data(), d_wt, sizeof(unsigned long long) * WW * nw, hipMemcpyDeviceToHost, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
     HIP_TRY(hipFree(d_wt));
     unsigned long long s0 = ~0ull, e1 = 0, e0 = ~0ull;
-    double sum = 0, smin = 1e30, smax = 0;
+    double sum = 0, smin = 1e30, smax = 0, ph[5] = {0, 0, 0, 0, 0};
     long long n = 0, tiles = 0;
     for (long long i = 0; i < nw; i++) {
-      if (!h[3 * i + 1]) continue;
-      const unsigned long long a0 = h[3 * i], a1 = h[3 * i + 1];
+      if (!h[WW * i + 1]) continue;
+      const unsigned long long a0 = h[WW * i], a1 = h[WW * i + 1];
       s0 = std::min(s0, a0); e1 = std::max(e1, a1); e0 = std::min(e0, a1);
       const double d = (double)(a1 - a0);
-      sum += d; smin = std::min(smin, d); smax = std::max(smax, d); n++; tiles += (long long)h[3 * i + 2];
+      sum += d; smin = std::min(smin, d); smax = std::max(smax, d); n++; tiles += (long long)h[WW * i + 2];
+      for (int k = 0; k < 5; k++) ph[k] += (double)h[WW * i + 3 + k];
     }
     if (const char *path = getenv("MIJ_K1_WTIME_DUMP")) {  // raw per-wave records
-      if (FILE *fp = fopen(path, "ab")) { fwrite(h.data(), sizeof(unsigned long long), 3 * nw, fp); fclose(fp); }
+      if (FILE *fp = fopen(path, "ab")) { fwrite(h.data(), sizeof(unsigned long long), WW * nw, fp); fclose(fp); }
     }
-    // s_memrealtime ticks at 100 MHz
+    // s_memrealtime ticks at 100 MHz; the phases are s_memtime (shader clock) per tile
     fprintf(stderr, "K1 waves %lld tiles %lld: span %.1f us, first end %.1f us, wave life mean %.1f min %.1f max %.1f us\n",
             n, tiles, (e1 - s0) / 100.0, (e0 - s0) / 100.0, sum / n / 100.0, smin / 100.0, smax / 100.0);
+    if (tiles)
+      fprintf(stderr, "K1 phases, clocks per tile: dma-wait %.0f colour %.0f dma-issue %.0f dct+quant %.0f store/emit %.0f\n",
+              ph[0] / tiles, ph[1] / tiles, ph[2] / tiles, ph[3] / tiles, ph[4] / tiles);
   }
   if (b->timing && mode != 6 && stage_events) HIP_TRY(hipEventRecord(b->ev[1], b->stream));
   if (mode == 1) HIP_TRY(launch_fix_blocks(k, b->stream));
@@ -902,6 +916,31 @@ extern "C" int mij_batch_dct(mij_batch *b, int nframes) {
   if (run_k1(b, nframes, 1)) return g_err;  // events 1, 2
   if (b->timing)
     for (int k = 3; k < MIJ_NSTAGES; k++) HIP_TRY(hipEventRecord(b->ev[k], b->stream));
+  return MIJ_OK;
+}
+
+// tests: the coefficient K1 on frames 0..n-1 through its audit variant,
+// which also exports every block's fast-path keep/replay decisions
+extern "C" int mij_batch_audit(mij_batch *b, int nframes, uint16_t *masks) {
+  if (pipe_check(b, "audit")) return g_err;
+  if (nframes < 1 || nframes > b->cap || !masks) return fail(MIJ_EINVAL, "audit: bad arguments");
+  if (b->rgb || b->use_fdims) return fail(MIJ_EINVAL, "audit: plain B, G, R batches only");
+  HIP_TRY(hipSetDevice(b->dev));
+  const size_t n = (size_t)nframes * b->g.nblk * 4;
+  if (b->audit_cap < n) {
+    if (b->d_audit) HIP_TRY(hipFree(b->d_audit));
+    b->d_audit = nullptr;
+    b->audit_cap = 0;
+    HIP_TRY(dalloc(&b->d_audit, n));
+    b->audit_cap = n;
+  }
+  HIP_TRY(hipMemsetAsync(b->d_audit, 0, sizeof(uint16_t) * n, b->stream));
+  b->audit = true;
+  const int rc = run_k1(b, nframes, 1);
+  b->audit = false;
+  if (rc) return g_err;
+  HIP_TRY(hipMemcpyAsync(masks, b->d_audit, sizeof(uint16_t) * n, hipMemcpyDeviceToHost, b->stream));
+  HIP_TRY(hipStreamSynchronize(b->stream));
   return MIJ_OK;
 }
 
@@ -1317,7 +1356,7 @@ extern "C" int mij_band_histograms(mij_batch *b, int n, const int16_t *prev_dc, 
     for (int c = 0; c < 3; c++) pred[f * 4 + c] = prev_dc[f * 3 + c];
   HIP_TRY(hipMemcpyAsync(b->d_dcpred, pred.data(), sizeof(int16_t) * n * 4, hipMemcpyHostToDevice,
                          b->stream));
-  EntArgs a = ent_args(b, n);
+  EntArgs a = ent_args(b, n, 0, true);
   HIP_TRY(launch_seg_dc(a, b->stream));
   HIP_TRY(hipMemcpyAsync(hist, b->d_hist, sizeof(uint32_t) * n * 4 * 257, hipMemcpyDeviceToHost,
                          b->stream));
@@ -1339,7 +1378,7 @@ extern "C" int mij_band_tables(mij_batch *b, int n, const uint32_t *hist, unsign
   if (!hist || !bits) return fail(MIJ_EINVAL, "band_tables: null argument");
   if (upload_hist_tables(b, n, hist)) return g_err;
   HIP_TRY(hipMemsetAsync(b->d_bitbase, 0, sizeof(uint32_t) * n * 4, b->stream));
-  EntArgs a = ent_args(b, n);
+  EntArgs a = ent_args(b, n, 0, true);
   HIP_TRY(launch_bits(a, b->stream));
   HIP_TRY(launch_scan(a, b->stream));
   HIP_TRY(hipMemcpyAsync(bits, b->d_scan_bits, sizeof(uint64_t) * n * 3, hipMemcpyDeviceToHost,
@@ -1361,7 +1400,7 @@ extern "C" int mij_band_pack(mij_batch *b, int n, const unsigned long long *bit_
     for (int c = 0; c < 3; c++) base[f * 4 + c] = (uint32_t)(bit_offset[f * 3 + c] & 31);
   HIP_TRY(hipMemcpyAsync(b->d_bitbase, base.data(), sizeof(uint32_t) * n * 4, hipMemcpyHostToDevice,
                          b->stream));
-  EntArgs a = ent_args(b, n);
+  EntArgs a = ent_args(b, n, 0, true);
   // k_pack_lb needs all-zero scan buffers: mij_band_words_all moves the band
   // words out and zeroes them; a band packed but never moved leaves them dirty
   if (b->raw_dirty) HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->raw_dirty * b->g.raw_fs, b->stream));

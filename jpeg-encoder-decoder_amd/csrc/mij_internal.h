@@ -150,12 +150,18 @@ struct K1Args {
   uint32_t *tok0;           // token mode: per segment its first token (the first block's DC)
   uint32_t *seg_ntok;       // token mode: tokens per segment
   uint32_t *hist;           // token mode: per frame [4][257] histograms
-  uint32_t *fix_list;       // coefficient mode: blocks (frame * nblk + blk) for k_fix_blocks
-  unsigned int *fix_count;  // coefficient mode: length of fix_list
-  unsigned long long *wtime;  // diagnostics only (MIJ_K1_WTIME): per wave start, end, tiles
+  // coefficient mode: per K1 N-tile (global tile * 3 + nt) the 16-bit mask of
+  // its blocks k_fix_blocks must recompute; all zero between launches (K1
+  // stores only nonzero masks, k_fix_blocks zeroes what it consumes)
+  uint16_t *fix_mask;
+  unsigned long long *wtime;  // diagnostics only (MIJ_K1_WTIME): per wave start, end, tiles,
+                              // then 5 phase times (K1_WTIME_WORDS words per wave)
   int rgb;                  // input bytes in R, G, B order (PPM) instead of B, G, R
   const int2 *fdims;        // per-frame image size (region batches), null: the canvas
+  uint16_t *audit;          // tests (mij_batch_audit): per frame, block, lane group g the 16
+                            // straddle bits of zigzag 16g..16g+15; null in every product launch
 };
+constexpr int K1_WTIME_WORDS = 8;
 // K1 diagnostic switches (timing attribution; outputs are wrong when set)
 constexpr int K1F_NO_LUT = 1, K1F_NO_REPLAY = 2, K1F_NO_COLOUR = 4, K1F_NO_DCT = 8,
               K1F_NO_STORE = 16, K1F_NO_QUANT = 32, K1F_NO_MFMA = 64,

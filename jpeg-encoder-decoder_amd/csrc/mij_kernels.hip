@@ -254,21 +254,25 @@ constexpr int TILE_RAW = TILE_W * 3 * TILE_H;  // 6144 B of BGR888 per tile
 // Streams a tile's 16 rows x 384 B into LDS with global_load_lds_dwordx4 (no
 // VGPRs for the data): instruction k moves rows 2k and 2k+1 = LDS bytes
 // [768k, 768k + 768); lane i < 48 moves the 16 B at row 2k + i / 24, column
-// 16 * (i % 24).  The per-lane offsets of the eight instructions are fixed
-// for the kernel (DmaOff, eight VGPRs); per tile only the frame/tile base
-// (one SGPR pair) and the LDS base (m0 = base + 768k) change, so the issue
-// needs no VALU and three SGPRs.
+// 16 * (i % 24).  One per-lane offset serves all eight instructions (DmaOff,
+// one VGPR for the kernel); instruction k's scalar base is the tile's base +
+// 2k rows (an SGPR pair each, SALU adds) and its LDS base m0 = base + 768k.
+// (Eight per-lane offsets, one per instruction, held eight VGPRs for the
+// whole kernel: at 168 the coefficient variant spilled one pair, and the
+// reload before every tile's DMA waited, vmcnt(0), for the previous tile's
+// coefficient stores.)
 constexpr int DMA_K = TILE_H / 2;
 struct DmaOff {
-  uint32_t v[DMA_K];
+  uint32_t v;
 };
 __device__ __forceinline__ DmaOff dma_offsets(int pitch, int lane) {
   const int l = lane < 48 ? lane : 0;
-  const uint32_t o = (uint32_t)((l / 24) * pitch + (l % 24) * 16);
-  DmaOff d;
-#pragma unroll
-  for (int k = 0; k < DMA_K; k++) d.v[k] = o + (uint32_t)(2 * k * pitch);
-  return d;
+  return DmaOff{(uint32_t)((l / 24) * pitch + (l % 24) * 16)};
+}
+template <int K>
+__device__ __forceinline__ void dma_one(uint32_t off, uint32_t lds, const uint8_t *src) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, %2 nt" : : "v"(off), "s"(lds), "s"(src)
+               : "memory", "m0");
 }
 __device__ __forceinline__ void issue_tile_dma(const K1Args &a, const TilePos &p, int lane, uint8_t *raw,
                                                const DmaOff &off) {
@@ -280,6 +284,7 @@ __device__ __forceinline__ void issue_tile_dma(const K1Args &a, const TilePos &p
   const uint32_t src_lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)srcv);
   const uint8_t *src = (const uint8_t *)(uintptr_t)(((uint64_t)src_hi << 32) | (uint64_t)src_lo);
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t *)raw);
+  const long long step = 2LL * a.pitch;  // kernel argument: an SGPR
   // right frame edge: only the valid columns
   const bool on = lane < 48 && (p.valid_px == TILE_W || (lane % 24) * 16 < p.valid_px * 3);
   // issued as asm so the compiler does not tie the next LDS read of `raw` to
@@ -287,19 +292,14 @@ __device__ __forceinline__ void issue_tile_dma(const K1Args &a, const TilePos &p
   // stores; K1 waits for the DMA itself (dma_wait) before its first store,
   // when the DMA has long landed
   if (on) {
-    asm volatile(
-        "s_mov_b32 m0, %8\n\tglobal_load_lds_dwordx4 %0, %9 nt\n\t"
-        "s_add_u32 m0, %8, 768\n\tglobal_load_lds_dwordx4 %1, %9 nt\n\t"
-        "s_add_u32 m0, %8, 1536\n\tglobal_load_lds_dwordx4 %2, %9 nt\n\t"
-        "s_add_u32 m0, %8, 2304\n\tglobal_load_lds_dwordx4 %3, %9 nt\n\t"
-        "s_add_u32 m0, %8, 3072\n\tglobal_load_lds_dwordx4 %4, %9 nt\n\t"
-        "s_add_u32 m0, %8, 3840\n\tglobal_load_lds_dwordx4 %5, %9 nt\n\t"
-        "s_add_u32 m0, %8, 4608\n\tglobal_load_lds_dwordx4 %6, %9 nt\n\t"
-        "s_add_u32 m0, %8, 5376\n\tglobal_load_lds_dwordx4 %7, %9 nt"
-        :
-        : "v"(off.v[0]), "v"(off.v[1]), "v"(off.v[2]), "v"(off.v[3]), "v"(off.v[4]), "v"(off.v[5]),
-          "v"(off.v[6]), "v"(off.v[7]), "s"(lds0), "s"(src)
-        : "memory", "m0", "scc");  // s_add_u32 writes SCC
+    dma_one<0>(off.v, lds0, src);
+    dma_one<1>(off.v, lds0 + 768, src + step);
+    dma_one<2>(off.v, lds0 + 1536, src + 2 * step);
+    dma_one<3>(off.v, lds0 + 2304, src + 3 * step);
+    dma_one<4>(off.v, lds0 + 3072, src + 4 * step);
+    dma_one<5>(off.v, lds0 + 3840, src + 5 * step);
+    dma_one<6>(off.v, lds0 + 4608, src + 6 * step);
+    dma_one<7>(off.v, lds0 + 5376, src + 7 * step);
   }
 }
 static_assert(DMA_K == 8 && TILE_W * 3 * 2 == 768, "issue_tile_dma: 8 instructions of 2 rows x 384 B");
@@ -572,6 +572,13 @@ constexpr uint32_t TOK_AC = 1u << 10;
 #ifndef MIJ_K1_ACMERGE
 #define MIJ_K1_ACMERGE 0
 #endif
+// software pipelining of K1's N-tiles (A/B knob; see the N-tile loop)
+#ifndef MIJ_K1_PIPE
+#define MIJ_K1_PIPE 0
+#endif
+#ifndef MIJ_K1_AREL
+#define MIJ_K1_AREL 0
+#endif
 // N-tile of the token K1 before whose stores the next tile's DMA is awaited
 // (A/B: 0, 1 and 2 measured equal, 3.36-3.39 ms)
 #ifndef MIJ_K1_DMAWAIT_NT
@@ -728,7 +735,8 @@ constexpr int K1M_TOK_OUT = 2;   // write per-segment token streams + histograms
 constexpr int K1M_COEF_IN = 4;   // read coefficient planes (DC differences) instead of pixels
 constexpr int K1M_RGB = 8;       // pixels in RGB order (PPM) instead of BGR (encoder.c:133)
 constexpr int K1M_REGIONS = 16;  // per-frame image sizes inside the canvas (region batches)
-constexpr int k1_base(int mode) { return mode & ~(K1M_RGB | K1M_REGIONS); }
+constexpr int K1M_AUDIT = 32;    // coefficient variant + every block's straddle decisions (tests)
+constexpr int k1_base(int mode) { return mode & ~(K1M_RGB | K1M_REGIONS | K1M_AUDIT); }
 
 // Waves per workgroup: the coefficient-only variant runs one 12-wave
 // workgroup per CU (3 waves per SIMD: 120 KB of per-wave tile buffers + the
@@ -757,6 +765,9 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   // region batches only: the frame sizes (compile-time null otherwise, so
   // the per-tile geometry folds to the batch's)
   constexpr bool REG = MODE & K1M_REGIONS;
+  // audit (tests only): per block the 64 keep/replay decisions of the fast
+  // path, exported so they can be compared with tests/tau_check.c's model
+  constexpr bool AUDIT = MODE & K1M_AUDIT;
   const int2 *const fdims = REG ? a.fdims : nullptr;
   __shared__ __attribute__((aligned(16))) uint8_t s_raw[PIX ? NW : 1][TILE_RAW];
   __shared__ __attribute__((aligned(16))) uint8_t s_tile[PIX ? NW : 1][LDS_WAVE];
@@ -846,6 +857,18 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
 #ifdef MIJ_K1_DIAG
   const unsigned long long w_t0 = __builtin_amdgcn_s_memrealtime();
   int w_ntiles = 0;
+  // per-phase wall time of this wave (s_memtime, shader clock), summed over
+  // its tiles: [0] DMA wait, [1] colour, [2] next-DMA issue, [3] DCT +
+  // quantise per N-tile, [4] store / emit per N-tile
+  unsigned long long ph[5] = {0, 0, 0, 0, 0}, tph = __builtin_amdgcn_s_memtime();
+#define K1_PHASE(k)                                                  \
+  do {                                                               \
+    const unsigned long long tn_ = __builtin_amdgcn_s_memtime();     \
+    ph[k] += tn_ - tph;                                              \
+    tph = tn_;                                                       \
+  } while (0)
+#else
+#define K1_PHASE(k)
 #endif
   // coefficients this lane replayed in FP64 (or listed for k_fix_blocks):
   // summed over the wave and added once at the end (an atomic per replaying
@@ -899,18 +922,22 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
         // flight (counted wait); the token variants waited before their first
         // store of the previous tile; the first tile and the diagnostic
         // variants without stores drain everything.
+        K1_PHASE(3);
         if (first || (kflags & (K1F_NO_DCT | K1F_NO_STORE)))
           dma_wait();
         else if (DEFER)
           dma_wait_behind_stores();
+        K1_PHASE(0);
         if (!(kflags & K1F_NO_COLOUR)) colour_stage<RGB, !LUT_LDS>(raw, L, c4, pr, lut, !(kflags & K1F_NO_LUT));
         wave_lds_sync();
+        K1_PHASE(1);
         // ---- stream the wave's next tile into the freed raw buffer -----------
         if (REG) skip_outside(tn);
         if (tn < tend) {
           pn = tpos(tn);
           issue_tile_dma(a, pn, lane, raw, doff);
         }
+        K1_PHASE(2);
       } else {
         if (REG) skip_outside(tn);
         if (tn < tend) pn = tpos(tn);
@@ -1076,12 +1103,26 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
         }
       };
       if (PIX && do_dct) {
+        // MIJ_K1_PIPE: N-tile nt + 1's MFMA chain is issued before N-tile nt
+        // is quantised, so the wave's own quantisation covers the chain's
+        // latency (two accumulator sets live)
+        v4i accs[MIJ_K1_PIPE ? 2 : 1][4];
+        float lcs[MIJ_K1_PIPE ? 2 : 1];  // per block: error bound of N in N units
+        if (MIJ_K1_PIPE) dct_ntile(0, accs[0], lcs[0]);
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
           const int comp = nt == 2 ? 1 : 0;
-          v4i acc[4];
-          float lc;  // per block: error bound of N in N units
-          dct_ntile(nt, acc, lc);
+          const int cur = MIJ_K1_PIPE ? (nt & 1) : 0;
+          if (!MIJ_K1_PIPE) {
+            dct_ntile(nt, accs[0], lcs[0]);
+          } else if (nt + 1 < 3) {
+#if MIJ_K1_AREL
+            asm volatile("" ::: "memory");  // A fragments re-read from LDS per N-tile
+#endif
+            dct_ntile(nt + 1, accs[cur ^ 1], lcs[cur ^ 1]);
+          }
+          v4i(&acc)[4] = accs[cur];
+          const float lc = lcs[cur];
           int o[16];
           // trunc(t - tau) is the output; the lane's sums of trunc(t - tau)
           // and trunc(t + tau) differ iff some coefficient's +-tau interval
@@ -1112,38 +1153,9 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
             }
           }
           const uint32_t hz = (uint32_t)(slo ^ shi);  // nonzero iff a hazard
-          {  // z = 0: exact from the pixel sum (fac = 0 above)
-            bool tie;
-            const int dcv = dc_fast(acc[0][0], 8 * q_dc[comp], s_inv8q[comp], tie);
-            if (g == 0) o[0] = dcv;
-            if (__ballot(tie && g == 0))
-              if (g == 0 && tie) o[0] = dc_tie(dcv, s_dctie[comp]);
-          }
-          if constexpr (DEFER) {
-            // blocks with a straddling coefficient go to the fix list;
-            // k_fix_blocks recomputes them in FP64 after this kernel
-            const unsigned long long need = __ballot(hz != 0);
-            if (need && !(kflags & K1F_NO_REPLAY)) {
-              int blk;
-              const bool valid = block_of(nt, blk);
-              const unsigned long long vm = __ballot(valid);
-              const uint32_t m16 = (uint32_t)((need | need >> 16 | need >> 32 | need >> 48) & vm) & 0xFFFFu;
-              if (m16) {
-                uint32_t base = 0;
-                if (lane == 0) {
-                  base = atomicAdd(a.fix_count, (unsigned)__popc(m16));
-                  nrep += (uint32_t)__popc(m16);
-                }
-                base = __builtin_amdgcn_readfirstlane(base);
-                if (g == 0 && ((m16 >> bcol) & 1u))
-                  a.fix_list[base + __popc(m16 & ((1u << bcol) - 1u))] = (uint32_t)p.f * (uint32_t)G.nblk + (uint32_t)blk;
-              }
-            }
-          }
-          if (!DEFER && __ballot(hz != 0) && !(kflags & K1F_NO_REPLAY)) {
-            // rare path: find the straddling coefficients (same arithmetic) and
-            // recompute them in FP64 exactly as encoder.c:87-109
-            const uint8_t *Pb = L + (nt * 16 + bcol) * LDS_BLK;
+          // the lane's straddling coefficients, one bit each (same arithmetic
+          // as the sums above, coefficient by coefficient)
+          auto straddle_mask = [&]() {
             uint32_t mm = 0;
 #pragma unroll
             for (int m = 0; m < 4; m++)
@@ -1155,6 +1167,42 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
                 const float tv = fmaf(fa, lc, 1.0e-6f);
                 mm |= (uint32_t)((int)fmaf(nf, fa, -tv) != (int)fmaf(nf, fa, tv)) << k;
               }
+            return mm;
+          };
+          if constexpr (AUDIT) {
+            int blk;
+            if (block_of(nt, blk)) a.audit[((long long)p.f * G.nblk + blk) * 4 + g] = (uint16_t)straddle_mask();
+          }
+          {  // z = 0: exact from the pixel sum (fac = 0 above)
+            bool tie;
+            const int dcv = dc_fast(acc[0][0], 8 * q_dc[comp], s_inv8q[comp], tie);
+            if (g == 0) o[0] = dcv;
+            if (__ballot(tie && g == 0))
+              if (g == 0 && tie) o[0] = dc_tie(dcv, s_dctie[comp]);
+          }
+          if constexpr (DEFER) {
+            // blocks with a straddling coefficient: the N-tile's 16-bit mask
+            // goes to the fix masks (one plain store, no returning atomic: a
+            // returning one waits, vmcnt(0), for the next tile's DMA and every
+            // store in flight); k_fix_blocks recomputes them in FP64 after
+            // this kernel
+            const unsigned long long need = __ballot(hz != 0);
+            if (need && !(kflags & K1F_NO_REPLAY)) {
+              int blk;
+              const bool valid = block_of(nt, blk);
+              const unsigned long long vm = __ballot(valid);
+              const uint32_t m16 = (uint32_t)((need | need >> 16 | need >> 32 | need >> 48) & vm) & 0xFFFFu;
+              if (m16 && lane == 0) {
+                a.fix_mask[(long long)t * 3 + nt] = (uint16_t)m16;
+                nrep += (uint32_t)__popc(m16);
+              }
+            }
+          }
+          if (!DEFER && __ballot(hz != 0) && !(kflags & K1F_NO_REPLAY)) {
+            // rare path: find the straddling coefficients (same arithmetic) and
+            // recompute them in FP64 exactly as encoder.c:87-109
+            const uint8_t *Pb = L + (nt * 16 + bcol) * LDS_BLK;
+            uint32_t mm = straddle_mask();
             nrep += (uint32_t)__popc(mm);
             while (mm) {
               const int k = __ffs(mm) - 1;
@@ -1168,7 +1216,9 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
           // token variants: the next tile's DMA has landed before the first
           // store (their VMEM count per tile varies)
           if (nt == MIJ_K1_DMAWAIT_NT && !DEFER && !(kflags & K1F_NO_DMAWAIT)) dma_wait();
+          K1_PHASE(3);
           finish(nt, o);
+          K1_PHASE(4);
         }
       } else if (!PIX) {
 #pragma unroll
@@ -1193,10 +1243,11 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   }
 #ifdef MIJ_K1_DIAG
   if (a.wtime && lane == 0) {
-    unsigned long long *w = a.wtime + 3 * ((long long)blockIdx.x * NW + wave);
+    unsigned long long *w = a.wtime + K1_WTIME_WORDS * ((long long)blockIdx.x * NW + wave);
     w[0] = w_t0;
     w[1] = __builtin_amdgcn_s_memrealtime();
     w[2] = (unsigned long long)w_ntiles;
+    for (int k = 0; k < 5; k++) w[3 + k] = ph[k];
   }
 #endif
   if (TOK) {  // per-frame histograms of this workgroup
@@ -1249,6 +1300,9 @@ __device__ __forceinline__ int cr_ref(const uint8_t *px, int ib, int ir) {
   return (int)(uint8_t)(int)v;
 }
 
+// The blocks come from K1's per-N-tile fix masks (K1Args::fix_mask): each
+// wave scans 64 masks per step, takes the nonzero ones in turn, zeroes them
+// and recomputes their blocks one after another.
 __global__ __launch_bounds__(256) void k_fix_blocks(K1Args a) {
   __shared__ __attribute__((aligned(8))) uint8_t s_px[4][64];
   __shared__ double s_inner[4][64];
@@ -1260,57 +1314,73 @@ __global__ __launch_bounds__(256) void k_fix_blocks(K1Args a) {
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const Geom G = a.g;
-  const unsigned n = *a.fix_count;
   const int x = lane & 7, y = lane >> 3;
   // lane z's output coefficient: zigzag z = frequency (v, u) (encoder.c:38-46)
   const int rz = c_zigzag[lane], v = rz >> 3, u = rz & 7;
   const int ib = a.rgb ? 2 : 0, ir = 2 - ib;
-  for (unsigned e = blockIdx.x * 4 + wave; e < n; e += gridDim.x * 4) {
-    const uint32_t id = a.fix_list[e];
-    const int f = (int)(id / (uint32_t)G.nblk), blk = (int)(id - (uint32_t)f * (uint32_t)G.nblk);
-    const uint8_t *img = a.in + (long long)f * a.in_fs;
-    const FGeom fg = frame_geom(G, a.fdims, f);
-    const int bw = fg.bw, mw = fg.mw;
-    int pv, comp;
-    if (blk < fg.nY) {  // lane = pixel (x, y) of the block
-      comp = 0;
-      const int bx = blk % bw, by = blk / bw;
-      pv = y_ref(img + (long long)(8 * by + y) * a.pitch + (8 * bx + x) * 3, ib, ir);
-    } else {
-      comp = 1;
-      const int c = blk - fg.nY, cr = c >= fg.nC, m = cr ? c - fg.nC : c;
-      const int mx = m % mw, my = m / mw;
-      const uint8_t *q = img + (long long)(16 * my + 2 * y) * a.pitch + (16 * mx + 2 * x) * 3;
-      int sum = 0;
-      for (int dy = 0; dy < 2; dy++)
-        for (int dx = 0; dx < 2; dx++) {
-          const uint8_t *px = q + (long long)dy * a.pitch + dx * 3;
-          sum += cr ? cr_ref(px, ib, ir) : cb_ref(px, ib, ir);
+  const long long nmask = (long long)a.nframes * G.tiles_per_frame * 3;
+  for (long long base = ((long long)blockIdx.x * 4 + wave) * 64; base < nmask; base += (long long)gridDim.x * 4 * 64) {
+    const long long e = base + lane;
+    const uint32_t mk = e < nmask ? a.fix_mask[e] : 0u;
+    unsigned long long any = __ballot(mk != 0);
+    if (mk) a.fix_mask[e] = 0;  // consumed: all zero again for the next K1
+    while (any) {
+      const int l = __ffsll((long long)any) - 1;
+      any &= any - 1ull;
+      uint32_t mm = (uint32_t)__builtin_amdgcn_readlane((int)mk, l);
+      const int tg = (int)((base + l) / 3), nt = (int)(base + l - 3LL * tg);  // global tile, N-tile
+      const int f = tg / G.tiles_per_frame, rem = tg - f * G.tiles_per_frame;
+      const int ty = rem / G.tiles_x, tx = rem - ty * G.tiles_x;
+      const uint8_t *img = a.in + (long long)f * a.in_fs;
+      const FGeom fg = frame_geom(G, a.fdims, f);
+      const int bw = fg.bw, mw = fg.mw;
+      while (mm) {
+        const int bb = __ffs(mm) - 1;
+        mm &= mm - 1u;
+        // the block of column bb of N-tile nt (K1's block_at)
+        const int blk = nt < 2 ? (2 * ty + nt) * bw + tx * 16 + bb
+                               : fg.nY + (bb >= 8 ? fg.nC : 0) + ty * mw + tx * 8 + (bb & 7);
+        int pv, comp;
+        if (nt < 2) {  // lane = pixel (x, y) of the block
+          comp = 0;
+          const int bx = tx * 16 + bb, by = 2 * ty + nt;
+          pv = y_ref(img + (long long)(8 * by + y) * a.pitch + (8 * bx + x) * 3, ib, ir);
+        } else {
+          comp = 1;
+          const int cr = bb >= 8, mx = tx * 8 + (bb & 7), my = ty;
+          const uint8_t *q = img + (long long)(16 * my + 2 * y) * a.pitch + (16 * mx + 2 * x) * 3;
+          int sum = 0;
+          for (int dy = 0; dy < 2; dy++)
+            for (int dx = 0; dx < 2; dx++) {
+              const uint8_t *px = q + (long long)dy * a.pitch + dx * 3;
+              sum += cr ? cr_ref(px, ib, ir) : cb_ref(px, ib, ir);
+            }
+          pv = sum / 4;
         }
-      pv = sum / 4;
+        s_px[wave][lane] = (uint8_t)pv;
+        wave_lds_sync();
+        {  // column pass, lane = (x_t = lane >> 3, y_f = lane & 7), summed from 0 in y_t order
+          const int xt = lane >> 3, yf = lane & 7;
+          double in = 0.0;
+          for (int yt = 0; yt < 8; yt++)
+            in = __dadd_rn(in, __dmul_rn((double)((int)s_px[wave][yt * 8 + xt] - 128), s_cos[yt * 8 + yf]));
+          s_inner[wave][xt * 8 + yf] = in;
+        }
+        wave_lds_sync();
+        // row pass for frequency (v, u), summed from 0 in x_t order, then the
+        // 1/sqrt2 factors (u first), /4, quantisation, clip
+        double freq = 0.0;
+        for (int xt = 0; xt < 8; xt++) freq = __dadd_rn(freq, __dmul_rn(s_inner[wave][xt * 8 + v], s_cos[xt * 8 + u]));
+        if (u == 0) freq = __dmul_rn(freq, SQRT1_2);
+        if (v == 0) freq = __dmul_rn(freq, SQRT1_2);
+        freq = __dmul_rn(freq, 0.25);
+        int o = (int)__ddiv_rn(freq, (double)s_q[comp][lane]);
+        o = o < -2048 ? -2048 : (o > 2047 ? 2047 : o);
+        a.coef[(long long)f * G.coef_fs + (long long)blk * 64 + lane] = (int16_t)o;
+        if (lane == 0) a.dc[(long long)f * G.nblk + blk] = (int16_t)o;
+        wave_lds_sync();
+      }
     }
-    s_px[wave][lane] = (uint8_t)pv;
-    wave_lds_sync();
-    {  // column pass, lane = (x_t = lane >> 3, y_f = lane & 7), summed from 0 in y_t order
-      const int xt = lane >> 3, yf = lane & 7;
-      double in = 0.0;
-      for (int yt = 0; yt < 8; yt++)
-        in = __dadd_rn(in, __dmul_rn((double)((int)s_px[wave][yt * 8 + xt] - 128), s_cos[yt * 8 + yf]));
-      s_inner[wave][xt * 8 + yf] = in;
-    }
-    wave_lds_sync();
-    // row pass for frequency (v, u), summed from 0 in x_t order, then the
-    // 1/sqrt2 factors (u first), /4, quantisation, clip
-    double freq = 0.0;
-    for (int xt = 0; xt < 8; xt++) freq = __dadd_rn(freq, __dmul_rn(s_inner[wave][xt * 8 + v], s_cos[xt * 8 + u]));
-    if (u == 0) freq = __dmul_rn(freq, SQRT1_2);
-    if (v == 0) freq = __dmul_rn(freq, SQRT1_2);
-    freq = __dmul_rn(freq, 0.25);
-    int o = (int)__ddiv_rn(freq, (double)s_q[comp][lane]);
-    o = o < -2048 ? -2048 : (o > 2047 ? 2047 : o);
-    a.coef[(long long)f * G.coef_fs + (long long)blk * 64 + lane] = (int16_t)o;
-    if (lane == 0) a.dc[(long long)f * G.nblk + blk] = (int16_t)o;
-    wave_lds_sync();
   }
 }
 
@@ -2641,7 +2711,9 @@ int k1_grid(int device, long long ntiles, int mode) {
 }
 
 hipError_t launch_fix_blocks(const K1Args &a, hipStream_t s) {
-  hipLaunchKernelGGL(k_fix_blocks, dim3(4096), dim3(256), 0, s, a);
+  // a persistent grid over the fix masks: 64 masks per wave step
+  const long long steps = ((long long)a.nframes * a.g.tiles_per_frame * 3 + 255) / 256;
+  hipLaunchKernelGGL(k_fix_blocks, dim3((unsigned)(steps < 4096 ? steps : 4096)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_colour_lut(uint32_t *lut, hipStream_t s) {
@@ -2657,7 +2729,10 @@ hipError_t launch_k1(const K1Args &a, int grid, int mode, hipStream_t s) {
   if (a.rgb && a.fdims) return hipErrorInvalidValue;  // not instantiated (the API refuses it)
   switch (mode) {
     case K1M_COEF_OUT:
-      if (a.rgb) launch_k1_mode<K1M_COEF_OUT | K1M_RGB>(a, grid, s);
+      if (a.audit) {
+        if (a.rgb || a.fdims) return hipErrorInvalidValue;  // tests audit plain B, G, R batches
+        launch_k1_mode<K1M_COEF_OUT | K1M_AUDIT>(a, grid, s);
+      } else if (a.rgb) launch_k1_mode<K1M_COEF_OUT | K1M_RGB>(a, grid, s);
       else if (a.fdims) launch_k1_mode<K1M_COEF_OUT | K1M_REGIONS>(a, grid, s);
       else launch_k1_mode<K1M_COEF_OUT>(a, grid, s);
       break;

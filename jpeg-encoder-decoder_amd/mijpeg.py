@@ -19,12 +19,12 @@ EXPORTS = [
     # drop-in (reference include/encoder.h:10-12)
     "rgb_to_dct", "init_huffman", "write_jpg",
     # extensions
-    "mij_set_input_stride", "mij_set_quality", "mij_last_error", "mij_strerror",
+    "mij_set_input_stride", "mij_set_quality", "mij_last_error", "mij_strerror", "mij_last_message",
     "mij_max_jpg_bytes", "mij_encode",
     "mij_batch_create", "mij_batch_destroy", "mij_batch_upload", "mij_batch_set_input",
     "mij_batch_encode", "mij_batch_keep_coefs", "mij_batch_set_split", "mij_batch_set_overlap", "mij_batch_dct", "mij_batch_sync", "mij_batch_output",
     "mij_batch_lengths", "mij_batch_coefs", "mij_batch_tables", "mij_batch_set_timing",
-    "mij_batch_stage_ms", "mij_batch_stage_history", "mij_batch_token_count", "mij_batch_geometry", "mij_batch_replays", "mij_batch_stream",
+    "mij_batch_stage_ms", "mij_batch_stage_history", "mij_batch_token_count", "mij_batch_geometry", "mij_batch_replays", "mij_batch_stream", "mij_batch_audit",
     "mij_band_analyze", "mij_band_histograms", "mij_band_tables", "mij_band_pack", "mij_band_words",
     "mij_assemble_begin", "mij_assemble_words", "mij_assemble_end",
     "mij_band_words_all", "mij_assemble_pieces", "mij_assembler_create",
@@ -89,6 +89,8 @@ def load() -> C.CDLL:
     lib.mij_last_error.restype = i
     lib.mij_strerror.restype = C.c_char_p
     lib.mij_strerror.argtypes = [i]
+    lib.mij_last_message.restype = C.c_char_p
+    lib.mij_last_message.argtypes = []
     lib.mij_max_jpg_bytes.restype = sz
     lib.mij_max_jpg_bytes.argtypes = [i, i]
     lib.mij_encode.argtypes = [p, i, Area, i, p, sz, C.POINTER(sz)]
@@ -103,6 +105,7 @@ def load() -> C.CDLL:
     lib.mij_batch_set_split.argtypes = [p, i]
     lib.mij_batch_set_overlap.argtypes = [p, i]
     lib.mij_batch_dct.argtypes = [p, i]
+    lib.mij_batch_audit.argtypes = [p, i, p]
     lib.mij_batch_sync.argtypes = [p]
     lib.mij_batch_output.argtypes = [p, i, p, sz, C.POINTER(sz)]
     lib.mij_batch_lengths.argtypes = [p, C.POINTER(sz), i]
@@ -193,7 +196,8 @@ def load() -> C.CDLL:
 def _check(rc: int, what: str) -> None:
     if rc != 0:
         lib = load()
-        raise MijError(f"{what}: {lib.mij_strerror(rc).decode()} ({rc})")
+        raise MijError(f"{what}: {lib.mij_strerror(rc).decode()} ({rc}): "
+                       f"{lib.mij_last_message().decode(errors='replace')}")
 
 
 def _ptr(a: np.ndarray) -> int:
@@ -423,6 +427,15 @@ class Batch:
         g = np.zeros(5, np.int64)
         _check(self.lib.mij_batch_geometry(self.h_, _ptr(g), 5), "geometry")
         return dict(zip(["w", "h", "nblk", "nseg", "tiles_per_frame"], [int(v) for v in g]))
+
+    def audit(self, n: int) -> np.ndarray:
+        """K1's fast-path keep/replay decisions (mij_batch_audit): uint64 per
+        block [n, nblk], bit z = zigzag coefficient z was replayed in FP64."""
+        nblk = self.geometry()["nblk"]
+        m = np.zeros((n, nblk, 4), np.uint16)
+        _check(self.lib.mij_batch_audit(self.h_, n, _ptr(m)), "audit")
+        m = m.astype(np.uint64)
+        return m[..., 0] | (m[..., 1] << np.uint64(16)) | (m[..., 2] << np.uint64(32)) | (m[..., 3] << np.uint64(48))
 
     def replays(self) -> int:
         return int(self.lib.mij_batch_replays(self.h_))

@@ -158,6 +158,21 @@ def main() -> None:
                         "jpg_sha256": sha(r), "jpg_len": len(r),
                         "source": "reference utils/original.c + set_quality (oracle/_ref)"}
                 print(f"  {k}: {len(r)} B")
+        # config 5 at frame size: a config-3 frame at Q=75 and one at Q=90
+        # (bench.py --quality 75 / 90 encodes exactly these contents)
+        for f, q in ((0, 75), (1, 90)):
+            rgb = recipes.config3_frame(f)[:, :, ::-1]  # the recipe is B, G, R
+            p = os.path.join(d, "in.ppm")
+            with open(p, "wb") as fh:
+                fh.write(ppm.ppm_bytes(np.ascontiguousarray(rgb)))
+            r = O.ref_quality_encode(p, q, d)
+            c = O.cref_encode(recipes.config3_frame(f), q)
+            assert r == c, f"config3_frame{f} Q={q} restatement mismatch"
+            k = f"config3_frame{f}_q{q}"
+            C[k] = {"quality": q, "input": f"recipes.config3_frame({f})", "frame": [3840, 2160],
+                    "region": [0, 0, 3840, 2160], "jpg_sha256": sha(r), "jpg_len": len(r),
+                    "source": "reference utils/original.c + set_quality (oracle/_ref)"}
+            print(f"  {k}: {len(r)} B")
 
     # full intermediates for the 64x64 plumbing case
     bgr = ppm.rgb_to_bgr(recipes.sample("sample_64x64"))

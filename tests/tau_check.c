@@ -246,7 +246,54 @@ static void *worker(void *arg) {
     return NULL;
 }
 
+/* tau_check dump <nblocks> <seed> <Q> <out>: the generated blocks and, for
+ * each, the rule's decision at every AC position under the LUMA table of
+ * quality Q, for tests/test_tau_kernel.py to compare with K1's own decisions
+ * (mij_batch_audit).  Writes <out>.px (nblocks x 64 bytes, row-major) and
+ * <out>.mask (nblocks uint64, bit z = zigzag coefficient z straddles a
+ * truncation boundary, i.e. trunc(lo) != trunc(hi)). */
+static int dump(long long nblocks, long long seed, int Q, const char *out) {
+    int lq[64], cq[64];
+    cref_quality_tables(Q, lq, cq);
+    char path[4096];
+    snprintf(path, sizeof path, "%s.px", out);
+    FILE *fp = fopen(path, "wb");
+    snprintf(path, sizeof path, "%s.mask", out);
+    FILE *fm = fopen(path, "wb");
+    if (!fp || !fm) return 2;
+    uint64_t st = 0x9E3779B97F4A7C15ULL ^ ((uint64_t)seed * 0xD1B54A32D192ED03ULL);
+    if (!st) st = 1;
+    uint8_t px[64];
+    for (long long b = 0; b < nblocks; b++) {
+        gen_block(&st, px);
+        int X[64], L1 = 0;
+        for (int k = 0; k < 64; k++) {
+            X[k] = px[k] - 128;
+            L1 += X[k] < 0 ? -X[k] : X[k];
+        }
+        const float lc = fmaf((float)L1, 0.72f, 80.0f);
+        uint64_t m = 0;
+        for (int z = 1; z < 64; z++) {
+            int64_t N = 0;
+            for (int k = 0; k < 64; k++) N += W[z][k] * X[k];
+            const float nf = (float)(int32_t)N;
+            const float fa = qfac[lq[k_zz[z]]];
+            const float tv = fmaf(fa, lc, 1.0e-6f);
+            if ((int)fmaf(nf, fa, -tv) != (int)fmaf(nf, fa, tv)) m |= 1ull << z;
+        }
+        fwrite(px, 1, 64, fp);
+        fwrite(&m, 8, 1, fm);
+    }
+    fclose(fp);
+    fclose(fm);
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc > 5 && !strcmp(argv[1], "dump")) {
+        build_tables();
+        return dump(atoll(argv[2]), atoll(argv[3]), atoi(argv[4]), argv[5]);
+    }
     const long long nblocks = argc > 1 ? atoll(argv[1]) : 100000;
     const long long seed = argc > 2 ? atoll(argv[2]) : 1;
     int nth = argc > 3 ? atoi(argv[3]) : 1;

@@ -67,6 +67,8 @@ def test_validation_precedes_device_use():
     assert lib.mij_set_input_stride(3) == 1
     assert not lib.mij_batch_create(0, 30, 16, 1, 50)
     assert lib.mij_last_error() == 1
+    # the failure's text names what was wrong (mij_last_message)
+    assert b"bad geometry 30x16" in lib.mij_last_message()
 
 
 def test_c_host_builds():

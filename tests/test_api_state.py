@@ -90,6 +90,6 @@ def test_assembler_refuses_pipeline_entry_points():
              lambda: a.set_split(True), lambda: a.set_overlap(2),
              lambda: mijpeg._check(a.lib.mij_batch_keep_coefs(a.h_, 1), "keep_coefs")]
     for c in calls:
-        with pytest.raises(mijpeg.MijError, match="assembler"):
+        with pytest.raises(mijpeg.MijError, match="an assembler only assembles"):
             c()
     a.close()

@@ -153,6 +153,23 @@ def test_quality_sweep_matches_original_c(manifest, q):
     b.close()
 
 
+@pytest.mark.parametrize("split", [False, True])
+def test_config5_frame_size_q75_q90_match_original_c(manifest, split):
+    """Config 5 at frame size: config-3 frames at Q=75 and Q=90 (thousands
+    of FP64 replays per frame) against the reference's own bytes
+    (utils/original.c + set_quality, oracle/gen_golden.py), both pipelines."""
+    for f, q in ((0, 75), (1, 90)):
+        ent = manifest[f"config3_frame{f}_q{q}"]
+        b = mijpeg.Batch(3840, 2160, 1, q)
+        b.set_split(split)
+        b.upload(recipes.config3_frame(f))
+        b.encode(1)
+        got = b.output(0)
+        assert len(got) == ent["jpg_len"] and sha(got) == ent["jpg_sha256"], (f, q, split)
+        assert b.replays() > 1000
+        b.close()
+
+
 def test_config3_batch_frames(manifest):
     """3840x2160 batch (config 3 shape): two natural frames + one uniform
     high-entropy frame, one launch sequence."""
