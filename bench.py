@@ -63,10 +63,14 @@ def parse():
     ap.add_argument("--coef-launches", type=int, default=3,
                     help="extra launches of the coefficient-output K1 variant after the timed "
                          "region, for its own 6 B/px roofline line (0 disables)")
-    ap.add_argument("--workload", choices=["config3", "config4", "regions", "detect", "decode"], default="config3",
+    ap.add_argument("--workload", choices=["config3", "config4", "regions", "detect", "decode", "stream"],
+                    default="config3",
                     help="config4: a stream of 7680x4320 frames, each split into MCU-row bands "
                          "over the ranks with the RCCL exchange steps (strong scaling)")
     ap.add_argument("--detect-frames", type=int, default=8, help="detect: distinct frames cycled")
+    ap.add_argument("--stream-files", type=int, default=64,
+                    help="stream: PPM files per step (config-3 recipe contents, 16 distinct)")
+    ap.add_argument("--stream-chunk", type=int, default=16, help="stream: frames per device batch")
     ap.add_argument("--frames4", type=int, default=8, help="config4 frames per step")
     ap.add_argument("--regions", type=int, default=100,
                     help="regions workload: rectangles per frame (main.c's diffDims holds up to 100)")
@@ -454,6 +458,138 @@ def run_decode(args, world, rank, local, dist):
         dist.destroy_process_group()
 
 
+def run_stream(args, world, rank, local, dist):
+    """SURVEY §8(f) rank 1, host-fed: PPM files on the host file system ->
+    .jpg files, through mij_stream (PPM parsing by original.c:294-365's rules
+    on host threads into pinned memory, H2D, encode, D2H and file writes of
+    one chunk overlapped with the GPU work of the other; two device batches in
+    ping-pong).  The timed region covers everything from the first file read
+    to the last .jpg written -- value is host-to-host Mpixels/s, PCIe and file
+    I/O included.  Frame-parallel over ranks (each rank its own files)."""
+    import hashlib
+    import shutil
+    import tempfile
+    import ppm
+    W, H, n = args.width, args.height, args.stream_files
+    gpu = 0 if dist is not None and dist.get_backend() != "nccl" else local
+    tmp = tempfile.mkdtemp(prefix=f"mij_stream_r{rank}_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        distinct = min(n, args.distinct)
+        contents = [rank * args.distinct + i for i in range(distinct)]
+        ins, outs = [], []
+        for i in range(n):
+            c = contents[i % distinct]
+            p = os.path.join(tmp, f"in_{i:04d}.ppm")
+            if i < distinct:
+                with open(p, "wb") as f:  # PPM is R, G, B; the recipe is B, G, R
+                    f.write(ppm.ppm_bytes(np.ascontiguousarray(recipes.config3_frame(c, H, W)[:, :, ::-1])))
+            else:
+                shutil.copyfile(ins[i % distinct], p)
+            ins.append(p)
+            outs.append(os.path.join(tmp, f"out_{i:04d}.jpg"))
+        st = mijpeg.Stream(W, H, args.stream_chunk, args.quality, device=gpu)
+        for _ in range(args.warmup):
+            st.encode_files(ins, outs)
+        if dist is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        agg = {k: 0.0 for k in mijpeg.Stream.STATS}
+        for _ in range(args.steps):
+            st.encode_files(ins, outs)
+            for k, v in st.stats().items():
+                agg[k] += v
+        el = time.perf_counter() - t0
+        if dist is not None:
+            dist.barrier()
+        el, px_all = sharding.reduce_timing(el, W * H * n * args.steps, dist, dist_device(dist, local))
+        st.close()
+        # every output file against the reference's bytes: the manifest's
+        # sha256 (reference build) where it holds the content, the oracle else
+        verified = pinned = 0
+        if args.verify:
+            gold = json.load(open(os.path.join(REPO, "tests", "golden", "manifest.json")))["cases"]
+            want = {}
+            for i in range(n):
+                c = contents[i % distinct]
+                if c not in want:
+                    g = gold.get(f"config3_frame{c}")
+                    if g and g["quality"] == args.quality and [W, H] == [3840, 2160]:
+                        want[c] = g["jpg_sha256"]
+                        pinned += 1
+                    else:
+                        import oracle as O
+                        want[c] = hashlib.sha256(O.cref_encode(recipes.config3_frame(c, H, W),
+                                                               args.quality)).hexdigest()
+                with open(outs[i], "rb") as f:
+                    if hashlib.sha256(f.read()).hexdigest() != want[c]:
+                        raise SystemExit(f"bench stream: {outs[i]} differs from the reference bytes")
+                verified += 1
+        res = {
+            "metric": "Mpixels/s encoded host-to-host (PPM files -> .jpg files, PCIe and file I/O included)",
+            "value": round(px_all / el / 1e6, 1), "unit": "Mpixels/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int8-MFMA exact + fp64 replay (bit-exact)",
+            "data": f"synthetic: {n} PPM files of the config-3 recipe ({distinct} distinct contents) "
+                    f"written to {os.path.dirname(tmp)} before timing",
+            "config": {"workload": f"stream: {n} x {W}x{H} PPM files -> .jpg files per step through "
+                                   f"mij_stream ({args.stream_chunk}-frame chunks, 2 batches in ping-pong)",
+                       "files": n, "width": W, "height": H, "quality": args.quality,
+                       "chunk": args.stream_chunk, "parallelism": f"frame-parallel x{world}"},
+            "files_per_s": round(n * args.steps * world / el, 1),
+            # per step, summed over the chunks (host read/parse, GPU encode
+            # between its events, D2H + file writes): they overlap, so their sum
+            # exceeds the step
+            "stage_s_per_step": {k: round(agg[k] / args.steps, 4) for k in ("read_s", "gpu_s", "write_s")},
+            "input_GB_per_s": round(agg["bytes_in"] / el / 1e9, 2),
+            "verified_files": verified, "verified_contents_pinned_to_reference_sha": pinned,
+        }
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = stream_cpu_baseline(ins[:distinct], outs, W, H, args)
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def stream_cpu_baseline(ins, outs, W, H, args):
+    """The reference on the same files: utils/original.c's program (PPM file
+    -> .jpg file, byte-identical to main/encoder.c at Q=50; oracle/_ref,
+    compiled from the reference sources), one process per file, run
+    back to back on one core for ~--cpu-seconds; else the C restatement."""
+    import subprocess
+    import oracle as O
+    if os.path.exists(O.REF_QUALITY):
+        work = os.path.join(os.path.dirname(ins[0]), "ref")
+        os.makedirs(os.path.join(work, "hisParts"), exist_ok=True)
+        n, t0 = 0, time.perf_counter()
+        while True:
+            subprocess.check_call([O.REF_QUALITY, ins[n % len(ins)], str(args.quality)], cwd=work,
+                                  stdout=subprocess.DEVNULL)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= args.cpu_seconds and n >= 2:
+                break
+        kind, what = "reference", "utils/original.c program (oracle/_ref/ref_quality), file -> file"
+    else:
+        import ppm
+        n, t0 = 0, time.perf_counter()
+        while True:
+            with open(ins[n % len(ins)], "rb") as f:
+                rgb = ppm.parse_ppm(f.read())
+            with open(os.path.join(os.path.dirname(ins[0]), "cref.jpg"), "wb") as f:
+                f.write(O.cref_encode(np.ascontiguousarray(rgb[:, :, ::-1]), args.quality))
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= args.cpu_seconds and n >= 2:
+                break
+        kind, what = "port", "oracle/cpu_ref.c, file -> file"
+    return {"value": round(n * W * H / el / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": kind,
+            "sample": f"{n} files of {W}x{H} in {el:.1f} s, {what}"}
+
+
 def make_frames(args, rank):
     """Distinct config-3 frames (recipe in tests/recipes.py), rank-offset so
     ranks encode different content."""
@@ -640,6 +776,8 @@ def main():
         return run_detect(args, world, rank, local, dist)
     if args.workload == "decode":
         return run_decode(args, world, rank, local, dist)
+    if args.workload == "stream":
+        return run_stream(args, world, rank, local, dist)
     W, H, F = args.width, args.height, args.frames
     frames = make_frames(args, rank)
     gpu = 0 if dist is not None and dist.get_backend() != "nccl" else local

@@ -572,9 +572,11 @@ constexpr uint32_t TOK_AC = 1u << 10;
 #ifndef MIJ_K1_ACMERGE
 #define MIJ_K1_ACMERGE 0
 #endif
-// software pipelining of K1's N-tiles (A/B knob; see the N-tile loop)
+// software pipelining of K1's N-tiles, token variants (see the N-tile loop;
+// measured: token K1 3.504 -> 3.441 and 3.514 -> 3.459 ms, two A/B rounds on
+// one box; the coefficient variant spills at 168 VGPRs with it, 3.12 -> 3.18)
 #ifndef MIJ_K1_PIPE
-#define MIJ_K1_PIPE 0
+#define MIJ_K1_PIPE 1
 #endif
 #ifndef MIJ_K1_AREL
 #define MIJ_K1_AREL 0
@@ -1106,14 +1108,15 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
         // MIJ_K1_PIPE: N-tile nt + 1's MFMA chain is issued before N-tile nt
         // is quantised, so the wave's own quantisation covers the chain's
         // latency (two accumulator sets live)
-        v4i accs[MIJ_K1_PIPE ? 2 : 1][4];
-        float lcs[MIJ_K1_PIPE ? 2 : 1];  // per block: error bound of N in N units
-        if (MIJ_K1_PIPE) dct_ntile(0, accs[0], lcs[0]);
+        constexpr bool PIPE = MIJ_K1_PIPE && TOK;
+        v4i accs[PIPE ? 2 : 1][4];
+        float lcs[PIPE ? 2 : 1];  // per block: error bound of N in N units
+        if (PIPE) dct_ntile(0, accs[0], lcs[0]);
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
           const int comp = nt == 2 ? 1 : 0;
-          const int cur = MIJ_K1_PIPE ? (nt & 1) : 0;
-          if (!MIJ_K1_PIPE) {
+          const int cur = PIPE ? (nt & 1) : 0;
+          if (!PIPE) {
             dct_ntile(nt, accs[0], lcs[0]);
           } else if (nt + 1 < 3) {
 #if MIJ_K1_AREL
