@@ -125,23 +125,47 @@ def run_config4(args, world, rank, local, dist):
     # the root assembles on an assembler batch: tables, scan buffers and
     # outputs only (no whole-frame input, coefficient or token buffers)
     full = mijpeg.Batch(W, H, n, args.quality, device=gpu, assembler=True) if rank == 0 else None
-    xch = sharding.TorchExchange(dist, dist_device(dist, local)) if dist is not None \
-        else sharding.LocalExchange(f"cuda:{gpu}")
+    # device-resident protocol (mij_band_*_async) when the collectives can run
+    # on device tensors -- one rank or RCCL; gloo rehearses the host protocol
+    on_dev = dist is None or dist.get_backend() == "nccl"
+    if on_dev:
+        xch = sharding.DeviceExchange(dist, f"cuda:{gpu}")
+    else:
+        xch = sharding.TorchExchange(dist, dist_device(dist, local))
+
+    def step(events=None):
+        if on_dev:
+            sharding.encode_banded_dev(band, n, xch, full, events=events)
+        else:
+            sharding.encode_banded(band, n, xch, full)
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
     for _ in range(args.warmup):
-        sharding.encode_banded(band, n, xch, full)
+        step()
+    if full is not None:
+        full.sync()
+    band.sync()
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        sharding.encode_banded(band, n, xch, full)
+        step()
     if full is not None:
         full.sync()
+    band.sync()
     el = time.perf_counter() - t0
     barrier()
+    # per-phase times of one more step (device protocol: events on the band
+    # stream between the phases)
+    phases = None
+    if on_dev:
+        import torch
+        ev = []
+        step(ev)
+        torch.cuda.synchronize()
+        phases = {ev[i][0]: round(ev[i - 1][1].elapsed_time(ev[i][1]), 4) for i in range(1, len(ev))}
     el, _ = sharding.reduce_timing(el, 0, dist, dist_device(dist, local))
     verified = 0
     if rank == 0 and args.verify:
@@ -163,9 +187,12 @@ def run_config4(args, world, rank, local, dist):
                                f"exchanges and a packed-word gather to rank 0",
                    "frames_per_step": n, "width": W, "height": H, "quality": args.quality,
                    "parallelism": f"band-parallel x{world}",
-                   "backend": dist.get_backend() if dist is not None else "none"},
+                   "backend": dist.get_backend() if dist is not None else "none",
+                   "protocol": "device-resident (mij_band_*_async)" if on_dev else "host arrays (gloo)"},
         "verified_frames": verified,
     }
+    if phases:
+        res["phases_ms"] = phases
     if rank == 0:
         print(json.dumps(res), flush=True)
     band.close()

@@ -280,6 +280,28 @@ int mij_assemble_pieces(mij_batch *b, const void *src, size_t src_words, int src
                         const unsigned long long *pieces, int npieces);
 mij_batch *mij_assembler_create(int device, int width, int height, int max_frames, int quality);
 
+/* The same exchange steps, device-resident: every pointer is device memory
+ * and every call only enqueues work on the batch's stream (mij_batch_stream)
+ * -- nothing waits for the host, so the caller's collectives (RCCL on that
+ * same stream) run between the calls.  Shapes: last/prev int16 [n][4]
+ * (component c at [f][c]), hist uint32 [n][4][257], bits uint64 [n][3],
+ * allbits uint64 [world][n][3] (the bands' bits in rank order).
+ *   band_pack_async     this band's bit offsets from allbits, packs, and
+ *                       writes its total word count to *d_nwords;
+ *   band_words_async    moves those words, (frame, scan) order, to d_dst
+ *                       (sized by the caller from *d_nwords);
+ *   assemble_async      (root) tables from the summed histograms, every
+ *                       band's words OR-ed into the scans from d_src (band
+ *                       r's words at row r, stride_words apart) and the JFIF
+ *                       assembly; read the frames with mij_batch_output. */
+int mij_band_analyze_async(mij_batch *b, int n, int16_t *d_last);
+int mij_band_histograms_async(mij_batch *b, int n, const int16_t *d_prev, uint32_t *d_hist);
+int mij_band_tables_async(mij_batch *b, int n, const uint32_t *d_ghist, uint64_t *d_bits);
+int mij_band_pack_async(mij_batch *b, int n, const uint64_t *d_allbits, int world, int rank, uint64_t *d_nwords);
+int mij_band_words_async(mij_batch *b, int n, uint32_t *d_dst);
+int mij_assemble_async(mij_batch *b, int n, const uint32_t *d_ghist, const uint64_t *d_allbits, int world,
+                       const uint32_t *d_src, size_t stride_words);
+
 /* ---- diagnostics used by the test-suite -----------------------------------*/
 /* 16x16x64 i8 MFMA layout probe: A, B are 64 lanes x 16 int8, D 64 x 4 int32 */
 int mij_probe_mfma(const int8_t *A, const int8_t *B, int32_t *D);
@@ -293,6 +315,11 @@ int mij_colour_lut(uint32_t *out);
  * zigzag coefficient 16 g + k straddled a truncation boundary (replayed in
  * FP64), blocks in the batch's coefficient order (Y, Cb, Cr). */
 int mij_batch_audit(mij_batch *b, int nframes, uint16_t *masks);
+/* Tests: the four optimized tables of frames 0..n-1 built from given counts
+ * hist[f][4][257] (DC-Y, AC-Y, DC-C, AC-C; entry 256 is ignored, the
+ * reserved count of encoder.c:367 is 1); read them with mij_batch_tables.
+ * MIJ_ETABLE when a frame's counts have no valid table (mij_last_message). */
+int mij_batch_build_tables(mij_batch *b, int n, const uint32_t *hist);
 /* name of the code object target the library was built for ("gfx950") */
 const char *mij_build_target(void);
 

@@ -39,6 +39,11 @@ hipError_t launch_gather_regions(uint8_t *dst, long long slot_bytes, int pitch, 
                                  long long src_pitch, const int4 *regions, int n, int max_h,
                                  hipStream_t s);
 hipError_t launch_mfma_probe(const int4 *A, const int4 *B, int4 *D, hipStream_t s);
+hipError_t launch_band_last(const int16_t *dc, const Geom &g, int n, int16_t *last, hipStream_t s);
+hipError_t launch_band_place(const unsigned long long *allbits, int world, int rank, int n, uint32_t *bit_base,
+                             unsigned long long *pieces, unsigned long long *nwords, hipStream_t s);
+hipError_t launch_band_assembly(const unsigned long long *allbits, int world, int n, unsigned long long stride,
+                                unsigned long long *pieces, unsigned long long *scan_bits, int *over, hipStream_t s);
 }  // namespace mij
 
 using namespace mij;
@@ -274,6 +279,7 @@ struct mij_batch {
   // whole frames from band words needs -- tables, scan buffers, outputs
   bool assembler = false;
   std::vector<unsigned long long> band_words;  // per frame x 3: packed words after mij_band_pack
+  int band_async_n = 0;                        // frames of the last mij_band_pack_async
   // region batches (mij_batch_set_frame_dims / _gather_regions): per-frame
   // image size inside the canvas slots; d_frame stages a host frame
   int2 *d_fdims = nullptr;
@@ -1370,6 +1376,120 @@ static int upload_hist_tables(mij_batch *b, int n, const uint32_t *hist) {
   HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * n, b->stream));
   EntArgs a = ent_args(b, n);
   HIP_TRY(launch_tables(a, b->stream));
+  return MIJ_OK;
+}
+
+// ---------------------------------------------------------------------------
+// the same band protocol, device-resident: every argument
+// and result is device memory, every call only enqueues on the batch stream
+// (mij_batch_stream), so the caller's collectives can run on that stream
+// between the calls and nothing waits for the host.  Table failures stay in
+// the frames' error flags (the root's mij_batch_output reports them).
+// ---------------------------------------------------------------------------
+static int ensure_pieces(mij_batch *b, size_t n) {
+  if (b->pieces_cap >= n) return MIJ_OK;
+  // (a buffer the stream may still read: wait for it before freeing)
+  if (b->d_pieces) {
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    HIP_TRY(hipFree(b->d_pieces));
+  }
+  b->d_pieces = nullptr;
+  b->pieces_cap = 0;
+  HIP_TRY(dalloc(&b->d_pieces, n * 4));
+  b->pieces_cap = n;
+  return MIJ_OK;
+}
+
+extern "C" int mij_band_analyze_async(mij_batch *b, int n, int16_t *d_last) {
+  if (band_check(b, n, "band_analyze_async")) return g_err;
+  if (!d_last) return fail(MIJ_EINVAL, "band_analyze_async: null d_last");
+  HIP_TRY(hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * n * 4 * 257, b->stream));
+  HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * n, b->stream));
+  if (run_k1(b, n, 2)) return g_err;
+  HIP_TRY(launch_band_last(b->d_dc, b->g, n, d_last, b->stream));
+  return MIJ_OK;
+}
+
+extern "C" int mij_band_histograms_async(mij_batch *b, int n, const int16_t *d_prev, uint32_t *d_hist) {
+  if (band_check(b, n, "band_histograms_async")) return g_err;
+  if (!d_prev || !d_hist) return fail(MIJ_EINVAL, "band_histograms_async: null argument");
+  HIP_TRY(hipMemcpyAsync(b->d_dcpred, d_prev, sizeof(int16_t) * n * 4, hipMemcpyDeviceToDevice, b->stream));
+  EntArgs a = ent_args(b, n, 0, true);
+  HIP_TRY(launch_seg_dc(a, b->stream));
+  HIP_TRY(hipMemcpyAsync(d_hist, b->d_hist, sizeof(uint32_t) * n * 4 * 257, hipMemcpyDeviceToDevice, b->stream));
+  return MIJ_OK;
+}
+
+extern "C" int mij_band_tables_async(mij_batch *b, int n, const uint32_t *d_ghist, uint64_t *d_bits) {
+  if (band_check(b, n, "band_tables_async")) return g_err;
+  if (!d_ghist || !d_bits) return fail(MIJ_EINVAL, "band_tables_async: null argument");
+  HIP_TRY(hipMemcpyAsync(b->d_hist, d_ghist, sizeof(uint32_t) * n * 4 * 257, hipMemcpyDeviceToDevice, b->stream));
+  EntArgs a = ent_args(b, n, 0, true);
+  HIP_TRY(launch_tables(a, b->stream));
+  HIP_TRY(hipMemsetAsync(b->d_bitbase, 0, sizeof(uint32_t) * n * 4, b->stream));
+  HIP_TRY(launch_bits(a, b->stream));
+  HIP_TRY(launch_scan(a, b->stream));
+  HIP_TRY(hipMemcpyAsync(d_bits, b->d_scan_bits, sizeof(uint64_t) * n * 3, hipMemcpyDeviceToDevice, b->stream));
+  return MIJ_OK;
+}
+
+extern "C" int mij_band_pack_async(mij_batch *b, int n, const uint64_t *d_allbits, int world, int rank,
+                                   uint64_t *d_nwords) {
+  if (band_check(b, n, "band_pack_async")) return g_err;
+  if (!d_allbits || !d_nwords || world < 1 || rank < 0 || rank >= world)
+    return fail(MIJ_EINVAL, "band_pack_async: bad arguments");
+  if (ensure_pieces(b, (size_t)n * 3)) return g_err;
+  HIP_TRY(launch_band_place((const unsigned long long *)d_allbits, world, rank, n, b->d_bitbase, b->d_pieces,
+                            (unsigned long long *)d_nwords, b->stream));
+  EntArgs a = ent_args(b, n, 0, true);
+  if (b->raw_dirty) HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->raw_dirty * b->g.raw_fs, b->stream));
+  b->raw_dirty = n;
+  HIP_TRY(launch_pack_lb(a, b->stream));
+  b->band_async_n = n;
+  return MIJ_OK;
+}
+
+extern "C" int mij_band_words_async(mij_batch *b, int n, uint32_t *d_dst) {
+  if (band_check(b, n, "band_words_async")) return g_err;
+  if (!d_dst || n != b->band_async_n) return fail(MIJ_EINVAL, "band_words_async: needs mij_band_pack_async of the same frames first");
+  // the move table of mij_band_pack_async, words of frames 0..n-1 in (frame,
+  // scan) order into d_dst (the caller sized it from that call's word
+  // count), zeroed behind
+  HIP_TRY(launch_move_pieces(b->d_raw, b->g, d_dst, b->d_pieces, n * 3, 64 * 1024, b->stream));
+  if (n >= b->raw_dirty) b->raw_dirty = 0;
+  return MIJ_OK;
+}
+
+extern "C" int mij_assemble_async(mij_batch *b, int n, const uint32_t *d_ghist, const uint64_t *d_allbits, int world,
+                                  const uint32_t *d_src, size_t stride_words) {
+  if (band_check(b, n, "assemble_async", true)) return g_err;
+  if (!d_ghist || !d_allbits || !d_src || world < 1) return fail(MIJ_EINVAL, "assemble_async: bad arguments");
+  if (ensure_pieces(b, (size_t)world * n * 3)) return g_err;
+  HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * n * b->g.raw_fs, b->stream));
+  b->raw_dirty = std::max(b->raw_dirty, n);
+  HIP_TRY(hipMemcpyAsync(b->d_hist, d_ghist, sizeof(uint32_t) * n * 4 * 257, hipMemcpyDeviceToDevice, b->stream));
+  HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * n, b->stream));
+  EntArgs a = ent_args(b, n);
+  HIP_TRY(launch_tables(a, b->stream));
+  HIP_TRY(launch_band_assembly((const unsigned long long *)d_allbits, world, n, stride_words, b->d_pieces,
+                               (unsigned long long *)b->d_scan_bits, b->d_err, b->stream));
+  HIP_TRY(launch_or_pieces(b->d_raw, b->g, d_src, b->d_pieces, world * n * 3, (long long)stride_words, b->stream));
+  HIP_TRY(launch_emit(a, b->stream));  // k_emit_write zeroes the words it reads
+  if (n >= b->raw_dirty) b->raw_dirty = 0;
+  b->last_frames = n;
+  return MIJ_OK;
+}
+
+// tests: the four tables of frames 0..n-1 from given counts (k_tables alone)
+extern "C" int mij_batch_build_tables(mij_batch *b, int n, const uint32_t *hist) {
+  if (band_check(b, n, "build_tables", true)) return g_err;
+  if (!hist) return fail(MIJ_EINVAL, "build_tables: null hist");
+  if (upload_hist_tables(b, n, hist)) return g_err;
+  std::vector<int> err((size_t)n);
+  HIP_TRY(hipMemcpyAsync(err.data(), b->d_err, sizeof(int) * n, hipMemcpyDeviceToHost, b->stream));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  for (int f = 0; f < n; f++)
+    if (err[f]) return fail(MIJ_ETABLE, "frame %d: Huffman table construction failed", f);
   return MIJ_OK;
 }
 

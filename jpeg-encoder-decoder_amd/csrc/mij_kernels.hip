@@ -1122,7 +1122,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
 #if MIJ_K1_AREL
             asm volatile("" ::: "memory");  // A fragments re-read from LDS per N-tile
 #endif
-            dct_ntile(nt + 1, accs[cur ^ 1], lcs[cur ^ 1]);
+            dct_ntile(nt + 1, accs[PIPE ? (cur ^ 1) : 0], lcs[PIPE ? (cur ^ 1) : 0]);
           }
           v4i(&acc)[4] = accs[cur];
           const float lc = lcs[cur];
@@ -1492,6 +1492,20 @@ __global__ __launch_bounds__(256) void k_seg_dc(EntArgs a) {
 // tracked by root label (code_len += 1 for both chains, :213-227) and the
 // `next` links are kept so the whole huff_code struct matches.
 // ===========================================================================
+// MIJ_TAB_QUEUE (default): the merge loop as the two-queue Huffman
+// construction -- the live nodes' keys (frequency, then the highest index
+// first: the <= scan of encoder.c:196-206) in two ascending queues, the
+// leaves sorted once (bitonic, in registers) and the merged nodes appended
+// in creation order (their frequencies never decrease; an equal-frequency
+// tie is inserted at its key's place), so v1 and v2 are always among the
+// four queue heads: O(1) per merge instead of a 64-lane top-2 reduction.
+// The queues live in LDS and every lane reads their heads (broadcast), so
+// each merge costs one LDS round trip and a few uniform VALU selects; the
+// code lengths come from the merge tree afterwards (pointer jumping).
+#ifndef MIJ_TAB_QUEUE
+#define MIJ_TAB_QUEUE 1
+#endif
+
 struct TabScratch {
   int next[257];
   int tail[257];
@@ -1505,6 +1519,16 @@ struct TabScratch {
   int scode[256];
   int n;
   int err;
+#if MIJ_TAB_QUEUE
+  // the two-queue merge (build_table_wave): keys of the sorted leaves (symbol
+  // 256 first) and of the merged nodes, ~0 past their ends; the merge tree
+  // (leaves 0..256, merge j = node 257 + j) and each label's current node
+  unsigned long long ql[260], qm[260];
+  int parent[514];
+  int depth[514];
+  int cur[257];
+  int fin[257];  // sym_freq after the merges (:221-222)
+#endif
 };
 
 __device__ __forceinline__ void top2(unsigned long long &k1, unsigned long long &k2,
@@ -1583,6 +1607,148 @@ __device__ void build_table_wave(const uint32_t *hist, const uint32_t *extra, Hu
   }
   if (lane < 32) { S->clf[lane] = 0; S->cnt[lane] = 0; }
   wave_lds_sync();
+#if MIJ_TAB_QUEUE
+  {
+    // the leaves: symbols 0..255 with a nonzero count, ascending by key
+    // (symbol 256 -- count 1, highest index -- is the smallest key of all and
+    // heads the queue); bitonic sort in registers, element i of the order in
+    // lane i & 63 of skey[i >> 6]
+    unsigned long long skey[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int sy = lane + 64 * r;
+      skey[r] = f[r] ? ((unsigned long long)f[r] << 9) | (unsigned)(256 - sy) : ~0ull;
+    }
+#pragma unroll
+    for (int k = 2; k <= 256; k <<= 1)
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        if (j >= 64) {
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int rp = r ^ (j >> 6);
+            if (rp > r) {
+              const bool up = (((lane + 64 * r) & k) == 0);
+              const unsigned long long x = skey[r], y = skey[rp];
+              const unsigned long long lo = x < y ? x : y, hi = x < y ? y : x;
+              skey[r] = up ? lo : hi;
+              skey[rp] = up ? hi : lo;
+            }
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const unsigned long long o = __shfl_xor(skey[r], j);
+            const bool up = (((lane + 64 * r) & k) == 0), lower = (lane & j) == 0;
+            const unsigned long long lo = skey[r] < o ? skey[r] : o, hi = skey[r] < o ? o : skey[r];
+            skey[r] = lower == up ? lo : hi;
+          }
+        }
+      }
+    int nl = 1;  // leaves: symbol 256 + the nonzero counts of 0..255
+#pragma unroll
+    for (int r = 0; r < 4; r++) nl += __popcll(__ballot(f[r] != 0));
+#pragma unroll
+    for (int r = 0; r < 4; r++) S->ql[1 + lane + 64 * r] = skey[r];
+    if (lane == 0) S->ql[0] = 512ull;  // symbol 256: count 1, index 256
+    if (lane < 3) S->ql[257 + lane] = ~0ull;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      const int sy = lane + 64 * i;
+      if (sy < 260) S->qm[sy] = ~0ull;
+      if (sy < 257) {
+        S->cur[sy] = sy;
+        S->fin[sy] = (int)f[i];
+        S->parent[sy] = -1;
+      }
+    }
+    wave_lds_sync();
+    // every lane runs the loop on the same (uniform) values; lane 0 alone
+    // writes.  v1 = the least key, v2 = the next (encoder.c:196-206)
+    int lh = 0, mh = 0, mt = 0;
+    unsigned long long mlast = 0;  // key of qm[mt - 1]
+    for (int step = 0; step + 1 < nl; step++) {
+      const unsigned long long a0 = S->ql[lh], b0 = S->ql[lh + 1], c0 = S->qm[mh], d0 = S->qm[mh + 1];
+      const bool ac = a0 < c0;
+      const unsigned long long k1 = ac ? a0 : c0, x = ac ? b0 : a0, y = ac ? c0 : d0;
+      const bool bx = x < y;  // x is a leaf, y a merged node
+      const unsigned long long k2 = bx ? x : y;
+      lh += (int)ac + (int)bx;
+      mh += 2 - (int)ac - (int)bx;
+      const int v1 = 256 - (int)(k1 & 511), v2 = 256 - (int)(k2 & 511);
+      const uint32_t fs = (uint32_t)(k1 >> 9) + (uint32_t)(k2 >> 9);
+      const unsigned long long K = ((unsigned long long)fs << 9) | (unsigned)(256 - v1);
+      // merged frequencies never decrease: an append, unless an equal-count
+      // node with a smaller key than K is already queued (rare)
+      int pos = mt;
+      if (mt > mh && mlast > K) {
+        while (pos > mh && S->qm[pos - 1] > K) {
+          if (lane == 0) S->qm[pos] = S->qm[pos - 1];
+          wave_lds_sync();
+          pos--;
+        }
+      }
+      if (lane == 0) {
+        S->qm[pos] = K;
+        S->fin[v1] = (int)fs;  // :221-222
+        S->fin[v2] = 0;
+        // :223-226: v2's chain joins v1's (next[tail(v1)] = v2), both one
+        // code bit longer -- the merge tree's node 257 + step
+        const int node = 257 + step;
+        S->parent[S->cur[v1]] = node;
+        S->parent[S->cur[v2]] = node;
+        S->parent[node] = -1;
+        S->cur[v1] = node;
+        const int t1 = S->tail[v1];
+        S->next[t1] = v2;
+        S->tail[v1] = S->tail[v2];
+      }
+      if (pos == mt) mlast = K;
+      mt++;
+      wave_lds_sync();
+    }
+    // code lengths = leaf depths in the merge tree (pointer jumping: nine
+    // rounds cover <= 513 nodes)
+    const int nnodes = 257 + max(nl - 1, 0);
+    int dp[9], pp[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      const int nd = lane + 64 * i;
+      pp[i] = nd < nnodes ? S->parent[nd] : -1;
+      dp[i] = pp[i] >= 0 ? 1 : 0;
+      if (nd < nnodes) S->depth[nd] = dp[i];
+    }
+    wave_lds_sync();
+    for (int round = 0; round < 9; round++) {
+      int nd2[9], np2[9];
+#pragma unroll
+      for (int i = 0; i < 9; i++) {
+        nd2[i] = pp[i] >= 0 ? dp[i] + S->depth[pp[i]] : dp[i];
+        np2[i] = pp[i] >= 0 ? S->parent[pp[i]] : -1;
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int i = 0; i < 9; i++) {
+        const int nd = lane + 64 * i;
+        dp[i] = nd2[i];
+        pp[i] = np2[i];
+        if (nd < nnodes) {
+          S->depth[nd] = dp[i];
+          S->parent[nd] = pp[i];
+        }
+      }
+      wave_lds_sync();
+    }
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      const int sy = lane + 64 * i;
+      if (sy < 257) {
+        cl[i] = dp[i];
+        f[i] = (uint32_t)S->fin[sy];
+      }
+    }
+  }
+#else
   for (;;) {
     unsigned long long k1 = ~0ull, k2 = ~0ull;
 #pragma unroll
@@ -1631,6 +1797,7 @@ __device__ void build_table_wave(const uint32_t *hist, const uint32_t *extra, Hu
     }
     wave_lds_sync();
   }
+#endif
   wave_lds_sync();
   int bad = 0;
 #pragma unroll
@@ -1863,8 +2030,15 @@ __global__ void k_scan(EntArgs a) {
     const unsigned long long excl = carry + x - v;
     if (i < ns) {
       a.seg_off[f0 + i] = excl;
-      if (i % PACK_SEGS == 0) raw[excl >> 5] = 0;
-      if (i % PACK_SEGS == PACK_SEGS - 1 || i == ns - 1) raw[(excl + v - 1) >> 5] = 0;
+      // (bits past the scan buffer: tokens that no K1 wrote -- flag the frame,
+      // never write out of bounds)
+      const unsigned long long wl = excl >> 5, wh = (excl + v - 1) >> 5;
+      if (wh >= (unsigned long long)a.g.raw_words[comp]) {
+        a.err[f] = 2;
+      } else {
+        if (i % PACK_SEGS == 0) raw[wl] = 0;
+        if (i % PACK_SEGS == PACK_SEGS - 1 || i == ns - 1) raw[wh] = 0;
+      }
     }
     carry += __shfl(x, 63);
   }
@@ -2662,6 +2836,75 @@ __global__ void k_move_pieces(uint32_t *raw, long long raw_fs, long long rw0, lo
     src[i] = 0u;
   }
 }
+// ---- one large frame in bands, device-resident control (mij_band_*_async):
+// the small per-frame values the bands exchange stay in HBM and these kernels
+// turn them into the next step's arguments, so no step waits for the host.
+// One thread per frame (n <= a batch's frames).
+
+// the last raw DC of every component of frames 0..n-1 (the next band's
+// predictors, encoder.c:168-177) -> last[f * 4 + c]
+__global__ void k_band_last(const int16_t *dc, Geom g, int n, int16_t *last) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= n) return;
+  const long long fb = (long long)f * g.nblk;
+  last[f * 4 + 0] = dc[fb + g.nY - 1];
+  last[f * 4 + 1] = dc[fb + g.nY + g.nC - 1];
+  last[f * 4 + 2] = dc[fb + g.nY + 2LL * g.nC - 1];
+  last[f * 4 + 3] = 0;
+}
+
+// this band's place in every scan from the gathered bit counts allbits[world][n][3]:
+// its start bit (the exclusive sum over the bands before it) in-word offset
+// -> bit_base[f * 4 + c], its word count, and the (frame, scan)-ordered move
+// table {frame * 3 + scan, words, first destination word} -> pieces; the
+// band's total words -> nwords[0]
+__global__ void k_band_place(const unsigned long long *allbits, int world, int rank, int n, uint32_t *bit_base,
+                             unsigned long long *pieces, unsigned long long *nwords) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  unsigned long long at = 0;
+  for (int f = 0; f < n; f++)
+    for (int c = 0; c < 3; c++) {
+      unsigned long long off = 0;
+      for (int r = 0; r < rank; r++) off += allbits[((long long)r * n + f) * 3 + c];
+      const unsigned long long bits = allbits[((long long)rank * n + f) * 3 + c];
+      const unsigned long long nw = ((off & 31) + bits + 31) >> 5;
+      bit_base[f * 4 + c] = (uint32_t)(off & 31);
+      unsigned long long *pc = pieces + 3 * (f * 3 + c);
+      pc[0] = (unsigned long long)(f * 3 + c);
+      pc[1] = nw;
+      pc[2] = at;
+      at += nw;
+    }
+  nwords[0] = at;
+}
+
+// the root's assembly table from allbits[world][n][3] for a gathered buffer
+// whose band-r row (stride words) holds that band's words in (frame, scan)
+// order: piece (r, f, c) = {frame * 3 + scan, first word in the scan, first
+// source word, words}; the scans' total bits -> scan_bits[f * 3 + c]
+__global__ void k_band_assembly(const unsigned long long *allbits, int world, int n, unsigned long long stride,
+                                unsigned long long *pieces, unsigned long long *scan_bits, int *over) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  for (int f = 0; f < n; f++)
+    for (int c = 0; c < 3; c++) scan_bits[f * 3 + c] = 0;
+  for (int r = 0; r < world; r++) {
+    unsigned long long at = 0;
+    for (int f = 0; f < n; f++)
+      for (int c = 0; c < 3; c++) {
+        const unsigned long long off = scan_bits[f * 3 + c], bits = allbits[((long long)r * n + f) * 3 + c];
+        const unsigned long long nw = ((off & 31) + bits + 31) >> 5;
+        unsigned long long *pc = pieces + 4 * (((long long)r * n + f) * 3 + c);
+        pc[0] = (unsigned long long)(f * 3 + c);
+        pc[1] = off >> 5;
+        pc[2] = (unsigned long long)r * stride + at;
+        pc[3] = nw;
+        at += nw;
+        scan_bits[f * 3 + c] = off + bits;
+      }
+    if (at > stride) *over = 1;  // a band's words beyond its row: assemble nothing wrong
+  }
+}
+
 // ---- tiny self-test used by the test-suite: exact i8 MFMA layout check ----
 __global__ void k_mfma_probe(const int4 *A, const int4 *B, int4 *D) {
   const int lane = threadIdx.x;
@@ -2806,6 +3049,21 @@ hipError_t launch_move_pieces(uint32_t *raw, const Geom &g, uint32_t *dst,
   const long long chunks = (max_words + 1023) / 1024;
   hipLaunchKernelGGL(k_move_pieces, dim3((unsigned)(chunks < 64 ? chunks : 64), (unsigned)npieces), dim3(256), 0, s,
                      raw, g.raw_fs, g.raw_words[0], g.raw_words[1], dst, d_pieces);
+  return hipGetLastError();
+}
+
+hipError_t launch_band_last(const int16_t *dc, const Geom &g, int n, int16_t *last, hipStream_t s) {
+  hipLaunchKernelGGL(k_band_last, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, dc, g, n, last);
+  return hipGetLastError();
+}
+hipError_t launch_band_place(const unsigned long long *allbits, int world, int rank, int n, uint32_t *bit_base,
+                             unsigned long long *pieces, unsigned long long *nwords, hipStream_t s) {
+  hipLaunchKernelGGL(k_band_place, dim3(1), dim3(64), 0, s, allbits, world, rank, n, bit_base, pieces, nwords);
+  return hipGetLastError();
+}
+hipError_t launch_band_assembly(const unsigned long long *allbits, int world, int n, unsigned long long stride,
+                                unsigned long long *pieces, unsigned long long *scan_bits, int *over, hipStream_t s) {
+  hipLaunchKernelGGL(k_band_assembly, dim3(1), dim3(64), 0, s, allbits, world, n, stride, pieces, scan_bits, over);
   return hipGetLastError();
 }
 

@@ -24,10 +24,12 @@ EXPORTS = [
     "mij_batch_create", "mij_batch_destroy", "mij_batch_upload", "mij_batch_set_input",
     "mij_batch_encode", "mij_batch_keep_coefs", "mij_batch_set_split", "mij_batch_set_overlap", "mij_batch_dct", "mij_batch_sync", "mij_batch_output",
     "mij_batch_lengths", "mij_batch_coefs", "mij_batch_tables", "mij_batch_set_timing",
-    "mij_batch_stage_ms", "mij_batch_stage_history", "mij_batch_token_count", "mij_batch_geometry", "mij_batch_replays", "mij_batch_stream", "mij_batch_audit",
+    "mij_batch_stage_ms", "mij_batch_stage_history", "mij_batch_token_count", "mij_batch_geometry", "mij_batch_replays", "mij_batch_stream", "mij_batch_audit", "mij_batch_build_tables",
     "mij_band_analyze", "mij_band_histograms", "mij_band_tables", "mij_band_pack", "mij_band_words",
     "mij_assemble_begin", "mij_assemble_words", "mij_assemble_end",
     "mij_band_words_all", "mij_assemble_pieces", "mij_assembler_create",
+    "mij_band_analyze_async", "mij_band_histograms_async", "mij_band_tables_async", "mij_band_pack_async",
+    "mij_band_words_async", "mij_assemble_async",
     "mij_probe_mfma", "mij_colour_lut", "mij_build_target",
     # change detector (reference include/brain.h:7-10 drop-in + extensions)
     "subsample", "store", "compare", "enlargeAdjust", "mij_set_frame_height",
@@ -106,6 +108,13 @@ def load() -> C.CDLL:
     lib.mij_batch_set_overlap.argtypes = [p, i]
     lib.mij_batch_dct.argtypes = [p, i]
     lib.mij_batch_audit.argtypes = [p, i, p]
+    lib.mij_band_analyze_async.argtypes = [p, i, p]
+    lib.mij_band_histograms_async.argtypes = [p, i, p, p]
+    lib.mij_band_tables_async.argtypes = [p, i, p, p]
+    lib.mij_band_pack_async.argtypes = [p, i, p, i, i, p]
+    lib.mij_band_words_async.argtypes = [p, i, p]
+    lib.mij_assemble_async.argtypes = [p, i, p, p, i, p, sz]
+    lib.mij_batch_build_tables.argtypes = [p, i, p]
     lib.mij_batch_sync.argtypes = [p]
     lib.mij_batch_output.argtypes = [p, i, p, sz, C.POINTER(sz)]
     lib.mij_batch_lengths.argtypes = [p, C.POINTER(sz), i]
@@ -437,6 +446,12 @@ class Batch:
         m = m.astype(np.uint64)
         return m[..., 0] | (m[..., 1] << np.uint64(16)) | (m[..., 2] << np.uint64(32)) | (m[..., 3] << np.uint64(48))
 
+    def build_tables(self, n: int, hist: np.ndarray) -> None:
+        """the four tables of frames 0..n-1 from given counts [n, 4, 257]
+        (mij_batch_build_tables; read them with tables())"""
+        h = np.ascontiguousarray(hist, np.uint32).reshape(n, 4, 257)
+        _check(self.lib.mij_batch_build_tables(self.h_, n, _ptr(h)), "build_tables")
+
     def replays(self) -> int:
         return int(self.lib.mij_batch_replays(self.h_))
 
@@ -497,6 +512,30 @@ class Batch:
             w = np.ascontiguousarray(src).view(np.uint32).reshape(-1)
             _check(self.lib.mij_assemble_pieces(self.h_, _ptr(w), w.size, 0, _ptr(pc), pc.shape[0]),
                    "assemble_pieces")
+
+    # ---- the device-resident band protocol (all pointers device memory) ----
+    def stream_ptr(self) -> int:
+        """the batch's HIP stream (hipStream_t), for torch.cuda.ExternalStream"""
+        return int(self.lib.mij_batch_stream(self.h_) or 0)
+
+    def band_analyze_async(self, n: int, d_last: int) -> None:
+        _check(self.lib.mij_band_analyze_async(self.h_, n, d_last), "band_analyze_async")
+
+    def band_histograms_async(self, n: int, d_prev: int, d_hist: int) -> None:
+        _check(self.lib.mij_band_histograms_async(self.h_, n, d_prev, d_hist), "band_histograms_async")
+
+    def band_tables_async(self, n: int, d_ghist: int, d_bits: int) -> None:
+        _check(self.lib.mij_band_tables_async(self.h_, n, d_ghist, d_bits), "band_tables_async")
+
+    def band_pack_async(self, n: int, d_allbits: int, world: int, rank: int, d_nwords: int) -> None:
+        _check(self.lib.mij_band_pack_async(self.h_, n, d_allbits, world, rank, d_nwords), "band_pack_async")
+
+    def band_words_async(self, n: int, d_dst: int) -> None:
+        _check(self.lib.mij_band_words_async(self.h_, n, d_dst), "band_words_async")
+
+    def assemble_async(self, n: int, d_ghist: int, d_allbits: int, world: int, d_src: int, stride_words: int) -> None:
+        _check(self.lib.mij_assemble_async(self.h_, n, d_ghist, d_allbits, world, d_src, stride_words),
+               "assemble_async")
 
     def assemble_begin(self, n: int, hist: np.ndarray) -> None:
         h = np.ascontiguousarray(hist, np.uint32).reshape(n, 4, 257)

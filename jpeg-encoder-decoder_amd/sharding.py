@@ -205,3 +205,104 @@ def encode_banded(band, n: int, xch, frame_batch=None):
         frame_batch.assemble_pieces(pieces, src=gathered.numpy())
     frame_batch.assemble_end(n, total)
     return total
+
+
+# ---------------------------------------------------------------------------
+# the band protocol device-resident (include/mijpeg.h mij_band_*_async):
+# every exchanged value stays in HBM, every library call and collective is
+# enqueued on the band batch's own HIP stream; one host read per step (the
+# largest band's word count, to size the gather)
+# ---------------------------------------------------------------------------
+
+class DeviceExchange:
+    """Collectives on device tensors for encode_banded_dev: torch.distributed
+    (nccl = RCCL over xGMI) with the current stream set to the band batch's
+    stream, or the identities of one rank (dist None).  Every result is a
+    device tensor; nothing is copied to the host."""
+
+    def __init__(self, dist=None, device="cuda:0"):
+        import torch
+        self.torch, self.dist, self.device = torch, dist, device
+        self.world = dist.get_world_size() if dist is not None else 1
+        self.rank = dist.get_rank() if dist is not None else 0
+
+    def all_gather(self, t):
+        """[world, *t.shape] (t's bytes, any dtype)"""
+        if self.world == 1:
+            return t.unsqueeze(0)
+        out = self.torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        self.dist.all_gather_into_tensor(out, t.contiguous())
+        return out
+
+    def all_reduce_sum(self, t):
+        if self.world > 1:
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return t
+
+    def gather(self, buf):
+        """every rank's equally sized buffer to the root: [world, n] there"""
+        if self.world == 1:
+            return buf.reshape(1, -1)
+        if self.rank == 0:
+            out = self.torch.empty((self.world, buf.numel()), dtype=buf.dtype, device=buf.device)
+            self.dist.gather(buf, gather_list=list(out.unbind(0)), dst=0)
+            return out
+        self.dist.gather(buf, dst=0)
+        return None
+
+
+def encode_banded_dev(band, n: int, xch, frame_batch=None, events=None):
+    """encode_banded with the device-resident protocol: the last DCs (int16
+    [n, 4], gathered as int32 pairs), the histograms (summed in place), the
+    bit counts (gathered) and the packed words (gathered to the root) never
+    leave HBM; the library calls and the collectives all run on the band
+    batch's stream.  The root's frame_batch (an assembler) waits for that
+    stream and assembles on its own.  `events`: optional list that receives
+    (name, torch.cuda.Event) pairs recorded on the band stream after each
+    phase.  Returns nothing; read the frames from frame_batch.output()."""
+    torch = xch.torch
+    rank, world = xch.rank, xch.world
+    dev = xch.device
+    s = torch.cuda.ExternalStream(band.stream_ptr(), device=dev)
+
+    def mark(name):
+        if events is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(s)
+            events.append((name, e))
+
+    with torch.cuda.stream(s):
+        mark("start")
+        last = torch.empty((n, 4), dtype=torch.int16, device=dev)
+        band.band_analyze_async(n, last.data_ptr())
+        mark("analyze")
+        lasts = xch.all_gather(last.view(torch.int32))           # [world, n, 2] = int16 [world, n, 4]
+        prev = torch.zeros((n, 4), dtype=torch.int16, device=dev) if rank == 0 else \
+            lasts[rank - 1].contiguous().view(torch.int16)
+        hist = torch.empty((n, 4, 257), dtype=torch.int32, device=dev)
+        band.band_histograms_async(n, prev.data_ptr(), hist.data_ptr())
+        xch.all_reduce_sum(hist)
+        mark("histograms")
+        bits = torch.empty((n, 3), dtype=torch.int64, device=dev)
+        band.band_tables_async(n, hist.data_ptr(), bits.data_ptr())
+        allbits = xch.all_gather(bits).contiguous()               # [world, n, 3]
+        mark("tables")
+        nw = torch.empty(1, dtype=torch.int64, device=dev)
+        band.band_pack_async(n, allbits.data_ptr(), world, rank, nw.data_ptr())
+        stride = int(xch.all_gather(nw).max().item())             # the one host read of a step
+        mark("pack")
+        buf = torch.empty(max(stride, 1), dtype=torch.int32, device=dev)
+        band.band_words_async(n, buf.data_ptr())
+        gathered = xch.gather(buf)
+        mark("words")
+        if rank != 0:
+            return
+    a = torch.cuda.ExternalStream(frame_batch.stream_ptr(), device=dev)
+    a.wait_stream(s)
+    with torch.cuda.stream(a):
+        frame_batch.assemble_async(n, hist.data_ptr(), allbits.data_ptr(), world, gathered.data_ptr(),
+                                   gathered.shape[1])
+    # the tensors read by the assembly are freed on the band stream: keep that
+    # stream behind the assembly
+    s.wait_stream(a)
+    mark("assemble")

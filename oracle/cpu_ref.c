@@ -282,6 +282,14 @@ static int build_table(cref_huff *hc) {
     return 0;
 }
 
+/* One table from a histogram of symbols 0..255 (encoder.c:180-301, with the
+ * reserved count sym_freq[256] = 1 of :367); 0, or the error of build_table. */
+int cref_build_table(const uint32_t freq[256], cref_huff *hc) {
+    for (int i = 0; i < 256; i++) hc->sym_freq[i] = (int)freq[i];
+    hc->sym_freq[256] = 1;
+    return build_table(hc);
+}
+
 int cref_init_huffman(const int16_t *Y, const int16_t *Cb, const int16_t *Cr,
                       cref_area d, cref_huff luma[2], cref_huff chroma[2]) {
     cref_huff *t[4] = {&luma[0], &luma[1], &chroma[0], &chroma[1]};

@@ -44,6 +44,10 @@ void cref_rgb_to_dct(const uint8_t *bgr, int stride_px, int16_t *Y, int16_t *Cb,
 int cref_init_huffman(const int16_t *Y, const int16_t *Cb, const int16_t *Cr,
                       cref_area d, cref_huff luma[2], cref_huff chroma[2]);
 
+/* encoder.c:180-301 for one histogram of symbols 0..255 (+ the reserved
+ * sym_freq[256] = 1 of :367).  0 on success. */
+int cref_build_table(const uint32_t freq[256], cref_huff *hc);
+
 /* encoder.c:549-644 (+383-532).  Writes into jpg, returns byte count. */
 size_t cref_write_jpg(uint8_t *jpg, const int16_t *Y, const int16_t *Cb,
                       const int16_t *Cr, cref_area d, const cref_huff luma[2],

@@ -64,6 +64,8 @@ def cref() -> C.CDLL:
         lib.cref_rgb_to_dct.argtypes = [p, C.c_int, p, p, p, Area, p, p]
         lib.cref_init_huffman.restype = C.c_int
         lib.cref_init_huffman.argtypes = [p, p, p, Area, p, p]
+        lib.cref_build_table.restype = C.c_int
+        lib.cref_build_table.argtypes = [p, p]
         lib.cref_write_jpg.restype = C.c_size_t
         lib.cref_write_jpg.argtypes = [p, p, p, p, Area, p, p, p, p]
         lib.cref_quality_tables.argtypes = [C.c_int, p, p]
@@ -194,6 +196,15 @@ def cref_encode(bgr: np.ndarray, quality: int = 50, region=None) -> bytes:
     if n == 0:
         raise ValueError("cref_encode rejected the input")
     return out[:n].tobytes()
+
+
+def cref_build_table(freq: np.ndarray):
+    """(rc, Huff) of one table built from counts of symbols 0..255
+    (encoder.c:180-301; sym_freq[256] = 1 as :367 sets it)."""
+    f = np.ascontiguousarray(freq, np.uint32).reshape(256)
+    h = Huff()
+    rc = cref().cref_build_table(_ptr(f), C.addressof(h))
+    return rc, h
 
 
 def cref_stages(bgr: np.ndarray, quality: int = 50, region=None):

@@ -253,3 +253,116 @@ def test_two_process_frame_parallel_hip_gloo():
         assert p.exitcode == 0
     assert (el, units) == (2.0, 5)
     assert blobs == [O.cref_encode(recipes.config3_frame(f, 160, 256)) for f in range(5)]
+
+
+# ---------------------------------------------------------------------------
+# the device-resident protocol (mij_band_*_async, sharding.encode_banded_dev)
+# ---------------------------------------------------------------------------
+
+def _dev_bands(port, q):
+    """In a fresh process (torch's HIP runtime first): W bands of the same
+    frames in one process through the async calls, the exchanges done with
+    torch ops on device tensors (full syncs between the steps), for W = 1..4;
+    then encode_banded_dev itself over a one-rank nccl group (ExternalStream
+    on the band batch's stream, RCCL collectives) twice in a row."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    import mijpeg
+    import recipes
+    dev = "cuda:0"
+    frames = np.stack([recipes.config3_frame(5, 320, 480), recipes.noise(320, 480, 9),
+                       recipes.config3_frame(6, 320, 480)])
+    n, H, W = frames.shape[:3]
+    res = {}
+    for world in (1, 2, 3, 4):
+        bands = []
+        for r in range(world):
+            r0, rows = sharding.band_rows(H, world, r)
+            b = mijpeg.Batch(W, rows, n)
+            b.upload(np.ascontiguousarray(frames[:, r0:r0 + rows]))
+            bands.append(b)
+        last = [torch.empty((n, 4), dtype=torch.int16, device=dev) for _ in bands]
+        for b, l in zip(bands, last):
+            b.band_analyze_async(n, l.data_ptr())
+            b.sync()
+        hist = [torch.empty((n, 4, 257), dtype=torch.int32, device=dev) for _ in bands]
+        zero = torch.zeros((n, 4), dtype=torch.int16, device=dev)
+        torch.cuda.synchronize()  # (torch zeroes it on its own stream)
+        for r, b in enumerate(bands):
+            b.band_histograms_async(n, (zero if r == 0 else last[r - 1]).data_ptr(), hist[r].data_ptr())
+            b.sync()
+        ghist = torch.stack(hist).sum(0, dtype=torch.int32).contiguous()
+        torch.cuda.synchronize()
+        bits = [torch.empty((n, 3), dtype=torch.int64, device=dev) for _ in bands]
+        for b, t in zip(bands, bits):
+            b.band_tables_async(n, ghist.data_ptr(), t.data_ptr())
+            b.sync()
+        allbits = torch.stack(bits).contiguous()
+        torch.cuda.synchronize()
+        nw = [torch.empty(1, dtype=torch.int64, device=dev) for _ in bands]
+        for r, b in enumerate(bands):
+            b.band_pack_async(n, allbits.data_ptr(), world, r, nw[r].data_ptr())
+            b.sync()
+        stride = max(int(x.item()) for x in nw)
+        gathered = torch.zeros((world, stride), dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        for r, b in enumerate(bands):
+            b.band_words_async(n, gathered[r].data_ptr())
+            b.sync()
+        full = mijpeg.Batch(W, H, n, assembler=True)
+        full.assemble_async(n, ghist.data_ptr(), allbits.data_ptr(), world, gathered.data_ptr(), stride)
+        full.sync()
+        res[world] = [full.output(f) for f in range(n)]
+        # the band batches encode whole frames correctly afterwards
+        bands[-1].encode(n)
+        res[(world, "after")] = bands[-1].output(0)
+        for b in bands:
+            b.close()
+        full.close()
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        band = mijpeg.Batch(W, H, n)
+        band.upload(frames)
+        full = mijpeg.Batch(W, H, n, assembler=True)
+        xch = sharding.DeviceExchange(dist, dev)
+        outs = []
+        for _ in range(2):
+            ev = []
+            sharding.encode_banded_dev(band, n, xch, full, events=ev)
+            full.sync()
+            outs.append([full.output(f) for f in range(n)])
+        res["nccl"] = outs
+        res["phases"] = [name for name, _ in ev]
+        band.close()
+        full.close()
+    finally:
+        dist.destroy_process_group()
+    q.put(res)
+
+
+def test_device_resident_band_protocol():
+    """mij_band_*_async for 1-4 bands in one process and encode_banded_dev
+    over a one-rank nccl group: the reference's bytes for whole frames
+    (/root/reference/main/encoder.c through the oracle), with every exchanged
+    value kept in device memory."""
+    import multiprocessing as mp
+    import oracle as O
+    import recipes
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_dev_bands, args=(_free_port(), q))
+    p.start()
+    res = q.get(timeout=600)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    frames = [recipes.config3_frame(5, 320, 480), recipes.noise(320, 480, 9), recipes.config3_frame(6, 320, 480)]
+    want = [O.cref_encode(f) for f in frames]
+    for world in (1, 2, 3, 4):
+        assert res[world] == want, f"{world} bands"
+        # a band batch left by the protocol encodes its own rows correctly
+        r0, rows = sharding.band_rows(320, world, world - 1)
+        assert res[(world, "after")] == O.cref_encode(np.ascontiguousarray(frames[0][r0:r0 + rows]))
+    assert res["nccl"] == [want, want]
+    assert res["phases"] == ["start", "analyze", "histograms", "tables", "pack", "words", "assemble"]
