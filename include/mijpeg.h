@@ -284,23 +284,33 @@ mij_batch *mij_assembler_create(int device, int width, int height, int max_frame
  * and every call only enqueues work on the batch's stream (mij_batch_stream)
  * -- nothing waits for the host, so the caller's collectives (RCCL on that
  * same stream) run between the calls.  Shapes: last/prev int16 [n][4]
- * (component c at [f][c]), hist uint32 [n][4][257], bits uint64 [n][3],
- * allbits uint64 [world][n][3] (the bands' bits in rank order).
- *   band_pack_async     this band's bit offsets from allbits, packs, and
- *                       writes its total word count to *d_nwords;
- *   band_words_async    moves those words, (frame, scan) order, to d_dst
- *                       (sized by the caller from *d_nwords);
- *   assemble_async      (root) tables from the summed histograms, every
- *                       band's words OR-ed into the scans from d_src (band
- *                       r's words at row r, stride_words apart) and the JFIF
- *                       assembly; read the frames with mij_batch_output. */
+ * (component c at [f][c]), hist uint32 [n][4][257],
+ * bits uint64 [3n + 1] (a band's bits per (frame, scan), then its word
+ * count), allbits uint64 [world][3n + 1] (every band's bits, rank order).
+ *   band_analyze_async     K1 over the band; its last raw DCs -> d_last
+ *   band_histograms_async  the segments' first DC tokens from the previous
+ *                          band's last DCs (zeros for band 0); the band's
+ *                          histograms -> d_hist (sum them over the bands)
+ *   band_pack_async        tables from the summed histograms, every scan of
+ *                          the band packed from bit 0 -> d_bits
+ *   band_words_async       moves those words, (frame, scan) order, to d_dst
+ *                          (sized by the caller from the word count)
+ *   assemble_tables_async  (root) the tables from the summed histograms (may
+ *                          run while the bands pack)
+ *   assemble_async         (root) every band's words shifted to its bit
+ *                          position (the sum of the earlier bands' bits) and
+ *                          OR-ed into the scans from d_src (band r's words at
+ *                          row r, stride_words apart), then the JFIF
+ *                          assembly; read the frames with mij_batch_output.
+ * Replaces the host protocol's mij_band_analyze / _histograms / _tables /
+ * _pack / _words_all and mij_assemble_begin / _pieces / _end. */
 int mij_band_analyze_async(mij_batch *b, int n, int16_t *d_last);
 int mij_band_histograms_async(mij_batch *b, int n, const int16_t *d_prev, uint32_t *d_hist);
-int mij_band_tables_async(mij_batch *b, int n, const uint32_t *d_ghist, uint64_t *d_bits);
-int mij_band_pack_async(mij_batch *b, int n, const uint64_t *d_allbits, int world, int rank, uint64_t *d_nwords);
+int mij_band_pack_async(mij_batch *b, int n, const uint32_t *d_ghist, uint64_t *d_bits);
 int mij_band_words_async(mij_batch *b, int n, uint32_t *d_dst);
-int mij_assemble_async(mij_batch *b, int n, const uint32_t *d_ghist, const uint64_t *d_allbits, int world,
-                       const uint32_t *d_src, size_t stride_words);
+int mij_assemble_tables_async(mij_batch *b, int n, const uint32_t *d_ghist);
+int mij_assemble_async(mij_batch *b, int n, const uint64_t *d_allbits, int world, const uint32_t *d_src,
+                       size_t stride_words);
 
 /* ---- diagnostics used by the test-suite -----------------------------------*/
 /* 16x16x64 i8 MFMA layout probe: A, B are 64 lanes x 16 int8, D 64 x 4 int32 */

@@ -40,8 +40,10 @@ hipError_t launch_gather_regions(uint8_t *dst, long long slot_bytes, int pitch, 
                                  hipStream_t s);
 hipError_t launch_mfma_probe(const int4 *A, const int4 *B, int4 *D, hipStream_t s);
 hipError_t launch_band_last(const int16_t *dc, const Geom &g, int n, int16_t *last, hipStream_t s);
-hipError_t launch_band_place(const unsigned long long *allbits, int world, int rank, int n, uint32_t *bit_base,
-                             unsigned long long *pieces, unsigned long long *nwords, hipStream_t s);
+hipError_t launch_band_count(const unsigned long long *scan_bits, int n, unsigned long long *pieces,
+                             unsigned long long *bits, hipStream_t s);
+hipError_t launch_or_shift_pieces(uint32_t *raw, const Geom &g, const uint32_t *src,
+                                  const unsigned long long *d_pieces, int npieces, long long max_words, hipStream_t s);
 hipError_t launch_band_assembly(const unsigned long long *allbits, int world, int n, unsigned long long stride,
                                 unsigned long long *pieces, unsigned long long *scan_bits, int *over, hipStream_t s);
 }  // namespace mij
@@ -280,6 +282,7 @@ struct mij_batch {
   bool assembler = false;
   std::vector<unsigned long long> band_words;  // per frame x 3: packed words after mij_band_pack
   int band_async_n = 0;                        // frames of the last mij_band_pack_async
+  int asm_tables_n = 0;                        // frames of the last mij_assemble_tables_async
   // region batches (mij_batch_set_frame_dims / _gather_regions): per-frame
   // image size inside the canvas slots; d_frame stages a host frame
   int2 *d_fdims = nullptr;
@@ -1420,31 +1423,22 @@ extern "C" int mij_band_histograms_async(mij_batch *b, int n, const int16_t *d_p
   return MIJ_OK;
 }
 
-extern "C" int mij_band_tables_async(mij_batch *b, int n, const uint32_t *d_ghist, uint64_t *d_bits) {
-  if (band_check(b, n, "band_tables_async")) return g_err;
-  if (!d_ghist || !d_bits) return fail(MIJ_EINVAL, "band_tables_async: null argument");
+extern "C" int mij_band_pack_async(mij_batch *b, int n, const uint32_t *d_ghist, uint64_t *d_bits) {
+  if (band_check(b, n, "band_pack_async")) return g_err;
+  if (!d_ghist || !d_bits) return fail(MIJ_EINVAL, "band_pack_async: null argument");
+  if (ensure_pieces(b, (size_t)n * 3)) return g_err;
+  // the tables from the summed histograms, then every scan of the band packed
+  // from bit 0 (the root shifts it to its place): no band waits for the bit
+  // counts of the bands before it
   HIP_TRY(hipMemcpyAsync(b->d_hist, d_ghist, sizeof(uint32_t) * n * 4 * 257, hipMemcpyDeviceToDevice, b->stream));
   EntArgs a = ent_args(b, n, 0, true);
   HIP_TRY(launch_tables(a, b->stream));
   HIP_TRY(hipMemsetAsync(b->d_bitbase, 0, sizeof(uint32_t) * n * 4, b->stream));
-  HIP_TRY(launch_bits(a, b->stream));
-  HIP_TRY(launch_scan(a, b->stream));
-  HIP_TRY(hipMemcpyAsync(d_bits, b->d_scan_bits, sizeof(uint64_t) * n * 3, hipMemcpyDeviceToDevice, b->stream));
-  return MIJ_OK;
-}
-
-extern "C" int mij_band_pack_async(mij_batch *b, int n, const uint64_t *d_allbits, int world, int rank,
-                                   uint64_t *d_nwords) {
-  if (band_check(b, n, "band_pack_async")) return g_err;
-  if (!d_allbits || !d_nwords || world < 1 || rank < 0 || rank >= world)
-    return fail(MIJ_EINVAL, "band_pack_async: bad arguments");
-  if (ensure_pieces(b, (size_t)n * 3)) return g_err;
-  HIP_TRY(launch_band_place((const unsigned long long *)d_allbits, world, rank, n, b->d_bitbase, b->d_pieces,
-                            (unsigned long long *)d_nwords, b->stream));
-  EntArgs a = ent_args(b, n, 0, true);
   if (b->raw_dirty) HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->raw_dirty * b->g.raw_fs, b->stream));
   b->raw_dirty = n;
   HIP_TRY(launch_pack_lb(a, b->stream));
+  HIP_TRY(launch_band_count((const unsigned long long *)b->d_scan_bits, n, b->d_pieces,
+                            (unsigned long long *)d_bits, b->stream));
   b->band_async_n = n;
   return MIJ_OK;
 }
@@ -1460,22 +1454,35 @@ extern "C" int mij_band_words_async(mij_batch *b, int n, uint32_t *d_dst) {
   return MIJ_OK;
 }
 
-extern "C" int mij_assemble_async(mij_batch *b, int n, const uint32_t *d_ghist, const uint64_t *d_allbits, int world,
-                                  const uint32_t *d_src, size_t stride_words) {
-  if (band_check(b, n, "assemble_async", true)) return g_err;
-  if (!d_ghist || !d_allbits || !d_src || world < 1) return fail(MIJ_EINVAL, "assemble_async: bad arguments");
-  if (ensure_pieces(b, (size_t)world * n * 3)) return g_err;
-  HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * n * b->g.raw_fs, b->stream));
-  b->raw_dirty = std::max(b->raw_dirty, n);
+extern "C" int mij_assemble_tables_async(mij_batch *b, int n, const uint32_t *d_ghist) {
+  if (band_check(b, n, "assemble_tables_async", true)) return g_err;
+  if (!d_ghist) return fail(MIJ_EINVAL, "assemble_tables_async: null d_ghist");
   HIP_TRY(hipMemcpyAsync(b->d_hist, d_ghist, sizeof(uint32_t) * n * 4 * 257, hipMemcpyDeviceToDevice, b->stream));
   HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * n, b->stream));
   EntArgs a = ent_args(b, n);
   HIP_TRY(launch_tables(a, b->stream));
+  b->asm_tables_n = n;
+  return MIJ_OK;
+}
+
+extern "C" int mij_assemble_async(mij_batch *b, int n, const uint64_t *d_allbits, int world, const uint32_t *d_src,
+                                  size_t stride_words) {
+  if (band_check(b, n, "assemble_async", true)) return g_err;
+  if (!d_allbits || !d_src || world < 1) return fail(MIJ_EINVAL, "assemble_async: bad arguments");
+  if (n != b->asm_tables_n) return fail(MIJ_EINVAL, "assemble_async: needs mij_assemble_tables_async of the same frames first");
+  if (ensure_pieces(b, (size_t)world * n * 3)) return g_err;
+  // the pieces' boundary words are OR-ed: the scans must start zeroed (a
+  // finished assembly leaves them so: k_emit_write zeroes what it reads)
+  if (b->raw_dirty) HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->raw_dirty * b->g.raw_fs, b->stream));
+  b->raw_dirty = std::max(b->raw_dirty, n);
+  EntArgs a = ent_args(b, n);
   HIP_TRY(launch_band_assembly((const unsigned long long *)d_allbits, world, n, stride_words, b->d_pieces,
                                (unsigned long long *)b->d_scan_bits, b->d_err, b->stream));
-  HIP_TRY(launch_or_pieces(b->d_raw, b->g, d_src, b->d_pieces, world * n * 3, (long long)stride_words, b->stream));
+  HIP_TRY(launch_or_shift_pieces(b->d_raw, b->g, d_src, b->d_pieces, world * n * 3, (long long)stride_words,
+                                 b->stream));
   HIP_TRY(launch_emit(a, b->stream));  // k_emit_write zeroes the words it reads
   if (n >= b->raw_dirty) b->raw_dirty = 0;
+  b->asm_tables_n = 0;
   b->last_frames = n;
   return MIJ_OK;
 }

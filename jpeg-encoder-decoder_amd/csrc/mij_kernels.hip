@@ -2853,55 +2853,75 @@ __global__ void k_band_last(const int16_t *dc, Geom g, int n, int16_t *last) {
   last[f * 4 + 3] = 0;
 }
 
-// this band's place in every scan from the gathered bit counts allbits[world][n][3]:
-// its start bit (the exclusive sum over the bands before it) in-word offset
-// -> bit_base[f * 4 + c], its word count, and the (frame, scan)-ordered move
-// table {frame * 3 + scan, words, first destination word} -> pieces; the
-// band's total words -> nwords[0]
-__global__ void k_band_place(const unsigned long long *allbits, int world, int rank, int n, uint32_t *bit_base,
-                             unsigned long long *pieces, unsigned long long *nwords) {
+// a band packed from bit 0 of every scan: its bits per scan (the pack's scan
+// totals) -> bits[f * 3 + c], its word count -> bits[3n], and the (frame,
+// scan)-ordered move table {frame * 3 + scan, words, first destination word}
+// -> pieces
+__global__ void k_band_count(const unsigned long long *scan_bits, int n, unsigned long long *pieces,
+                             unsigned long long *bits) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   unsigned long long at = 0;
-  for (int f = 0; f < n; f++)
-    for (int c = 0; c < 3; c++) {
-      unsigned long long off = 0;
-      for (int r = 0; r < rank; r++) off += allbits[((long long)r * n + f) * 3 + c];
-      const unsigned long long bits = allbits[((long long)rank * n + f) * 3 + c];
-      const unsigned long long nw = ((off & 31) + bits + 31) >> 5;
-      bit_base[f * 4 + c] = (uint32_t)(off & 31);
-      unsigned long long *pc = pieces + 3 * (f * 3 + c);
-      pc[0] = (unsigned long long)(f * 3 + c);
-      pc[1] = nw;
-      pc[2] = at;
-      at += nw;
-    }
-  nwords[0] = at;
+  for (int i = 0; i < 3 * n; i++) {
+    const unsigned long long b = scan_bits[i], nw = (b + 31) >> 5;
+    bits[i] = b;
+    unsigned long long *pc = pieces + 3 * i;
+    pc[0] = (unsigned long long)i;
+    pc[1] = nw;
+    pc[2] = at;
+    at += nw;
+  }
+  bits[3 * n] = at;
 }
 
-// the root's assembly table from allbits[world][n][3] for a gathered buffer
-// whose band-r row (stride words) holds that band's words in (frame, scan)
-// order: piece (r, f, c) = {frame * 3 + scan, first word in the scan, first
-// source word, words}; the scans' total bits -> scan_bits[f * 3 + c]
+// the root's assembly table from allbits[world][3n + 1] (k_band_count's
+// output of every band) for a gathered buffer whose band-r row (stride words)
+// holds that band's words in (frame, scan) order: piece (r, f, c) = {frame * 3
+// + scan, first bit in the scan (the sum of the earlier bands' bits, encoder.c
+// :462-502's running bit position), first source word, bits}; the scans'
+// total bits -> scan_bits[f * 3 + c]
 __global__ void k_band_assembly(const unsigned long long *allbits, int world, int n, unsigned long long stride,
                                 unsigned long long *pieces, unsigned long long *scan_bits, int *over) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  for (int f = 0; f < n; f++)
-    for (int c = 0; c < 3; c++) scan_bits[f * 3 + c] = 0;
+  for (int i = 0; i < 3 * n; i++) scan_bits[i] = 0;
   for (int r = 0; r < world; r++) {
+    const unsigned long long *rb = allbits + (long long)r * (3 * n + 1);
     unsigned long long at = 0;
-    for (int f = 0; f < n; f++)
-      for (int c = 0; c < 3; c++) {
-        const unsigned long long off = scan_bits[f * 3 + c], bits = allbits[((long long)r * n + f) * 3 + c];
-        const unsigned long long nw = ((off & 31) + bits + 31) >> 5;
-        unsigned long long *pc = pieces + 4 * (((long long)r * n + f) * 3 + c);
-        pc[0] = (unsigned long long)(f * 3 + c);
-        pc[1] = off >> 5;
-        pc[2] = (unsigned long long)r * stride + at;
-        pc[3] = nw;
-        at += nw;
-        scan_bits[f * 3 + c] = off + bits;
-      }
+    for (int i = 0; i < 3 * n; i++) {
+      const unsigned long long off = scan_bits[i], bits = rb[i];
+      unsigned long long *pc = pieces + 4 * ((long long)r * 3 * n + i);
+      pc[0] = (unsigned long long)i;
+      pc[1] = off;
+      pc[2] = (unsigned long long)r * stride + at;
+      pc[3] = bits;
+      at += (bits + 31) >> 5;
+      scan_bits[i] = off + bits;
+    }
     if (at > stride) *over = 1;  // a band's words beyond its row: assemble nothing wrong
+  }
+}
+
+// Every band's words OR-ed into the scans at their bit positions (one launch,
+// piece blockIdx.y = {frame * 3 + scan, first bit in the scan, first source
+// word, bits}): a band packed from bit 0 lands shifted right by its start
+// bit's in-word offset (big-endian bit order), so scan word j of the piece
+// takes the low bits of source word j - 1 and the high bits of word j.
+// Neighbouring bands share at most their boundary word and run concurrently:
+// a piece's first and last scan words are OR-ed atomically.
+__global__ void k_or_shift_pieces(uint32_t *raw, long long raw_fs, long long rw0, long long rw1,
+                                  const uint32_t *src, const unsigned long long *pieces) {
+  const unsigned long long *pc = pieces + 4 * (long long)blockIdx.y;
+  const long long fc = (long long)pc[0], bits = (long long)pc[3];
+  if (!bits) return;
+  const long long f = fc / 3, c = fc - 3 * f;
+  const int sh = (int)(pc[1] & 31);
+  const long long nsrc = (bits + 31) >> 5, ndst = (sh + bits + 31) >> 5;
+  uint32_t *dst = raw + f * raw_fs + (c == 0 ? 0 : rw0 + (c == 2 ? rw1 : 0)) + (long long)(pc[1] >> 5);
+  const uint32_t *sp = src + (long long)pc[2];
+  for (long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x; j < ndst; j += (long long)gridDim.x * blockDim.x) {
+    uint32_t v = j < nsrc ? sp[j] >> sh : 0u;
+    if (sh && j > 0) v |= sp[j - 1] << (32 - sh);
+    if (j == 0 || j == ndst - 1) atomicOr(&dst[j], v);
+    else dst[j] = v;
   }
 }
 
@@ -3056,14 +3076,22 @@ hipError_t launch_band_last(const int16_t *dc, const Geom &g, int n, int16_t *la
   hipLaunchKernelGGL(k_band_last, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, dc, g, n, last);
   return hipGetLastError();
 }
-hipError_t launch_band_place(const unsigned long long *allbits, int world, int rank, int n, uint32_t *bit_base,
-                             unsigned long long *pieces, unsigned long long *nwords, hipStream_t s) {
-  hipLaunchKernelGGL(k_band_place, dim3(1), dim3(64), 0, s, allbits, world, rank, n, bit_base, pieces, nwords);
+hipError_t launch_band_count(const unsigned long long *scan_bits, int n, unsigned long long *pieces,
+                             unsigned long long *bits, hipStream_t s) {
+  hipLaunchKernelGGL(k_band_count, dim3(1), dim3(64), 0, s, scan_bits, n, pieces, bits);
   return hipGetLastError();
 }
 hipError_t launch_band_assembly(const unsigned long long *allbits, int world, int n, unsigned long long stride,
                                 unsigned long long *pieces, unsigned long long *scan_bits, int *over, hipStream_t s) {
   hipLaunchKernelGGL(k_band_assembly, dim3(1), dim3(64), 0, s, allbits, world, n, stride, pieces, scan_bits, over);
+  return hipGetLastError();
+}
+hipError_t launch_or_shift_pieces(uint32_t *raw, const Geom &g, const uint32_t *src,
+                                  const unsigned long long *d_pieces, int npieces, long long max_words, hipStream_t s) {
+  if (npieces <= 0 || max_words <= 0) return hipSuccess;
+  const long long chunks = (max_words + 1 + 1023) / 1024;
+  hipLaunchKernelGGL(k_or_shift_pieces, dim3((unsigned)(chunks < 64 ? chunks : 64), (unsigned)npieces), dim3(256), 0,
+                     s, raw, g.raw_fs, g.raw_words[0], g.raw_words[1], src, d_pieces);
   return hipGetLastError();
 }
 

@@ -28,8 +28,8 @@ EXPORTS = [
     "mij_band_analyze", "mij_band_histograms", "mij_band_tables", "mij_band_pack", "mij_band_words",
     "mij_assemble_begin", "mij_assemble_words", "mij_assemble_end",
     "mij_band_words_all", "mij_assemble_pieces", "mij_assembler_create",
-    "mij_band_analyze_async", "mij_band_histograms_async", "mij_band_tables_async", "mij_band_pack_async",
-    "mij_band_words_async", "mij_assemble_async",
+    "mij_band_analyze_async", "mij_band_histograms_async", "mij_band_pack_async",
+    "mij_band_words_async", "mij_assemble_tables_async", "mij_assemble_async",
     "mij_probe_mfma", "mij_colour_lut", "mij_build_target",
     # change detector (reference include/brain.h:7-10 drop-in + extensions)
     "subsample", "store", "compare", "enlargeAdjust", "mij_set_frame_height",
@@ -110,10 +110,10 @@ def load() -> C.CDLL:
     lib.mij_batch_audit.argtypes = [p, i, p]
     lib.mij_band_analyze_async.argtypes = [p, i, p]
     lib.mij_band_histograms_async.argtypes = [p, i, p, p]
-    lib.mij_band_tables_async.argtypes = [p, i, p, p]
-    lib.mij_band_pack_async.argtypes = [p, i, p, i, i, p]
+    lib.mij_band_pack_async.argtypes = [p, i, p, p]
     lib.mij_band_words_async.argtypes = [p, i, p]
-    lib.mij_assemble_async.argtypes = [p, i, p, p, i, p, sz]
+    lib.mij_assemble_tables_async.argtypes = [p, i, p]
+    lib.mij_assemble_async.argtypes = [p, i, p, i, p, sz]
     lib.mij_batch_build_tables.argtypes = [p, i, p]
     lib.mij_batch_sync.argtypes = [p]
     lib.mij_batch_output.argtypes = [p, i, p, sz, C.POINTER(sz)]
@@ -524,18 +524,19 @@ class Batch:
     def band_histograms_async(self, n: int, d_prev: int, d_hist: int) -> None:
         _check(self.lib.mij_band_histograms_async(self.h_, n, d_prev, d_hist), "band_histograms_async")
 
-    def band_tables_async(self, n: int, d_ghist: int, d_bits: int) -> None:
-        _check(self.lib.mij_band_tables_async(self.h_, n, d_ghist, d_bits), "band_tables_async")
-
-    def band_pack_async(self, n: int, d_allbits: int, world: int, rank: int, d_nwords: int) -> None:
-        _check(self.lib.mij_band_pack_async(self.h_, n, d_allbits, world, rank, d_nwords), "band_pack_async")
+    def band_pack_async(self, n: int, d_ghist: int, d_bits: int) -> None:
+        """tables from the summed histograms, the band packed from bit 0;
+        d_bits: uint64 [3n + 1] device buffer (bits per scan, word count)"""
+        _check(self.lib.mij_band_pack_async(self.h_, n, d_ghist, d_bits), "band_pack_async")
 
     def band_words_async(self, n: int, d_dst: int) -> None:
         _check(self.lib.mij_band_words_async(self.h_, n, d_dst), "band_words_async")
 
-    def assemble_async(self, n: int, d_ghist: int, d_allbits: int, world: int, d_src: int, stride_words: int) -> None:
-        _check(self.lib.mij_assemble_async(self.h_, n, d_ghist, d_allbits, world, d_src, stride_words),
-               "assemble_async")
+    def assemble_tables_async(self, n: int, d_ghist: int) -> None:
+        _check(self.lib.mij_assemble_tables_async(self.h_, n, d_ghist), "assemble_tables_async")
+
+    def assemble_async(self, n: int, d_allbits: int, world: int, d_src: int, stride_words: int) -> None:
+        _check(self.lib.mij_assemble_async(self.h_, n, d_allbits, world, d_src, stride_words), "assemble_async")
 
     def assemble_begin(self, n: int, hist: np.ndarray) -> None:
         h = np.ascontiguousarray(hist, np.uint32).reshape(n, 4, 257)

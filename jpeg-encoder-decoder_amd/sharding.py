@@ -256,14 +256,17 @@ def encode_banded_dev(band, n: int, xch, frame_batch=None, events=None):
     [n, 4], gathered as int32 pairs), the histograms (summed in place), the
     bit counts (gathered) and the packed words (gathered to the root) never
     leave HBM; the library calls and the collectives all run on the band
-    batch's stream.  The root's frame_batch (an assembler) waits for that
-    stream and assembles on its own.  `events`: optional list that receives
-    (name, torch.cuda.Event) pairs recorded on the band stream after each
-    phase.  Returns nothing; read the frames from frame_batch.output()."""
+    batch's stream.  Every band packs from bit 0, so the bands pack at once;
+    the root shifts each band's words to its bit position while assembling.
+    The root's frame_batch (an assembler) builds its tables on its own stream
+    while the bands pack, then assembles.  `events`: optional list that
+    receives (name, torch.cuda.Event) pairs recorded on the band stream after
+    each phase.  Returns nothing; read the frames from frame_batch.output()."""
     torch = xch.torch
     rank, world = xch.rank, xch.world
     dev = xch.device
     s = torch.cuda.ExternalStream(band.stream_ptr(), device=dev)
+    a = torch.cuda.ExternalStream(frame_batch.stream_ptr(), device=dev) if rank == 0 else None
 
     def mark(name):
         if events is not None:
@@ -283,25 +286,24 @@ def encode_banded_dev(band, n: int, xch, frame_batch=None, events=None):
         band.band_histograms_async(n, prev.data_ptr(), hist.data_ptr())
         xch.all_reduce_sum(hist)
         mark("histograms")
-        bits = torch.empty((n, 3), dtype=torch.int64, device=dev)
-        band.band_tables_async(n, hist.data_ptr(), bits.data_ptr())
-        allbits = xch.all_gather(bits).contiguous()               # [world, n, 3]
-        mark("tables")
-        nw = torch.empty(1, dtype=torch.int64, device=dev)
-        band.band_pack_async(n, allbits.data_ptr(), world, rank, nw.data_ptr())
-        stride = int(xch.all_gather(nw).max().item())             # the one host read of a step
+        if a is not None:
+            a.wait_stream(s)
+            with torch.cuda.stream(a):
+                frame_batch.assemble_tables_async(n, hist.data_ptr())
+        bits = torch.empty(3 * n + 1, dtype=torch.int64, device=dev)
+        band.band_pack_async(n, hist.data_ptr(), bits.data_ptr())
+        allbits = xch.all_gather(bits).contiguous()               # [world, 3n + 1]
         mark("pack")
+        stride = int(allbits[:, 3 * n].max().item())              # the one host read of a step
         buf = torch.empty(max(stride, 1), dtype=torch.int32, device=dev)
         band.band_words_async(n, buf.data_ptr())
         gathered = xch.gather(buf)
         mark("words")
-        if rank != 0:
+        if a is None:
             return
-    a = torch.cuda.ExternalStream(frame_batch.stream_ptr(), device=dev)
     a.wait_stream(s)
     with torch.cuda.stream(a):
-        frame_batch.assemble_async(n, hist.data_ptr(), allbits.data_ptr(), world, gathered.data_ptr(),
-                                   gathered.shape[1])
+        frame_batch.assemble_async(n, allbits.data_ptr(), world, gathered.data_ptr(), gathered.shape[1])
     # the tensors read by the assembly are freed on the band stream: keep that
     # stream behind the assembly
     s.wait_stream(a)

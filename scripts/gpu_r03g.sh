@@ -14,3 +14,7 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -2 gpurun_out/t_bands.log
 timeout -k 10 200 python3 bench.py --workload config4 --steps 20 --warmup 3 > gpurun_out/c4.log 2>&1 || { tail -20 gpurun_out/c4.log; exit 1; }
 tail -1 gpurun_out/c4.log
+if [ -n "$C4PROF" ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c4prof -o c4 -- python3 bench.py --workload config4 --steps 10 --warmup 2 > gpurun_out/c4prof.log 2>&1 || { tail -20 gpurun_out/c4prof.log; exit 1; }
+  f=$(find gpurun_out/c4prof -name "c4_kernel_stats.csv" | head -1); [ -n "$f" ] && cut -d, -f1-4 "$f" | head -20; python3 scripts/trace_gaps.py "${f%_kernel_stats.csv}_kernel_trace.csv" 30
+fi

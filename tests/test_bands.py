@@ -295,24 +295,20 @@ def _dev_bands(port, q):
             b.sync()
         ghist = torch.stack(hist).sum(0, dtype=torch.int32).contiguous()
         torch.cuda.synchronize()
-        bits = [torch.empty((n, 3), dtype=torch.int64, device=dev) for _ in bands]
+        full = mijpeg.Batch(W, H, n, assembler=True)
+        full.assemble_tables_async(n, ghist.data_ptr())
+        bits = [torch.empty(3 * n + 1, dtype=torch.int64, device=dev) for _ in bands]
         for b, t in zip(bands, bits):
-            b.band_tables_async(n, ghist.data_ptr(), t.data_ptr())
+            b.band_pack_async(n, ghist.data_ptr(), t.data_ptr())
             b.sync()
         allbits = torch.stack(bits).contiguous()
-        torch.cuda.synchronize()
-        nw = [torch.empty(1, dtype=torch.int64, device=dev) for _ in bands]
-        for r, b in enumerate(bands):
-            b.band_pack_async(n, allbits.data_ptr(), world, r, nw[r].data_ptr())
-            b.sync()
-        stride = max(int(x.item()) for x in nw)
+        stride = int(allbits[:, 3 * n].max())
         gathered = torch.zeros((world, stride), dtype=torch.int32, device=dev)
         torch.cuda.synchronize()
         for r, b in enumerate(bands):
             b.band_words_async(n, gathered[r].data_ptr())
             b.sync()
-        full = mijpeg.Batch(W, H, n, assembler=True)
-        full.assemble_async(n, ghist.data_ptr(), allbits.data_ptr(), world, gathered.data_ptr(), stride)
+        full.assemble_async(n, allbits.data_ptr(), world, gathered.data_ptr(), stride)
         full.sync()
         res[world] = [full.output(f) for f in range(n)]
         # the band batches encode whole frames correctly afterwards
@@ -365,4 +361,4 @@ def test_device_resident_band_protocol():
         r0, rows = sharding.band_rows(320, world, world - 1)
         assert res[(world, "after")] == O.cref_encode(np.ascontiguousarray(frames[0][r0:r0 + rows]))
     assert res["nccl"] == [want, want]
-    assert res["phases"] == ["start", "analyze", "histograms", "tables", "pack", "words", "assemble"]
+    assert res["phases"] == ["start", "analyze", "histograms", "pack", "words", "assemble"]
