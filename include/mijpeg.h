@@ -289,12 +289,18 @@ mij_batch *mij_assembler_create(int device, int width, int height, int max_frame
  * count), allbits uint64 [world][3n + 1] (every band's bits, rank order).
  *   band_analyze_async     K1 over the band; its last raw DCs -> d_last
  *   band_histograms_async  the segments' first DC tokens from the previous
- *                          band's last DCs (zeros for band 0); the band's
- *                          histograms -> d_hist (sum them over the bands)
- *   band_pack_async        tables from the summed histograms, every scan of
- *                          the band packed from bit 0 -> d_bits
+ *                          band's last DCs (d_prev; null for band 0: zeros);
+ *                          the band's histograms -> d_hist (sum them over
+ *                          the bands)
+ *   band_tables_async      tables from the summed histograms; an upper bound
+ *                          of the band's words (its histograms weighted by
+ *                          the code lengths, +3 per frame) -> *d_bound, so
+ *                          the caller can size the word exchange while the
+ *                          band packs
+ *   band_pack_async        every scan of the band packed from bit 0 -> d_bits
  *   band_words_async       moves those words, (frame, scan) order, to d_dst
- *                          (sized by the caller from the word count)
+ *                          (cap_words long; words beyond it are dropped and
+ *                          the root's assembly fails those frames)
  *   assemble_tables_async  (root) the tables from the summed histograms (may
  *                          run while the bands pack)
  *   assemble_async         (root) every band's words shifted to its bit
@@ -306,8 +312,9 @@ mij_batch *mij_assembler_create(int device, int width, int height, int max_frame
  * _pack / _words_all and mij_assemble_begin / _pieces / _end. */
 int mij_band_analyze_async(mij_batch *b, int n, int16_t *d_last);
 int mij_band_histograms_async(mij_batch *b, int n, const int16_t *d_prev, uint32_t *d_hist);
-int mij_band_pack_async(mij_batch *b, int n, const uint32_t *d_ghist, uint64_t *d_bits);
-int mij_band_words_async(mij_batch *b, int n, uint32_t *d_dst);
+int mij_band_tables_async(mij_batch *b, int n, const uint32_t *d_ghist, uint64_t *d_bound);
+int mij_band_pack_async(mij_batch *b, int n, uint64_t *d_bits);
+int mij_band_words_async(mij_batch *b, int n, uint32_t *d_dst, size_t cap_words);
 int mij_assemble_tables_async(mij_batch *b, int n, const uint32_t *d_ghist);
 int mij_assemble_async(mij_batch *b, int n, const uint64_t *d_allbits, int world, const uint32_t *d_src,
                        size_t stride_words);

@@ -32,7 +32,8 @@ hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s);
 hipError_t launch_emit(const EntArgs &a, hipStream_t s);
 hipError_t launch_or_words(uint32_t *dst, const uint32_t *src, long long n, hipStream_t s);
 hipError_t launch_move_pieces(uint32_t *raw, const Geom &g, uint32_t *dst,
-                              const unsigned long long *d_pieces, int npieces, long long max_words, hipStream_t s);
+                              const unsigned long long *d_pieces, int npieces, long long max_words, long long cap,
+                              hipStream_t s);
 hipError_t launch_or_pieces(uint32_t *raw, const Geom &g, const uint32_t *src,
                             const unsigned long long *d_pieces, int npieces, long long max_words, hipStream_t s);
 hipError_t launch_gather_regions(uint8_t *dst, long long slot_bytes, int pitch, const uint8_t *src,
@@ -40,6 +41,8 @@ hipError_t launch_gather_regions(uint8_t *dst, long long slot_bytes, int pitch, 
                                  hipStream_t s);
 hipError_t launch_mfma_probe(const int4 *A, const int4 *B, int4 *D, hipStream_t s);
 hipError_t launch_band_last(const int16_t *dc, const Geom &g, int n, int16_t *last, hipStream_t s);
+hipError_t launch_band_bound(const uint32_t *hist, const uint32_t *ehuf, int n, unsigned long long *acc,
+                             unsigned long long *bound, hipStream_t s);
 hipError_t launch_band_count(const unsigned long long *scan_bits, int n, unsigned long long *pieces,
                              unsigned long long *bits, hipStream_t s);
 hipError_t launch_or_shift_pieces(uint32_t *raw, const Geom &g, const uint32_t *src,
@@ -283,6 +286,7 @@ struct mij_batch {
   std::vector<unsigned long long> band_words;  // per frame x 3: packed words after mij_band_pack
   int band_async_n = 0;                        // frames of the last mij_band_pack_async
   int asm_tables_n = 0;                        // frames of the last mij_assemble_tables_async
+  unsigned long long *d_bound_acc = nullptr;   // k_band_bound: {sum, arrivals}, left zeroed by its last workgroup
   // region batches (mij_batch_set_frame_dims / _gather_regions): per-frame
   // image size inside the canvas slots; d_frame stages a host frame
   int2 *d_fdims = nullptr;
@@ -325,7 +329,8 @@ static void batch_free(mij_batch *b) {
                   b->d_ehuf, b->d_raw, b->d_tok, b->d_tok0, b->d_seg_ntok, b->d_seg_bits, b->d_seg_off,
                   b->d_scan_bits, b->d_out_len, b->d_hc, b->d_out, b->d_err, b->d_replays,
                   b->d_dcpred, b->d_bitbase, b->d_stage, b->d_fixmask, b->d_audit, b->d_ffc, b->d_choff,
-                  b->d_pack_state, b->d_pack_ticket, b->d_fdims, b->d_frame, b->d_regions, b->d_pieces};
+                  b->d_pack_state, b->d_pack_ticket, b->d_fdims, b->d_frame, b->d_regions, b->d_pieces,
+                  b->d_bound_acc};
   for (void *p : ptrs)
     if (p) hipFree(p);
   for (auto &row : b->evh)
@@ -544,7 +549,13 @@ static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0, bool band = false
   // 16 on large low-Q batches (emit 0.247 -> 0.232 ms at config 3, Q=50),
   // 64 otherwise (Q=90: 0.62 at 64 against 0.68 at 16; a single frame needs
   // the width)
-  a.emit_slots = (nframes >= 43 && b->quality <= 60) ? 16 : 64;
+  // 256 on frames of 8 Mpixels and more (config 4: few scans of hundreds of
+  // chunks each)
+  static const int slots_env = getenv("MIJ_EMIT_SLOTS") ? atoi(getenv("MIJ_EMIT_SLOTS")) : 0;  // A/B
+  a.emit_slots = slots_env > 0                           ? slots_env
+                 : (nframes >= 43 && b->quality <= 60)   ? 16
+                 : ((long long)b->g.w * b->g.h >= (8 << 20)) ? 256
+                                                           : 64;
   if (f0) {  // sub-batch: frames f0.. of the batch (every per-frame array shifted)
     const Geom &g = b->g;
     const long long F = f0, gpf = (g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((g.nsc + PACK_SEGS - 1) / PACK_SEGS);
@@ -1415,27 +1426,43 @@ extern "C" int mij_band_analyze_async(mij_batch *b, int n, int16_t *d_last) {
 
 extern "C" int mij_band_histograms_async(mij_batch *b, int n, const int16_t *d_prev, uint32_t *d_hist) {
   if (band_check(b, n, "band_histograms_async")) return g_err;
-  if (!d_prev || !d_hist) return fail(MIJ_EINVAL, "band_histograms_async: null argument");
-  HIP_TRY(hipMemcpyAsync(b->d_dcpred, d_prev, sizeof(int16_t) * n * 4, hipMemcpyDeviceToDevice, b->stream));
-  EntArgs a = ent_args(b, n, 0, true);
+  if (!d_hist) return fail(MIJ_EINVAL, "band_histograms_async: null d_hist");
+  // the previous band's last DCs are read in place (null: band 0, zeros)
+  EntArgs a = ent_args(b, n);
+  a.dc_pred = d_prev;
   HIP_TRY(launch_seg_dc(a, b->stream));
   HIP_TRY(hipMemcpyAsync(d_hist, b->d_hist, sizeof(uint32_t) * n * 4 * 257, hipMemcpyDeviceToDevice, b->stream));
   return MIJ_OK;
 }
 
-extern "C" int mij_band_pack_async(mij_batch *b, int n, const uint32_t *d_ghist, uint64_t *d_bits) {
-  if (band_check(b, n, "band_pack_async")) return g_err;
-  if (!d_ghist || !d_bits) return fail(MIJ_EINVAL, "band_pack_async: null argument");
+extern "C" int mij_band_tables_async(mij_batch *b, int n, const uint32_t *d_ghist, uint64_t *d_bound) {
+  if (band_check(b, n, "band_tables_async")) return g_err;
+  if (!d_ghist || !d_bound) return fail(MIJ_EINVAL, "band_tables_async: null argument");
   if (ensure_pieces(b, (size_t)n * 3)) return g_err;
-  // the tables from the summed histograms, then every scan of the band packed
-  // from bit 0 (the root shifts it to its place): no band waits for the bit
-  // counts of the bands before it
-  HIP_TRY(hipMemcpyAsync(b->d_hist, d_ghist, sizeof(uint32_t) * n * 4 * 257, hipMemcpyDeviceToDevice, b->stream));
-  EntArgs a = ent_args(b, n, 0, true);
+  // the tables from the summed histograms (read in place), then the band's
+  // words bounded from its own histograms and those code lengths: the caller
+  // sizes the word exchange from the bound while the band packs
+  EntArgs a = ent_args(b, n);
+  a.hist = const_cast<uint32_t *>(d_ghist);
   HIP_TRY(launch_tables(a, b->stream));
-  HIP_TRY(hipMemsetAsync(b->d_bitbase, 0, sizeof(uint32_t) * n * 4, b->stream));
+  if (!b->d_bound_acc) {
+    HIP_TRY(dalloc(&b->d_bound_acc, 2));
+    HIP_TRY(hipMemsetAsync(b->d_bound_acc, 0, 2 * sizeof(unsigned long long), b->stream));
+  }
+  HIP_TRY(launch_band_bound(b->d_hist, b->d_ehuf, n, b->d_bound_acc, (unsigned long long *)d_bound, b->stream));
+  b->band_async_n = -n;  // tables built, not packed yet
+  return MIJ_OK;
+}
+
+extern "C" int mij_band_pack_async(mij_batch *b, int n, uint64_t *d_bits) {
+  if (band_check(b, n, "band_pack_async")) return g_err;
+  if (!d_bits) return fail(MIJ_EINVAL, "band_pack_async: null d_bits");
+  if (b->band_async_n != -n) return fail(MIJ_EINVAL, "band_pack_async: needs mij_band_tables_async of the same frames first");
+  // every scan of the band packed from bit 0 (the root shifts it to its
+  // place): no band waits for the bit counts of the bands before it
   if (b->raw_dirty) HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->raw_dirty * b->g.raw_fs, b->stream));
   b->raw_dirty = n;
+  EntArgs a = ent_args(b, n);
   HIP_TRY(launch_pack_lb(a, b->stream));
   HIP_TRY(launch_band_count((const unsigned long long *)b->d_scan_bits, n, b->d_pieces,
                             (unsigned long long *)d_bits, b->stream));
@@ -1443,13 +1470,13 @@ extern "C" int mij_band_pack_async(mij_batch *b, int n, const uint32_t *d_ghist,
   return MIJ_OK;
 }
 
-extern "C" int mij_band_words_async(mij_batch *b, int n, uint32_t *d_dst) {
+extern "C" int mij_band_words_async(mij_batch *b, int n, uint32_t *d_dst, size_t cap_words) {
   if (band_check(b, n, "band_words_async")) return g_err;
   if (!d_dst || n != b->band_async_n) return fail(MIJ_EINVAL, "band_words_async: needs mij_band_pack_async of the same frames first");
   // the move table of mij_band_pack_async, words of frames 0..n-1 in (frame,
-  // scan) order into d_dst (the caller sized it from that call's word
-  // count), zeroed behind
-  HIP_TRY(launch_move_pieces(b->d_raw, b->g, d_dst, b->d_pieces, n * 3, 64 * 1024, b->stream));
+  // scan) order into d_dst (cap_words long: words beyond it are dropped, and
+  // the root's assembly sees the overflow in the counts), zeroed behind
+  HIP_TRY(launch_move_pieces(b->d_raw, b->g, d_dst, b->d_pieces, n * 3, 64 * 1024, (long long)cap_words, b->stream));
   if (n >= b->raw_dirty) b->raw_dirty = 0;
   return MIJ_OK;
 }
@@ -1457,9 +1484,9 @@ extern "C" int mij_band_words_async(mij_batch *b, int n, uint32_t *d_dst) {
 extern "C" int mij_assemble_tables_async(mij_batch *b, int n, const uint32_t *d_ghist) {
   if (band_check(b, n, "assemble_tables_async", true)) return g_err;
   if (!d_ghist) return fail(MIJ_EINVAL, "assemble_tables_async: null d_ghist");
-  HIP_TRY(hipMemcpyAsync(b->d_hist, d_ghist, sizeof(uint32_t) * n * 4 * 257, hipMemcpyDeviceToDevice, b->stream));
   HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * n, b->stream));
   EntArgs a = ent_args(b, n);
+  a.hist = const_cast<uint32_t *>(d_ghist);  // (read in place: k_tables only reads it)
   HIP_TRY(launch_tables(a, b->stream));
   b->asm_tables_n = n;
   return MIJ_OK;
@@ -1602,7 +1629,7 @@ extern "C" int mij_band_words_all(mij_batch *b, int n, void *dst, size_t cap_wor
     }
     HIP_TRY(hipMemcpyAsync(b->d_pieces, pcs.data(), sizeof(unsigned long long) * pcs.size(), hipMemcpyHostToDevice,
                            b->stream));
-    HIP_TRY(launch_move_pieces(b->d_raw, b->g, d, b->d_pieces, np, max_words, b->stream));
+    HIP_TRY(launch_move_pieces(b->d_raw, b->g, d, b->d_pieces, np, max_words, (long long)total, b->stream));
   }
   if (!dst_on_device && total)
     HIP_TRY(hipMemcpyAsync(dst, d, total * 4, hipMemcpyDeviceToHost, b->stream));

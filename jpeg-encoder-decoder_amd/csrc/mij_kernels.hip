@@ -2825,14 +2825,13 @@ __global__ void k_or_pieces(uint32_t *raw, long long raw_fs, long long rw0, long
 // all-zero buffers): piece blockIdx.y = {frame * 3 + scan, words, first
 // destination word}, from the start of the scan.
 __global__ void k_move_pieces(uint32_t *raw, long long raw_fs, long long rw0, long long rw1,
-                              uint32_t *dst, const unsigned long long *pieces) {
+                              uint32_t *dst, const unsigned long long *pieces, long long cap) {
   const unsigned long long *pc = pieces + 3 * (long long)blockIdx.y;
-  const long long fc = (long long)pc[0], n = (long long)pc[1];
+  const long long fc = (long long)pc[0], n = (long long)pc[1], d0 = (long long)pc[2];
   const long long f = fc / 3, c = fc - 3 * f;
   uint32_t *src = raw + f * raw_fs + (c == 0 ? 0 : rw0 + (c == 2 ? rw1 : 0));
-  uint32_t *dp = dst + (long long)pc[2];
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    dp[i] = src[i];
+    if (d0 + i < cap) dst[d0 + i] = src[i];  // (past the destination: dropped, still zeroed)
     src[i] = 0u;
   }
 }
@@ -2896,7 +2895,47 @@ __global__ void k_band_assembly(const unsigned long long *allbits, int world, in
       at += (bits + 31) >> 5;
       scan_bits[i] = off + bits;
     }
-    if (at > stride) *over = 1;  // a band's words beyond its row: assemble nothing wrong
+    if (at > stride)  // a band's words beyond its row: fail the frames, assemble nothing wrong
+      for (int f = 0; f < n; f++) over[f] = 1;
+  }
+}
+
+// An upper bound of a band's words before it packs: its bits per frame are
+// exactly the sum over its tokens of code length + magnitude bits (the low
+// nibble of the symbol, encoder.c:385-423), i.e. its own histograms
+// (hist[f][t][sym]) weighted by the tables' code lengths (ehuf, len << 16 |
+// code); the three scans' words round up at most 3 words more.  A wave per
+// frame; the workgroups' sums meet in acc = {sum, arrivals}, which the last
+// workgroup to arrive reads, writes to bound[0] and leaves zeroed.
+__global__ __launch_bounds__(256) void k_band_bound(const uint32_t *hist, const uint32_t *ehuf, int n,
+                                                    unsigned long long *acc, unsigned long long *bound) {
+  __shared__ unsigned long long s_w[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, f = blockIdx.x * 4 + w;
+  unsigned long long words = 0;
+  if (f < n) {
+    unsigned long long b = 0;
+    for (int t = 0; t < 4; t++) {
+      const uint32_t *h = hist + ((long long)f * 4 + t) * 257;
+      const uint32_t *e = ehuf + ((long long)f * 4 + t) * 256;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int s = 64 * k + lane;
+        b += (unsigned long long)h[s] * ((e[s] >> 16) + (s & 15));
+      }
+    }
+    for (int off = 32; off; off >>= 1) b += __shfl_xor(b, off);
+    words = (b + 31) / 32 + 3;
+  }
+  if (lane == 0) s_w[w] = words;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(&acc[0], s_w[0] + s_w[1] + s_w[2] + s_w[3]);
+    __threadfence();
+    if (atomicAdd(&acc[1], 1ull) == gridDim.x - 1) {
+      __threadfence();
+      bound[0] = atomicExch(&acc[0], 0ull);
+      acc[1] = 0;
+    }
   }
 }
 
@@ -3064,16 +3103,22 @@ hipError_t launch_or_pieces(uint32_t *raw, const Geom &g, const uint32_t *src,
 }
 
 hipError_t launch_move_pieces(uint32_t *raw, const Geom &g, uint32_t *dst,
-                              const unsigned long long *d_pieces, int npieces, long long max_words, hipStream_t s) {
+                              const unsigned long long *d_pieces, int npieces, long long max_words, long long cap,
+                              hipStream_t s) {
   if (npieces <= 0 || max_words <= 0) return hipSuccess;
   const long long chunks = (max_words + 1023) / 1024;
   hipLaunchKernelGGL(k_move_pieces, dim3((unsigned)(chunks < 64 ? chunks : 64), (unsigned)npieces), dim3(256), 0, s,
-                     raw, g.raw_fs, g.raw_words[0], g.raw_words[1], dst, d_pieces);
+                     raw, g.raw_fs, g.raw_words[0], g.raw_words[1], dst, d_pieces, cap);
   return hipGetLastError();
 }
 
 hipError_t launch_band_last(const int16_t *dc, const Geom &g, int n, int16_t *last, hipStream_t s) {
   hipLaunchKernelGGL(k_band_last, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, dc, g, n, last);
+  return hipGetLastError();
+}
+hipError_t launch_band_bound(const uint32_t *hist, const uint32_t *ehuf, int n, unsigned long long *acc,
+                             unsigned long long *bound, hipStream_t s) {
+  hipLaunchKernelGGL(k_band_bound, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, hist, ehuf, n, acc, bound);
   return hipGetLastError();
 }
 hipError_t launch_band_count(const unsigned long long *scan_bits, int n, unsigned long long *pieces,

@@ -28,7 +28,7 @@ EXPORTS = [
     "mij_band_analyze", "mij_band_histograms", "mij_band_tables", "mij_band_pack", "mij_band_words",
     "mij_assemble_begin", "mij_assemble_words", "mij_assemble_end",
     "mij_band_words_all", "mij_assemble_pieces", "mij_assembler_create",
-    "mij_band_analyze_async", "mij_band_histograms_async", "mij_band_pack_async",
+    "mij_band_analyze_async", "mij_band_histograms_async", "mij_band_tables_async", "mij_band_pack_async",
     "mij_band_words_async", "mij_assemble_tables_async", "mij_assemble_async",
     "mij_probe_mfma", "mij_colour_lut", "mij_build_target",
     # change detector (reference include/brain.h:7-10 drop-in + extensions)
@@ -110,8 +110,9 @@ def load() -> C.CDLL:
     lib.mij_batch_audit.argtypes = [p, i, p]
     lib.mij_band_analyze_async.argtypes = [p, i, p]
     lib.mij_band_histograms_async.argtypes = [p, i, p, p]
-    lib.mij_band_pack_async.argtypes = [p, i, p, p]
-    lib.mij_band_words_async.argtypes = [p, i, p]
+    lib.mij_band_tables_async.argtypes = [p, i, p, p]
+    lib.mij_band_pack_async.argtypes = [p, i, p]
+    lib.mij_band_words_async.argtypes = [p, i, p, sz]
     lib.mij_assemble_tables_async.argtypes = [p, i, p]
     lib.mij_assemble_async.argtypes = [p, i, p, i, p, sz]
     lib.mij_batch_build_tables.argtypes = [p, i, p]
@@ -524,13 +525,18 @@ class Batch:
     def band_histograms_async(self, n: int, d_prev: int, d_hist: int) -> None:
         _check(self.lib.mij_band_histograms_async(self.h_, n, d_prev, d_hist), "band_histograms_async")
 
-    def band_pack_async(self, n: int, d_ghist: int, d_bits: int) -> None:
-        """tables from the summed histograms, the band packed from bit 0;
-        d_bits: uint64 [3n + 1] device buffer (bits per scan, word count)"""
-        _check(self.lib.mij_band_pack_async(self.h_, n, d_ghist, d_bits), "band_pack_async")
+    def band_tables_async(self, n: int, d_ghist: int, d_bound: int) -> None:
+        """tables from the summed histograms; an upper bound of the band's
+        words -> d_bound (uint64 [1] device buffer)"""
+        _check(self.lib.mij_band_tables_async(self.h_, n, d_ghist, d_bound), "band_tables_async")
 
-    def band_words_async(self, n: int, d_dst: int) -> None:
-        _check(self.lib.mij_band_words_async(self.h_, n, d_dst), "band_words_async")
+    def band_pack_async(self, n: int, d_bits: int) -> None:
+        """the band packed from bit 0; d_bits: uint64 [3n + 1] device buffer
+        (bits per scan, then the word count)"""
+        _check(self.lib.mij_band_pack_async(self.h_, n, d_bits), "band_pack_async")
+
+    def band_words_async(self, n: int, d_dst: int, cap_words: int) -> None:
+        _check(self.lib.mij_band_words_async(self.h_, n, d_dst, cap_words), "band_words_async")
 
     def assemble_tables_async(self, n: int, d_ghist: int) -> None:
         _check(self.lib.mij_assemble_tables_async(self.h_, n, d_ghist), "assemble_tables_async")

@@ -239,6 +239,14 @@ class DeviceExchange:
             self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return t
 
+    def host_buffer(self, n: int):
+        """a pinned host int64 buffer of n values, reused (a step reads it
+        before the next step writes it)"""
+        hb = getattr(self, "_host", None)
+        if hb is None or hb.numel() < n:
+            hb = self._host = self.torch.empty(n, dtype=self.torch.int64, pin_memory=True)
+        return hb[:n]
+
     def gather(self, buf):
         """every rank's equally sized buffer to the root: [world, n] there"""
         if self.world == 1:
@@ -255,8 +263,9 @@ def encode_banded_dev(band, n: int, xch, frame_batch=None, events=None):
     """encode_banded with the device-resident protocol: the last DCs (int16
     [n, 4], gathered as int32 pairs), the histograms (summed in place), the
     bit counts (gathered) and the packed words (gathered to the root) never
-    leave HBM; the library calls and the collectives all run on the band
-    batch's stream.  Every band packs from bit 0, so the bands pack at once;
+    leave HBM -- only the bands' word bounds (one int64 per rank) come to the
+    host, to size the word exchange; the library calls and the collectives all
+    run on the band batch's stream.  Every band packs from bit 0, so the bands pack at once;
     the root shifts each band's words to its bit position while assembling.
     The root's frame_batch (an assembler) builds its tables on its own stream
     while the bands pack, then assembles.  `events`: optional list that
@@ -279,31 +288,49 @@ def encode_banded_dev(band, n: int, xch, frame_batch=None, events=None):
         last = torch.empty((n, 4), dtype=torch.int16, device=dev)
         band.band_analyze_async(n, last.data_ptr())
         mark("analyze")
-        lasts = xch.all_gather(last.view(torch.int32))           # [world, n, 2] = int16 [world, n, 4]
-        prev = torch.zeros((n, 4), dtype=torch.int16, device=dev) if rank == 0 else \
-            lasts[rank - 1].contiguous().view(torch.int16)
+        prev = 0                                                  # band 0: zeros
+        if world > 1:
+            lasts = xch.all_gather(last.view(torch.int32))       # [world, n, 2] = int16 [world, n, 4]
+            if rank:
+                prev = lasts[rank - 1].contiguous().view(torch.int16)
         hist = torch.empty((n, 4, 257), dtype=torch.int32, device=dev)
-        band.band_histograms_async(n, prev.data_ptr(), hist.data_ptr())
+        band.band_histograms_async(n, prev if isinstance(prev, int) else prev.data_ptr(), hist.data_ptr())
         xch.all_reduce_sum(hist)
         mark("histograms")
         if a is not None:
             a.wait_stream(s)
             with torch.cuda.stream(a):
                 frame_batch.assemble_tables_async(n, hist.data_ptr())
+        # the bands' word bounds reach the host while the bands pack: no step
+        # waits for the packing before the word exchange is issued
+        bound = torch.empty(1, dtype=torch.int64, device=dev)
+        band.band_tables_async(n, hist.data_ptr(), bound.data_ptr())
+        bounds = xch.all_gather(bound)                            # [world, 1]
+        # (the copy into pinned memory runs on torch's own stream: the host
+        # allocator keeps an event of the copy's stream, and the library's
+        # stream may be gone before that event is released)
+        h_bounds = xch.host_buffer(world)
+        d = torch.cuda.default_stream(dev)
+        d.wait_stream(s)
+        with torch.cuda.stream(d):
+            h_bounds.copy_(bounds.view(-1), non_blocking=True)
+            ready = torch.cuda.Event()
+            ready.record(d)
         bits = torch.empty(3 * n + 1, dtype=torch.int64, device=dev)
-        band.band_pack_async(n, hist.data_ptr(), bits.data_ptr())
+        band.band_pack_async(n, bits.data_ptr())
         allbits = xch.all_gather(bits).contiguous()               # [world, 3n + 1]
         mark("pack")
-        stride = int(allbits[:, 3 * n].max().item())              # the one host read of a step
-        buf = torch.empty(max(stride, 1), dtype=torch.int32, device=dev)
-        band.band_words_async(n, buf.data_ptr())
+        ready.synchronize()
+        stride = max(1, int(h_bounds.max()))
+        buf = torch.empty(stride, dtype=torch.int32, device=dev)
+        band.band_words_async(n, buf.data_ptr(), stride)
         gathered = xch.gather(buf)
         mark("words")
         if a is None:
             return
     a.wait_stream(s)
     with torch.cuda.stream(a):
-        frame_batch.assemble_async(n, allbits.data_ptr(), world, gathered.data_ptr(), gathered.shape[1])
+        frame_batch.assemble_async(n, allbits.data_ptr(), world, gathered.data_ptr(), stride)
     # the tensors read by the assembly are freed on the band stream: keep that
     # stream behind the assembly
     s.wait_stream(a)

@@ -276,7 +276,8 @@ def _dev_bands(port, q):
                        recipes.config3_frame(6, 320, 480)])
     n, H, W = frames.shape[:3]
     res = {}
-    for world in (1, 2, 3, 4):
+
+    def protocol(world, shrink=0):
         bands = []
         for r in range(world):
             r0, rows = sharding.band_rows(H, world, r)
@@ -288,35 +289,50 @@ def _dev_bands(port, q):
             b.band_analyze_async(n, l.data_ptr())
             b.sync()
         hist = [torch.empty((n, 4, 257), dtype=torch.int32, device=dev) for _ in bands]
-        zero = torch.zeros((n, 4), dtype=torch.int16, device=dev)
-        torch.cuda.synchronize()  # (torch zeroes it on its own stream)
         for r, b in enumerate(bands):
-            b.band_histograms_async(n, (zero if r == 0 else last[r - 1]).data_ptr(), hist[r].data_ptr())
+            b.band_histograms_async(n, 0 if r == 0 else last[r - 1].data_ptr(), hist[r].data_ptr())
             b.sync()
         ghist = torch.stack(hist).sum(0, dtype=torch.int32).contiguous()
         torch.cuda.synchronize()
         full = mijpeg.Batch(W, H, n, assembler=True)
         full.assemble_tables_async(n, ghist.data_ptr())
+        bound = [torch.empty(1, dtype=torch.int64, device=dev) for _ in bands]
         bits = [torch.empty(3 * n + 1, dtype=torch.int64, device=dev) for _ in bands]
-        for b, t in zip(bands, bits):
-            b.band_pack_async(n, ghist.data_ptr(), t.data_ptr())
+        for b, d, t in zip(bands, bound, bits):
+            b.band_tables_async(n, ghist.data_ptr(), d.data_ptr())
+            b.band_pack_async(n, t.data_ptr())
             b.sync()
         allbits = torch.stack(bits).contiguous()
-        stride = int(allbits[:, 3 * n].max())
+        # the bounds hold (at most 3 words per frame above the words)
+        for d, t in zip(bound, bits):
+            assert 0 <= int(d) - int(t[3 * n]) <= 3 * n
+        stride = int(torch.cat(bound).max()) - shrink
         gathered = torch.zeros((world, stride), dtype=torch.int32, device=dev)
         torch.cuda.synchronize()
         for r, b in enumerate(bands):
-            b.band_words_async(n, gathered[r].data_ptr())
+            b.band_words_async(n, gathered[r].data_ptr(), stride)
             b.sync()
         full.assemble_async(n, allbits.data_ptr(), world, gathered.data_ptr(), stride)
         full.sync()
-        res[world] = [full.output(f) for f in range(n)]
+        out = []
+        for f in range(n):
+            try:
+                out.append(full.output(f))
+            except mijpeg.MijError as e:
+                out.append(str(e))
         # the band batches encode whole frames correctly afterwards
         bands[-1].encode(n)
-        res[(world, "after")] = bands[-1].output(0)
+        after = bands[-1].output(0)
         for b in bands:
             b.close()
         full.close()
+        return out, after
+
+    for world in (1, 2, 3, 4):
+        res[world], res[(world, "after")] = protocol(world)
+    # a word buffer shorter than a band's words: every frame fails, nothing
+    # is written past the buffer
+    res["short"], _ = protocol(2, shrink=4000)
     dist.init_process_group("nccl", rank=0, world_size=1)
     try:
         band = mijpeg.Batch(W, H, n)
@@ -360,5 +376,6 @@ def test_device_resident_band_protocol():
         # a band batch left by the protocol encodes its own rows correctly
         r0, rows = sharding.band_rows(320, world, world - 1)
         assert res[(world, "after")] == O.cref_encode(np.ascontiguousarray(frames[0][r0:r0 + rows]))
+    assert all(isinstance(o, str) for o in res["short"]), res["short"]
     assert res["nccl"] == [want, want]
     assert res["phases"] == ["start", "analyze", "histograms", "pack", "words", "assemble"]
