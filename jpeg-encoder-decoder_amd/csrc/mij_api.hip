@@ -687,10 +687,82 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   // segment-first DC tokens: inside k_tables (its DC-table waves), or on
   // their own when the caller's tables are given
   static const int segdc_dbg = getenv("MIJ_SEGDC_DBG") ? atoi(getenv("MIJ_SEGDC_DBG")) : 0;  // diag build
-  a.seg_dc = dc_fix && !tables_given ? 1 | segdc_dbg : 0;
-  if (dc_fix && tables_given) HIP_TRY(launch_seg_dc(a, st));
+  // (A/B: MIJ_SEGDC_FUSED=1 runs them in k_tables' DC waves -- two waves per
+  // frame, 0.11 ms of a config-3 launch against a few us spread over the chip)
+  static const bool segdc_fused = getenv("MIJ_SEGDC_FUSED") && atoi(getenv("MIJ_SEGDC_FUSED"));
+  a.seg_dc = dc_fix && !tables_given && segdc_fused ? 1 | segdc_dbg : 0;
+  if (dc_fix && !a.seg_dc) HIP_TRY(launch_seg_dc(a, st));
   if (t) HIP_TRY(hipEventRecord(b->ev[4], st));
-  if (!tables_given) HIP_TRY(launch_tables(a, st));
+  // diagnostics (MIJ_TAB_TIME with the diag build): per-wave phase clocks of k_tables
+  static const bool ttime = getenv("MIJ_TAB_TIME") != nullptr;
+  if (!tables_given && ttime) {
+    EntArgs at = a;
+    const size_t nt = (size_t)nframes * 4 * 10;
+    HIP_TRY(hipMalloc(&at.dbg, sizeof(unsigned long long) * nt));
+    HIP_TRY(hipMemsetAsync(at.dbg, 0, sizeof(unsigned long long) * nt, st));
+    HIP_TRY(launch_tables(at, st));
+    std::vector<unsigned long long> h(nt);
+    HIP_TRY(hipMemcpyAsync(h.data(), at.dbg, sizeof(unsigned long long) * nt, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipFree(at.dbg));
+    // s_memtime: shader clocks; phases 0-1 load, 1-2 sort, 2-3 merges, 3-4
+    // depths, 4-5 counts + limit, 5-6 symbol order, 6-7 codes + stores
+    for (int kind = 0; kind < 2; kind++) {
+      double ph[8] = {0};
+      int cnt = 0;
+      for (int f = 0; f < nframes; f++)
+        for (int tt = kind; tt < 4; tt += 2) {
+          const unsigned long long *r = &h[((size_t)f * 4 + tt) * 10];
+          if (!r[7]) continue;
+          for (int k = 0; k < 7; k++) ph[k] += (double)(r[k + 1] - r[k]);
+          ph[7] += (double)(r[0] - r[8]);  // kernel entry -> table start (DC waves: the segment DCs)
+          cnt++;
+        }
+      if (cnt)
+        fprintf(stderr, "k_tables %s waves %d, clocks: pre %.0f load %.0f sort %.0f merge %.0f depth %.0f limit %.0f order %.0f codes %.0f\n",
+                kind ? "AC" : "DC", cnt, ph[7] / cnt, ph[0] / cnt, ph[1] / cnt, ph[2] / cnt, ph[3] / cnt, ph[4] / cnt,
+                ph[5] / cnt, ph[6] / cnt);
+    }
+    {  // one frame's span: first wave entry to last wave end
+      double span = 0;
+      for (int f = 0; f < nframes; f++) {
+        unsigned long long t0 = ~0ull, t1 = 0;
+        for (int tt = 0; tt < 4; tt++) {
+          const unsigned long long *r = &h[((size_t)f * 4 + tt) * 10];
+          t0 = std::min(t0, r[8]);
+          t1 = std::max(t1, r[7]);
+        }
+        span += (double)(t1 - t0);
+      }
+      double sw = 0, ww = 0, ent = 0;
+      for (int f = 0; f < nframes; f++)
+        for (int tt = 0; tt < 4; tt += 2) {
+          const unsigned long long *r = &h[((size_t)f * 4 + tt) * 10];
+          sw += (double)(r[9] - r[8]);
+          ww += (double)(r[0] - r[9]);
+        }
+      for (int f = 0; f < nframes; f++) {
+        unsigned long long e0 = ~0ull, e1 = 0;
+        for (int tt = 0; tt < 4; tt++) {
+          e0 = std::min(e0, h[((size_t)f * 4 + tt) * 10 + 8]);
+          e1 = std::max(e1, h[((size_t)f * 4 + tt) * 10 + 8]);
+        }
+        ent += (double)(e1 - e0);
+      }
+      if (nframes == 1)
+        for (int tt = 0; tt < 4; tt++) {
+          const unsigned long long *r = &h[(size_t)tt * 10];
+          fprintf(stderr, "k_tables wave %d: entry +%lld start +%lld end +%lld; phases %lld %lld %lld %lld %lld %lld %lld\n", tt,
+                  (long long)(r[8] - h[8]), (long long)(r[0] - h[8]), (long long)(r[7] - h[8]), (long long)(r[1] - r[0]),
+                  (long long)(r[2] - r[1]), (long long)(r[3] - r[2]), (long long)(r[4] - r[3]), (long long)(r[5] - r[4]),
+                  (long long)(r[6] - r[5]), (long long)(r[7] - r[6]));
+        }
+      fprintf(stderr, "k_tables frame span %.0f clocks; DC waves: segment DCs %.0f, wait %.0f; wave entry spread %.0f\n",
+              span / nframes, sw / (2.0 * nframes), ww / (2.0 * nframes), ent / nframes);
+    }
+  } else if (!tables_given) {
+    HIP_TRY(launch_tables(a, st));
+  }
   if (t) HIP_TRY(hipEventRecord(b->ev[5], st));
   // segment bits, scan offsets and packing in one look-back pass
   if (b->raw_dirty) {

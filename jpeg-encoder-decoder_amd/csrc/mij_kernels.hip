@@ -1442,6 +1442,38 @@ struct SegDc {
   int comp, dc, pred;
   bool ok;
 };
+#ifndef MIJ_SEGDC_BF
+#define MIJ_SEGDC_BF 0
+#endif
+#ifndef MIJ_SEGDC_U
+#define MIJ_SEGDC_U 32
+#endif
+#if MIJ_SEGDC_BF
+// (branch-free: seg_info's cases as selects and both loads from clamped
+// addresses, so a lane's U segments issue their loads back to back)
+__device__ __forceinline__ SegDc seg_dc_load(const EntArgs &a, const FGeom &fg, int f, int s) {
+  const Geom &G = a.g;
+  SegDc r;
+  const bool y = s < G.nsy;
+  const int c = s - G.nsy;
+  r.comp = y ? 0 : (c >= G.nsc ? 2 : 1);
+  const int local = y ? s : (r.comp == 1 ? c : c - G.nsc);
+  const int cstart = y ? 0 : (r.comp == 1 ? fg.nY : fg.nY + fg.nC);
+  const int row = (int)div_by((uint32_t)max(local, 0), G.tx_m, G.tx_s), tx = local - row * G.tiles_x;
+  const int first = cstart + row * (y ? fg.bw : fg.mw) + tx * (y ? 16 : 8);
+  r.ok = s >= 0 && s < G.nseg && row < (y ? 2 * fg.rows : fg.rows) && tx < fg.tiles_x;
+  const long long fb = (long long)f * G.nblk;
+  const int at = r.ok ? first : 0;
+  const int dc = (int)a.dc[fb + at];
+  const int prev = (int)a.dc[fb + max(at - 1, 0)];
+  // a component's first block is predicted from 0 (encoder.c:168-177), or
+  // from the previous band's last DC when the frame is split into bands
+  const int p0 = a.dc_pred ? (int)a.dc_pred[f * 4 + r.comp] : 0;
+  r.dc = r.ok ? dc : 0;
+  r.pred = !r.ok ? 0 : (first == cstart ? p0 : prev);
+  return r;
+}
+#else
 __device__ __forceinline__ SegDc seg_dc_load(const EntArgs &a, const FGeom &fg, int f, int s) {
   SegDc r;
   int first, cstart, local;
@@ -1456,7 +1488,11 @@ __device__ __forceinline__ SegDc seg_dc_load(const EntArgs &a, const FGeom &fg, 
   }
   return r;
 }
-__device__ __forceinline__ void seg_dc_store(const EntArgs &a, int f, int s, const SegDc &r, uint32_t (*h)[16]) {
+#endif
+// The class counts go to hs[(luma ? 0 : 16) + class][lane & 31]: 32 copies
+// of every counter, so a wave's 64 atomics meet at most in pairs (one
+// counter per class took every lane of a wave with the same class in turn).
+__device__ __forceinline__ void seg_dc_store(const EntArgs &a, int f, int s, const SegDc &r, uint32_t *hs, int lane) {
   if (!r.ok) return;
   const int diff = r.dc - r.pred;
   const int cls = mag_class(diff);
@@ -1464,20 +1500,21 @@ __device__ __forceinline__ void seg_dc_store(const EntArgs &a, int f, int s, con
   if (!(a.seg_dc & 2))
 #endif
   a.tok0[(long long)f * a.g.nseg + s] = (uint32_t)cls | (mag_bits(diff, cls) << 16);
-  atomicAdd(&h[r.comp ? 1 : 0][cls], 1u);
+  atomicAdd(&hs[((r.comp ? 16 : 0) + cls) * 32 + (lane & 31)], 1u);
 }
 
 __global__ __launch_bounds__(256) void k_seg_dc(EntArgs a) {
-  __shared__ uint32_t h[2][16];
+  __shared__ uint32_t hs[32 * 32];
   const int per = (a.g.nseg + 255) / 256;
   const int f = blockIdx.x / per;
   const int s = (blockIdx.x - f * per) * 256 + threadIdx.x;
-  if (threadIdx.x < 32) (&h[0][0])[threadIdx.x] = 0;
+  for (int i = threadIdx.x; i < 32 * 32; i += 256) hs[i] = 0;
   __syncthreads();
-  if (s < a.g.nseg) seg_dc_store(a, f, s, seg_dc_load(a, frame_geom(a.g, a.fdims, f), f, s), h);
+  if (s < a.g.nseg) seg_dc_store(a, f, s, seg_dc_load(a, frame_geom(a.g, a.fdims, f), f, s), hs, threadIdx.x & 63);
   __syncthreads();
   if (threadIdx.x < 32) {
-    const uint32_t v = (&h[0][0])[threadIdx.x];
+    uint32_t v = 0;
+    for (int c = 0; c < 32; c++) v += hs[threadIdx.x * 32 + ((c + threadIdx.x) & 31)];
     if (v)
       atomicAdd(&a.hist[((long long)f * 4 + (threadIdx.x >= 16 ? 2 : 0)) * 257 + (threadIdx.x & 15)], v);
   }
@@ -1503,7 +1540,7 @@ __global__ __launch_bounds__(256) void k_seg_dc(EntArgs a) {
 // each merge costs one LDS round trip and a few uniform VALU selects; the
 // code lengths come from the merge tree afterwards (pointer jumping).
 #ifndef MIJ_TAB_QUEUE
-#define MIJ_TAB_QUEUE 1
+#define MIJ_TAB_QUEUE 2
 #endif
 
 struct TabScratch {
@@ -1589,8 +1626,15 @@ __device__ __forceinline__ void top2_swap(unsigned long long &k1, unsigned long 
 }
 
 // extra: DC class counts the caller adds to hist (the segment-first DCs), or null
+// (MIJ_K1_DIAG build, MIJ_TAB_TIME: tm != null gets the wave's phase clocks)
+#ifdef MIJ_K1_DIAG
+#define TAB_T(k) do { if (tm && lane == 0) tm[k] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define TAB_T(k) do { } while (0)
+#endif
 __device__ void build_table_wave(const uint32_t *hist, const uint32_t *extra, HuffCode *hc, uint32_t *ehuf,
-                                 TabScratch *S, int lane, int *err) {
+                                 TabScratch *S, int lane, int *err, unsigned long long *tm = nullptr) {
+  TAB_T(0);
   uint32_t f[5];
   int cl[5], gr[5];
 #pragma unroll
@@ -1607,6 +1651,7 @@ __device__ void build_table_wave(const uint32_t *hist, const uint32_t *extra, Hu
   }
   if (lane < 32) { S->clf[lane] = 0; S->cnt[lane] = 0; }
   wave_lds_sync();
+  TAB_T(1);
 #if MIJ_TAB_QUEUE
   {
     // the leaves: symbols 0..255 with a nonzero count, ascending by key
@@ -1663,6 +1708,7 @@ __device__ void build_table_wave(const uint32_t *hist, const uint32_t *extra, Hu
       }
     }
     wave_lds_sync();
+    TAB_T(2);
     // every lane runs the loop on the same (uniform) values; lane 0 alone
     // writes.  v1 = the least key, v2 = the next (encoder.c:196-206)
     int lh = 0, mh = 0, mt = 0;
@@ -1707,6 +1753,7 @@ __device__ void build_table_wave(const uint32_t *hist, const uint32_t *extra, Hu
       mt++;
       wave_lds_sync();
     }
+    TAB_T(3);
     // code lengths = leaf depths in the merge tree (pointer jumping: nine
     // rounds cover <= 513 nodes)
     const int nnodes = 257 + max(nl - 1, 0);
@@ -1799,6 +1846,7 @@ __device__ void build_table_wave(const uint32_t *hist, const uint32_t *extra, Hu
   }
 #endif
   wave_lds_sync();
+  TAB_T(4);
   int bad = 0;
 #pragma unroll
   for (int i = 0; i < 5; i++) {
@@ -1860,6 +1908,7 @@ __device__ void build_table_wave(const uint32_t *hist, const uint32_t *extra, Hu
     }
   }
   wave_lds_sync();
+  TAB_T(5);
   if (S->err) {
     if (lane == 0) *err = 1;
     return;
@@ -1880,6 +1929,7 @@ __device__ void build_table_wave(const uint32_t *hist, const uint32_t *extra, Hu
     }
   }
   wave_lds_sync();
+  TAB_T(6);
   const int n = S->n;
   // every output address is written exactly once, from LDS staging
   for (int k = lane; k < 256; k += 64) {
@@ -1905,6 +1955,444 @@ __device__ void build_table_wave(const uint32_t *hist, const uint32_t *extra, Hu
     hc->sym_code[k] = S->scode[k];
     ehuf[k] = L ? ((uint32_t)L << 16) | (uint32_t)S->scode[k] : 0u;
   }
+  TAB_T(7);
+}
+
+// ---------------------------------------------------------------------------
+// build_table_wave2 (MIJ_TAB_QUEUE 2): the same tables, every phase without a
+// lane-serial LDS chain.
+//  - leaves sorted by a register bitonic network (DPP / permlane partners, no
+//    LDS round trips);
+//  - the two-queue merge runs on uniform values read with v_readlane from
+//    64-entry register windows of the queues; a key carries its node's id and
+//    leaf count, so lane 0 only writes (the new queue entry and the two
+//    children's parent links, no dependent reads);
+//  - code lengths (leaf depths) and the chain order of :223-226 (a leaf's
+//    place = the leaves of the left subtrees it hangs right of) by pointer
+//    jumping over the merge tree;
+//  - counts, the 16-bit limit loop (:239-259), the symbol order (:262-268) and
+//    the canonical codes (:280-300) on per-lane length vectors with ballots
+//    and readlane.
+// Key: freq << 32 | (256 - label) << 19 | leaves << 10 | node; (freq, label)
+// order the entries (labels of live entries are distinct), the low bits ride
+// along.  Nodes: leaf = its queue slot (0 = symbol 256), merge j = nl + j.
+// ---------------------------------------------------------------------------
+struct TabScratch2 {
+  union {
+    struct {
+      unsigned long long ql[257 + 64];  // sorted leaves, ~0 past the end
+      unsigned long long qm[256 + 64];  // merged nodes in queue order
+    };
+    struct {  // after the merges
+      int sorted[256];
+      int slen[256];
+      int scode[256];
+    };
+  };
+  int par[514];  // node -> parent (0xFFFF: root), then pointer-jumping state
+  int dep[514];
+  int off[514];
+  int scl[257];  // symbol -> code length (unlimited)
+  int spos[257];  // symbol -> place in the chain
+  int seq[257];   // chain order -> symbol
+};
+
+__device__ __forceinline__ unsigned long long rl64(unsigned long long v, int idx) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, idx);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), idx);
+  return ((unsigned long long)hi << 32) | lo;
+}
+// the value of lane ^ J (J < 64)
+template <int J>
+__device__ __forceinline__ unsigned long long xor_fetch(unsigned long long x, int lane) {
+  if constexpr (J == 1) return dpp_u64<0xB1>(x);  // quad_perm [1,0,3,2]
+  else if constexpr (J == 2) return dpp_u64<0x4E>(x);  // quad_perm [2,3,0,1]
+  else if constexpr (J == 4) {
+    const unsigned long long up = dpp_u64<0x12C>(x), dn = dpp_u64<0x124>(x);  // row_ror:12 (lane+4), :4 (lane-4)
+    return (lane & 4) ? dn : up;
+  } else if constexpr (J == 8) return dpp_u64<0x128>(x);  // row_ror:8
+  else {
+    unsigned long long a, b;
+    swap_u64<J>(x, a, b);
+    return (lane & J) ? a : b;
+  }
+}
+// the value of lane ^ (K - 1) (K <= 64)
+template <int K>
+__device__ __forceinline__ unsigned long long flip_fetch(unsigned long long x, int lane) {
+  if constexpr (K == 2) return dpp_u64<0xB1>(x);
+  else if constexpr (K == 4) return dpp_u64<0x1B>(x);  // quad_perm [3,2,1,0]
+  else if constexpr (K == 8) return dpp_u64<0x141>(x);  // row_half_mirror
+  else if constexpr (K == 16) return dpp_u64<0x140>(x);  // row_mirror
+  else if constexpr (K == 32) return dpp_u64<0x140>(xor_fetch<16>(x, lane));
+  else return flip_fetch<32>(xor_fetch<32>(x, lane), lane);
+}
+__device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsigned long long b) { return a < b ? a : b; }
+__device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a < b ? b : a; }
+
+// ascending bitonic sort of 256 keys, element e = lane + 64 r in k[r]
+template <int J>
+__device__ __forceinline__ void bsort_half(unsigned long long (&k)[4], int lane) {
+  if constexpr (J >= 64) {
+    constexpr int R = J / 64;
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      if (!(r & R)) {
+        const unsigned long long x = k[r], y = k[r | R];
+        k[r] = umin64(x, y);
+        k[r | R] = umax64(x, y);
+      }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const unsigned long long p = xor_fetch<J>(k[r], lane);
+      k[r] = (lane & J) ? umax64(k[r], p) : umin64(k[r], p);
+    }
+  }
+  if constexpr (J > 1) bsort_half<J / 2>(k, lane);
+}
+template <int K>
+__device__ __forceinline__ void bsort_level(unsigned long long (&k)[4], int lane) {
+  if constexpr (K <= 64) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const unsigned long long p = flip_fetch<K>(k[r], lane);
+      k[r] = (lane & (K / 2)) ? umax64(k[r], p) : umin64(k[r], p);
+    }
+  } else {
+    // partner e ^ (K - 1): register r ^ (K / 64 - 1), lane ^ 63
+    constexpr int X = K / 64 - 1;
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      if (r < (r ^ X)) {
+        const int q = r ^ X;
+        const unsigned long long mr = flip_fetch<64>(k[r], lane), mq = flip_fetch<64>(k[q], lane);
+        k[r] = umin64(k[r], mq);
+        k[q] = umax64(k[q], mr);
+      }
+  }
+  if constexpr (K >= 4) bsort_half<K / 4>(k, lane);
+  if constexpr (K < 256) bsort_level<K * 2>(k, lane);
+}
+
+__device__ void build_table_wave2(const uint32_t *hist, const uint32_t *extra, HuffCode *hc, uint32_t *ehuf,
+                                  TabScratch2 *S, int lane, int *err, unsigned long long *tm = nullptr) {
+  TAB_T(0);
+  uint32_t f[5];
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const int s = lane + 64 * i;
+    f[i] = s < 256 ? hist[s] : (s == 256 ? 1u : 0u);  // :364-367
+    if (extra && i == 0 && lane < 16) f[i] += extra[lane];
+    if (s < 257) S->scl[s] = 0;
+  }
+  TAB_T(1);
+  // leaves: symbols 0..255 with a count, ascending; symbol 256 (count 1, the
+  // highest index) is the least key of all and heads the queue
+  unsigned long long k[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++)
+    k[r] = f[r] ? ((unsigned long long)f[r] << 32) | ((unsigned long long)(256 - (lane + 64 * r)) << 19) | (1ull << 10)
+                : ~0ull;
+  bsort_level<2>(k, lane);
+  int nl = 1;
+#pragma unroll
+  for (int r = 0; r < 4; r++) nl += __popcll(__ballot(f[r] != 0));
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int q = 1 + lane + 64 * r;
+    S->ql[q] = k[r] == ~0ull ? ~0ull : k[r] | (unsigned)q;
+  }
+  if (lane == 0) S->ql[0] = (1ull << 32) | (1ull << 10);
+  S->ql[257 + lane] = ~0ull;
+#pragma unroll
+  for (int i = 0; i < 5; i++)
+    if (lane + 64 * i < 320) S->qm[lane + 64 * i] = ~0ull;
+  wave_lds_sync();
+  TAB_T(2);
+  // the merges (encoder.c:196-226) on uniform values; v1 = the least key, v2
+  // the next; K = the merged node, queued at its key's place
+  // (keys as two 32-bit words -- freq, then label | leaves | node -- so the
+  // uniform compares stay on the scalar unit)
+  int lw = 0, mw = 0, lh = 0, mh = 0, mt = 0;
+  uint32_t wlh, wll, wmh = ~0u, wml = ~0u;
+  {
+    const unsigned long long v = S->ql[lane];
+    wlh = (uint32_t)(v >> 32);
+    wll = (uint32_t)v;
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  }
+  uint32_t mlh = 0, mll = 0;  // the last appended key
+  int root_label = 256;
+  uint32_t total = 1;
+  for (int step = 0; step + 1 < nl; step++) {
+    // (window reloads wait for their loads inside the branch, so the common
+    // path never waits for lane 0's queue and tree stores)
+    if (lh + 1 - lw > 63) {
+      lw = lh;
+      const unsigned long long v = S->ql[lw + lane];
+      wlh = (uint32_t)(v >> 32);
+      wll = (uint32_t)v;
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    }
+    if (mh + 1 - mw > 63) {
+      mw = mh;
+      const unsigned long long v = S->qm[mw + lane];
+      wmh = (uint32_t)(v >> 32);
+      wml = (uint32_t)v;
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+    }
+    const int il = lh - lw, im = mh - mw;
+    const uint32_t ah = __builtin_amdgcn_readlane(wlh, il), al = __builtin_amdgcn_readlane(wll, il);
+    const uint32_t bh = __builtin_amdgcn_readlane(wlh, il + 1), bl = __builtin_amdgcn_readlane(wll, il + 1);
+    const uint32_t ch = __builtin_amdgcn_readlane(wmh, im), cl0 = __builtin_amdgcn_readlane(wml, im);
+    const uint32_t dh = __builtin_amdgcn_readlane(wmh, im + 1), dl = __builtin_amdgcn_readlane(wml, im + 1);
+    const bool ac = ah < ch || (ah == ch && al < cl0);
+    const uint32_t k1h = ac ? ah : ch, k1l = ac ? al : cl0;
+    const uint32_t xh = ac ? bh : ah, xl = ac ? bl : al, yh = ac ? ch : dh, yl = ac ? cl0 : dl;
+    const bool bx = xh < yh || (xh == yh && xl < yl);
+    const uint32_t k2h = bx ? xh : yh, k2l = bx ? xl : yl;
+    const int dlh = ac ? (bx ? 2 : 1) : (bx ? 1 : 0);
+    lh += dlh;
+    mh += 2 - dlh;
+    const int lab1 = (int)(k1l >> 19);  // 256 - v1
+    const uint32_t fs = k1h + k2h;
+    const int sz1 = (int)((k1l >> 10) & 511), sz2 = (int)((k2l >> 10) & 511);
+    const int c1 = (int)(k1l & 1023), c2 = (int)(k2l & 1023), node = nl + step;
+    const uint32_t Kh = fs, Kl = ((uint32_t)lab1 << 19) | ((uint32_t)(sz1 + sz2) << 10) | (uint32_t)node;
+    if (lane == 0) {
+      S->par[c1] = node;
+      S->par[c2] = node;
+      S->off[c1] = 0;
+      S->off[c2] = sz1;  // v2's chain follows v1's (:223-226)
+    }
+    const unsigned long long K = ((unsigned long long)Kh << 32) | Kl;
+    if (mt > mh && (mlh > Kh || (mlh == Kh && mll > Kl))) {
+      // (rare) an equal-count node with a smaller key is queued: insert
+      int pos = mt;
+      wave_lds_sync();
+      while (pos > mh && S->qm[pos - 1] > K) {
+        if (lane == 0) S->qm[pos] = S->qm[pos - 1];
+        wave_lds_sync();
+        pos--;
+      }
+      if (lane == 0) S->qm[pos] = K;
+      wave_lds_sync();
+      mw = mh;
+      const unsigned long long v = S->qm[mw + lane];
+      wmh = (uint32_t)(v >> 32);
+      wml = (uint32_t)v;
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+    } else {
+      if (lane == 0) S->qm[mt] = K;
+      if (lane == mt - mw) {
+        wmh = Kh;
+        wml = Kl;
+      }
+      mlh = Kh;
+      mll = Kl;
+    }
+    mt++;
+    root_label = 256 - lab1;
+    total = fs;
+  }
+  const int nn = 2 * nl - 1, root = nn - 1;
+  if (lane == 0) {
+    S->par[root] = 0xFFFF;
+    S->off[root] = 0;
+  }
+  wave_lds_sync();
+  TAB_T(3);
+  // depth and chain place of every node: pointer jumping to the root
+  {
+    int pp[9], dd[9], oo[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      const int nd = lane + 64 * i;
+      pp[i] = 0xFFFF;
+      dd[i] = 0;
+      oo[i] = 0;
+      if (64 * i < nn && nd < nn) {
+        pp[i] = S->par[nd];
+        oo[i] = S->off[nd];
+        dd[i] = pp[i] != 0xFFFF;
+        S->dep[nd] = dd[i];
+      }
+    }
+    wave_lds_sync();
+    for (int round = 0; round < 10; round++) {
+      bool more = false;
+#pragma unroll
+      for (int i = 0; i < 9; i++) more |= pp[i] != 0xFFFF;
+      if (!__ballot(more)) break;
+      int nd2[9], no2[9], np2[9];
+#pragma unroll
+      for (int i = 0; i < 9; i++) {
+        nd2[i] = dd[i];
+        no2[i] = oo[i];
+        np2[i] = pp[i];
+        if (64 * i < nn && pp[i] != 0xFFFF) {
+          nd2[i] += S->dep[pp[i]];
+          no2[i] += S->off[pp[i]];
+          np2[i] = S->par[pp[i]];
+        }
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int i = 0; i < 9; i++) {
+        const int nd = lane + 64 * i;
+        dd[i] = nd2[i];
+        oo[i] = no2[i];
+        pp[i] = np2[i];
+        if (64 * i < nn && nd < nn) {
+          S->dep[nd] = dd[i];
+          S->off[nd] = oo[i];
+          S->par[nd] = pp[i];
+        }
+      }
+      wave_lds_sync();
+    }
+    // leaves (nodes 0..nl-1): their symbols' lengths and chain places
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      const int q = lane + 64 * i;
+      if (q < nl && nl > 1) {
+        const int sy = 256 - (int)((S->ql[q] >> 19) & 511);
+        S->scl[sy] = dd[i];
+        S->spos[sy] = oo[i];
+        S->seq[oo[i]] = sy;
+      }
+    }
+  }
+  wave_lds_sync();
+  TAB_T(4);
+  int cl[5];
+  int bad = 0, maxl = 0;
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const int s = lane + 64 * i;
+    cl[i] = 0;
+    if (s < 257) {
+      cl[i] = S->scl[s];
+      const bool in = cl[i] > 0;
+      const int nx = in && S->spos[s] + 1 < nl ? S->seq[S->spos[s] + 1] : -1;
+      hc->sym_freq[s] = in ? (s == root_label ? (int)total : 0) : (int)f[i];  // :221-222
+      hc->code_len[s] = cl[i];
+      hc->next[s] = nx;
+      if (cl[i] >= 32) bad = 1;  // the reference indexes code_len_freq out of bounds
+      maxl = max(maxl, cl[i]);
+    }
+  }
+  if (__ballot(bad)) {
+    if (lane == 0) *err = 1;
+    return;
+  }
+  for (int o = 32; o; o >>= 1) maxl = max(maxl, __shfl_xor(maxl, o));
+  // code_len_freq (all 257 symbols) and counts of 0..255, length L in lane L
+  int clf = 0, cnt = 0;
+  for (int L = 1; L <= maxl; L++) {
+    int c = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) c += __popcll(__ballot(cl[i] == L));
+    const int c256 = __popcll(__ballot(lane == 0 && cl[4] == L));
+    if (lane == L) {
+      clf = c + c256;
+      cnt = c;
+    }
+  }
+  int nlc = clf;
+  for (int o = 32; o; o >>= 1) nlc += __shfl_xor(nlc, o);
+  bool fail = nlc < 2;
+  if (!fail) {
+    // :239-259 limit to 16 bits
+    int i = 31;
+    for (int guard = 0; guard < 4096; guard++) {
+      if (__builtin_amdgcn_readlane(clf, i) > 0) {
+        const unsigned long long m = __ballot(clf > 0) & ((1ull << (i - 1)) - 1ull);
+        if (!m) {
+          fail = true;
+          break;
+        }
+        const int j = 63 - __clzll(m);
+        clf += (lane == i ? -2 : 0) + (lane == i - 1 ? 1 : 0) + (lane == j + 1 ? 2 : 0) + (lane == j ? -1 : 0);
+        continue;
+      }
+      i--;
+      if (i != 16) continue;
+      const unsigned long long m = __ballot(clf != 0) & ((1ull << 17) - 1ull);
+      i = 63 - __clzll(m);
+      clf -= lane == i ? 1 : 0;
+      break;
+    }
+  }
+  const int cum = (int)wave_scan64((uint32_t)(lane <= 16 ? clf : 0));
+  const int basev = (int)wave_scan64((uint32_t)cnt) - cnt;
+  int n = cnt;
+  for (int o = 32; o; o >>= 1) n += __shfl_xor(n, o);
+  if (!fail && (__builtin_amdgcn_readlane(cum, 16) != n || n >= 255)) fail = true;
+  if (fail) {
+    if (lane == 0) *err = 1;
+    return;
+  }
+  // :280-300 canonical first codes, length L in lane L
+  int fc = 0;
+  {
+    int code = 0, started = 0;
+    for (int L = 1; L <= 16; L++) {
+      if (started) code <<= 1;
+      if (lane == L) fc = code;
+      const int cL = __builtin_amdgcn_readlane(clf, L);
+      if (cL) started = 1;
+      code += cL;
+    }
+  }
+  TAB_T(5);
+  // :262-268 order symbols 0..255 by (unlimited length, value)
+  {
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (int L = 1; L <= maxl; L++) {
+      int at = __builtin_amdgcn_readlane(basev, L);
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const unsigned long long m = __ballot(cl[r] == L);
+        if (cl[r] == L) S->sorted[at + __popcll(m & lt)] = lane + 64 * r;
+        at += __popcll(m);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    S->slen[lane + 64 * r] = 0;
+    S->scode[lane + 64 * r] = -1;
+  }
+  wave_lds_sync();
+  TAB_T(6);
+#pragma unroll
+  for (int r = 0; r < 4; r++) {  // :271-276 and :280-300
+    const int kk = lane + 64 * r;
+    int L = 1;
+    for (int l = 1; l <= 16; l++) L += __builtin_amdgcn_readlane(cum, l) <= kk ? 1 : 0;
+    L = min(L, 16);
+    // (lane reads with every lane active: an inactive source lane reads 0)
+    const int code = __shfl(fc, L) + (kk - __shfl(cum, L - 1));
+    if (kk < n) {
+      const int sy = S->sorted[kk];
+      S->slen[sy] = L;
+      S->scode[sy] = code;
+    }
+  }
+  wave_lds_sync();
+  if (lane < 32) hc->code_len_freq[lane] = clf;
+  for (int kk = lane; kk < 256; kk += 64) {
+    // sym_sorted: -1 past the end, except that the sentinel write of :277
+    // lands in sym_sorted[255] (it aliases sym_code_len[-1], structs.h:10-11)
+    hc->sym_sorted[kk] = kk < n ? S->sorted[kk] : (kk == 255 ? 0 : -1);
+    const int L = S->slen[kk];
+    hc->sym_code_len[kk] = L;
+    hc->sym_code[kk] = S->scode[kk];
+    ehuf[kk] = L ? ((uint32_t)L << 16) | (uint32_t)S->scode[kk] : 0u;
+  }
+  TAB_T(7);
 }
 
 // With a.seg_dc the DC-table waves (0, 2) first compute the segments' first
@@ -1912,22 +2400,29 @@ __device__ void build_table_wave(const uint32_t *hist, const uint32_t *extra, Hu
 // each, 32 segments in flight per lane) while the AC-table waves, the long
 // pole (~160 symbols to merge against <= 12), already build theirs.
 __global__ __launch_bounds__(256) void k_tables(EntArgs a) {
+#if MIJ_TAB_QUEUE == 2
+  __shared__ TabScratch2 S[4];
+#else
   __shared__ TabScratch S[4];
+#endif
   __shared__ uint32_t h[2][16];
+  __shared__ uint32_t hs[32 * 32];  // seg_dc_store's spread counters
   __shared__ int s_done;
   const int f = blockIdx.x, t = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#ifdef MIJ_K1_DIAG
+  if (a.dbg && lane == 0) a.dbg[((long long)f * 4 + t) * 10 + 8] = __builtin_amdgcn_s_memtime();
+#endif
   const uint32_t *extra = nullptr;
-  if (a.seg_dc && t == 0) {
-    if (lane < 32) (&h[0][0])[lane] = 0;
-    if (lane == 0) s_done = 0;
+  if (a.seg_dc) {
+    for (int i = threadIdx.x; i < 32 * 32; i += 256) hs[i] = 0;
+    if (threadIdx.x == 0) s_done = 0;
   }
   __syncthreads();
   if (a.seg_dc && !(t & 1)) {
-    uint32_t(*hh)[16] = h;
     const FGeom fg = frame_geom(a.g, a.fdims, f);
     const int half = (a.g.nseg + 1) / 2;
     const int sb = t == 0 ? 0 : half, se = t == 0 ? half : a.g.nseg;
-    constexpr int U = 32;  // segments in flight per lane
+    constexpr int U = MIJ_SEGDC_U;  // segments in flight per lane
     for (int s0 = sb + lane; s0 < se; s0 += 64 * U) {
       SegDc r[U];
 #pragma unroll
@@ -1936,17 +2431,34 @@ __global__ __launch_bounds__(256) void k_tables(EntArgs a) {
         r[u] = s < se ? seg_dc_load(a, fg, f, s) : SegDc{0, 0, 0, false};
       }
 #pragma unroll
-      for (int u = 0; u < U; u++) seg_dc_store(a, f, s0 + 64 * u, r[u], hh);
+      for (int u = 0; u < U; u++) seg_dc_store(a, f, s0 + 64 * u, r[u], hs, lane);
     }
+#ifdef MIJ_K1_DIAG
+    if (a.dbg && lane == 0) a.dbg[((long long)f * 4 + t) * 10 + 9] = __builtin_amdgcn_s_memtime();
+#endif
     // both DC waves' counts are in before either builds its table
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) atomicAdd(&s_done, 1);
     while (__hip_atomic_load(&s_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 2)
       __builtin_amdgcn_s_sleep(2);
+    // this wave's component: the 32 copies of its 16 counters summed
+    if (lane < 16) {
+      const int key = (t >> 1) * 16 + lane;
+      uint32_t v = 0;
+      for (int c = 0; c < 32; c++) v += hs[key * 32 + ((c + lane) & 31)];
+      h[t >> 1][lane] = v;
+    }
+    wave_lds_sync();
     extra = h[t >> 1];
   }
-  build_table_wave(a.hist + ((long long)f * 4 + t) * 257, extra, (HuffCode *)a.hc + (long long)f * 4 + t,
-                   (uint32_t *)a.ehuf + ((long long)f * 4 + t) * 256, &S[t], lane, a.err + f);
+#if MIJ_TAB_QUEUE == 2
+  build_table_wave2(
+#else
+  build_table_wave(
+#endif
+                   a.hist + ((long long)f * 4 + t) * 257, extra, (HuffCode *)a.hc + (long long)f * 4 + t,
+                   (uint32_t *)a.ehuf + ((long long)f * 4 + t) * 256, &S[t], lane, a.err + f,
+                   a.dbg ? a.dbg + ((long long)f * 4 + t) * 10 : nullptr);
 }
 
 // code tables from caller-owned huff_code structs (drop-in write_jpg)
