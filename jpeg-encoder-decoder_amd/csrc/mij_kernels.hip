@@ -2030,6 +2030,84 @@ __device__ __forceinline__ unsigned long long flip_fetch(unsigned long long x, i
 __device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsigned long long b) { return a < b ? a : b; }
 __device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a < b ? b : a; }
 
+// 32-bit partners for the narrow-key sort
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+template <int J>
+__device__ __forceinline__ uint32_t xor_fetch32(uint32_t x, int lane) {
+  if constexpr (J == 1) return dpp32<0xB1>(x);
+  else if constexpr (J == 2) return dpp32<0x4E>(x);
+  else if constexpr (J == 4) {
+    // (both moves with every lane active: a DPP under a lane branch reads 0
+    // from the inactive lanes)
+    const uint32_t up = dpp32<0x12C>(x), dn = dpp32<0x124>(x);
+    return (lane & 4) ? dn : up;
+  }
+  else if constexpr (J == 8) return dpp32<0x128>(x);
+  else if constexpr (J == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return (lane & 16) ? r[0] : r[1];
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return (lane & 32) ? r[0] : r[1];
+  }
+}
+template <int K>
+__device__ __forceinline__ uint32_t flip_fetch32(uint32_t x, int lane) {
+  if constexpr (K == 2) return dpp32<0xB1>(x);
+  else if constexpr (K == 4) return dpp32<0x1B>(x);
+  else if constexpr (K == 8) return dpp32<0x141>(x);
+  else if constexpr (K == 16) return dpp32<0x140>(x);
+  else if constexpr (K == 32) return dpp32<0x140>(xor_fetch32<16>(x, lane));
+  else return flip_fetch32<32>(xor_fetch32<32>(x, lane), lane);
+}
+__device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint32_t umax32(uint32_t a, uint32_t b) { return a < b ? b : a; }
+template <int J>
+__device__ __forceinline__ void bsort_half32(uint32_t (&k)[4], int lane) {
+  if constexpr (J >= 64) {
+    constexpr int R = J / 64;
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      if (!(r & R)) {
+        const uint32_t x = k[r], y = k[r | R];
+        k[r] = umin32(x, y);
+        k[r | R] = umax32(x, y);
+      }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const uint32_t p = xor_fetch32<J>(k[r], lane);
+      k[r] = (lane & J) ? umax32(k[r], p) : umin32(k[r], p);
+    }
+  }
+  if constexpr (J > 1) bsort_half32<J / 2>(k, lane);
+}
+template <int K>
+__device__ __forceinline__ void bsort_level32(uint32_t (&k)[4], int lane) {
+  if constexpr (K <= 64) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const uint32_t p = flip_fetch32<K>(k[r], lane);
+      k[r] = (lane & (K / 2)) ? umax32(k[r], p) : umin32(k[r], p);
+    }
+  } else {
+    constexpr int X = K / 64 - 1;
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      if (r < (r ^ X)) {
+        const int q = r ^ X;
+        const uint32_t mr = flip_fetch32<64>(k[r], lane), mq = flip_fetch32<64>(k[q], lane);
+        k[r] = umin32(k[r], mq);
+        k[q] = umax32(k[q], mr);
+      }
+  }
+  if constexpr (K >= 4) bsort_half32<K / 4>(k, lane);
+  if constexpr (K < 256) bsort_level32<K * 2>(k, lane);
+}
+
 // ascending bitonic sort of 256 keys, element e = lane + 64 r in k[r]
 template <int J>
 __device__ __forceinline__ void bsort_half(unsigned long long (&k)[4], int lane) {
@@ -2090,11 +2168,31 @@ __device__ void build_table_wave2(const uint32_t *hist, const uint32_t *extra, H
   // leaves: symbols 0..255 with a count, ascending; symbol 256 (count 1, the
   // highest index) is the least key of all and heads the queue
   unsigned long long k[4];
+  bool wide = false;
 #pragma unroll
-  for (int r = 0; r < 4; r++)
-    k[r] = f[r] ? ((unsigned long long)f[r] << 32) | ((unsigned long long)(256 - (lane + 64 * r)) << 19) | (1ull << 10)
-                : ~0ull;
-  bsort_level<2>(k, lane);
+  for (int r = 0; r < 4; r++) wide |= f[r] >= (1u << 23);
+#ifndef MIJ_TAB_SORT32
+#define MIJ_TAB_SORT32 1
+#endif
+  if (!MIJ_TAB_SORT32 || __ballot(wide)) {
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      k[r] = f[r] ? ((unsigned long long)f[r] << 32) | ((unsigned long long)(256 - (lane + 64 * r)) << 19) | (1ull << 10)
+                  : ~0ull;
+    bsort_level<2>(k, lane);
+  } else {
+    // counts below 2^23 (every frame up to 8K at Q=50): the same order on
+    // 32-bit keys (count << 9 | 256 - symbol), half the partner moves
+    uint32_t k32[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) k32[r] = f[r] ? (f[r] << 9) | (uint32_t)(256 - (lane + 64 * r)) : ~0u;
+    bsort_level32<2>(k32, lane);
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      k[r] = k32[r] == ~0u ? ~0ull
+                           : ((unsigned long long)(k32[r] >> 9) << 32) | ((unsigned long long)(k32[r] & 511) << 19) |
+                                 (1ull << 10);
+  }
   int nl = 1;
 #pragma unroll
   for (int r = 0; r < 4; r++) nl += __popcll(__ballot(f[r] != 0));
@@ -2267,7 +2365,7 @@ __device__ void build_table_wave2(const uint32_t *hist, const uint32_t *extra, H
   wave_lds_sync();
   TAB_T(4);
   int cl[5];
-  int bad = 0, maxl = 0;
+  int bad = 0;
 #pragma unroll
   for (int i = 0; i < 5; i++) {
     const int s = lane + 64 * i;
@@ -2280,17 +2378,18 @@ __device__ void build_table_wave2(const uint32_t *hist, const uint32_t *extra, H
       hc->code_len[s] = cl[i];
       hc->next[s] = nx;
       if (cl[i] >= 32) bad = 1;  // the reference indexes code_len_freq out of bounds
-      maxl = max(maxl, cl[i]);
     }
   }
   if (__ballot(bad)) {
     if (lane == 0) *err = 1;
     return;
   }
-  for (int o = 32; o; o >>= 1) maxl = max(maxl, __shfl_xor(maxl, o));
-  // code_len_freq (all 257 symbols) and counts of 0..255, length L in lane L
-  int clf = 0, cnt = 0;
-  for (int L = 1; L <= maxl; L++) {
+  // code_len_freq (all 257 symbols) and counts of 0..255, length L in lane L;
+  // the nl leaves (nl - 1 of them symbols 0..255) are all counted by the
+  // longest length
+  int clf = 0, cnt = 0, maxl = 0;
+  const int nlc = nl > 1 ? nl : 0;
+  for (int L = 1, seen = 0; seen < nlc && L < 32; L++) {
     int c = 0;
 #pragma unroll
     for (int i = 0; i < 4; i++) c += __popcll(__ballot(cl[i] == L));
@@ -2299,9 +2398,9 @@ __device__ void build_table_wave2(const uint32_t *hist, const uint32_t *extra, H
       clf = c + c256;
       cnt = c;
     }
+    seen += c + c256;
+    maxl = L;
   }
-  int nlc = clf;
-  for (int o = 32; o; o >>= 1) nlc += __shfl_xor(nlc, o);
   bool fail = nlc < 2;
   if (!fail) {
     // :239-259 limit to 16 bits
@@ -2327,8 +2426,7 @@ __device__ void build_table_wave2(const uint32_t *hist, const uint32_t *extra, H
   }
   const int cum = (int)wave_scan64((uint32_t)(lane <= 16 ? clf : 0));
   const int basev = (int)wave_scan64((uint32_t)cnt) - cnt;
-  int n = cnt;
-  for (int o = 32; o; o >>= 1) n += __shfl_xor(n, o);
+  const int n = nlc ? nlc - 1 : 0;  // symbols 0..255 with a code
   if (!fail && (__builtin_amdgcn_readlane(cum, 16) != n || n >= 255)) fail = true;
   if (fail) {
     if (lane == 0) *err = 1;
