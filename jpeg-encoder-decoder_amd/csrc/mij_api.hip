@@ -991,7 +991,12 @@ extern "C" int mij_batch_set_overlap(mij_batch *b, int nsub) {
   if (nsub < 1 || nsub > 16) return fail(MIJ_EINVAL, "set_overlap: 1..16 sub-batches");
   HIP_TRY(hipSetDevice(b->dev));
   if (nsub > 1 && !b->stream2) {
-    HIP_TRY(hipStreamCreateWithFlags(&b->stream2, hipStreamNonBlocking));
+    // the entropy stream at the highest priority: its small workgroups take
+    // the CU room the running K1 leaves before the next K1's do
+    int lo = 0, hi = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    static const int prio_env = getenv("MIJ_OVERLAP_PRIO") ? atoi(getenv("MIJ_OVERLAP_PRIO")) : 1;  // A/B
+    HIP_TRY(hipStreamCreateWithPriority(&b->stream2, hipStreamNonBlocking, prio_env ? hi : lo));
     for (auto &e : b->ov_k1) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&b->ov_done, hipEventDisableTiming));
   }

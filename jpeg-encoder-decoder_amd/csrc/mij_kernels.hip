@@ -1503,12 +1503,17 @@ __device__ __forceinline__ void seg_dc_store(const EntArgs &a, int f, int s, con
   atomicAdd(&hs[((r.comp ? 16 : 0) + cls) * 32 + (lane & 31)], 1u);
 }
 
-__global__ __launch_bounds__(256) void k_seg_dc(EntArgs a) {
+#ifndef MIJ_SEGDC_WG
+#define MIJ_SEGDC_WG 256
+#endif
+// (MIJ_SEGDC_WG 64: one-wave workgroups, which fit beside a running 10-wave
+// K1 -- 256-thread ones wait for it to end; profiles/r03/overlap_trace.txt)
+__global__ __launch_bounds__(MIJ_SEGDC_WG) void k_seg_dc(EntArgs a) {
   __shared__ uint32_t hs[32 * 32];
-  const int per = (a.g.nseg + 255) / 256;
+  const int per = (a.g.nseg + MIJ_SEGDC_WG - 1) / MIJ_SEGDC_WG;
   const int f = blockIdx.x / per;
-  const int s = (blockIdx.x - f * per) * 256 + threadIdx.x;
-  for (int i = threadIdx.x; i < 32 * 32; i += 256) hs[i] = 0;
+  const int s = (blockIdx.x - f * per) * MIJ_SEGDC_WG + threadIdx.x;
+  for (int i = threadIdx.x; i < 32 * 32; i += MIJ_SEGDC_WG) hs[i] = 0;
   __syncthreads();
   if (s < a.g.nseg) seg_dc_store(a, f, s, seg_dc_load(a, frame_geom(a.g, a.fdims, f), f, s), hs, threadIdx.x & 63);
   __syncthreads();
@@ -2558,6 +2563,22 @@ __global__ __launch_bounds__(256) void k_tables(EntArgs a) {
                    (uint32_t *)a.ehuf + ((long long)f * 4 + t) * 256, &S[t], lane, a.err + f,
                    a.dbg ? a.dbg + ((long long)f * 4 + t) * 10 : nullptr);
 }
+
+#if MIJ_TAB_QUEUE == 2
+// The same tables one wave (workgroup) per table when the segment DCs ran on
+// their own (k_seg_dc): 14 KB of LDS per workgroup instead of 61 KB, so the
+// tables of one sub-batch fit beside the next sub-batch's K1 (overlap path).
+__global__ __launch_bounds__(64) void k_tables_1w(EntArgs a) {
+  __shared__ TabScratch2 S;
+  const int f = blockIdx.x >> 2, t = blockIdx.x & 3, lane = threadIdx.x;
+#ifdef MIJ_K1_DIAG
+  if (a.dbg && lane == 0) a.dbg[((long long)f * 4 + t) * 10 + 8] = __builtin_amdgcn_s_memtime();
+#endif
+  build_table_wave2(a.hist + ((long long)f * 4 + t) * 257, nullptr, (HuffCode *)a.hc + (long long)f * 4 + t,
+                    (uint32_t *)a.ehuf + ((long long)f * 4 + t) * 256, &S, lane, a.err + f,
+                    a.dbg ? a.dbg + ((long long)f * 4 + t) * 10 : nullptr);
+}
+#endif
 
 // code tables from caller-owned huff_code structs (drop-in write_jpg)
 __global__ void k_ehuf_struct(const HuffCode *hc, uint32_t *ehuf) {
@@ -3670,7 +3691,8 @@ hipError_t launch_k1(const K1Args &a, int grid, int mode, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t launch_seg_dc(const EntArgs &a, hipStream_t s) {
-  hipLaunchKernelGGL(k_seg_dc, dim3(a.nframes * ((a.g.nseg + 255) / 256)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_seg_dc, dim3(a.nframes * ((a.g.nseg + MIJ_SEGDC_WG - 1) / MIJ_SEGDC_WG)), dim3(MIJ_SEGDC_WG),
+                     0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_dc_diff(int16_t *coef, const int16_t *dc, const Geom &g, int nframes,
@@ -3681,6 +3703,12 @@ hipError_t launch_dc_diff(int16_t *coef, const int16_t *dc, const Geom &g, int n
   return hipGetLastError();
 }
 hipError_t launch_tables(const EntArgs &a, hipStream_t s) {
+#if MIJ_TAB_QUEUE == 2
+  if (!a.seg_dc) {
+    hipLaunchKernelGGL(k_tables_1w, dim3(a.nframes * 4), dim3(64), 0, s, a);
+    return hipGetLastError();
+  }
+#endif
   hipLaunchKernelGGL(k_tables, dim3(a.nframes), dim3(256), 0, s, a);
   return hipGetLastError();
 }
