@@ -167,11 +167,25 @@ def run_config4(args, world, rank, local, dist):
         torch.cuda.synchronize()
         phases = {ev[i][0]: round(ev[i - 1][1].elapsed_time(ev[i][1]), 4) for i in range(1, len(ev))}
     el, _ = sharding.reduce_timing(el, 0, dist, dist_device(dist, local))
-    verified = 0
+    verified = golden = 0
     if rank == 0 and args.verify:
+        import hashlib
         import oracle as O
+        # config4_frame0/1 also against the reference build's sha256
+        # (tests/golden/manifest.json, oracle/gen_golden.py)
+        man = {}
+        mpath = os.path.join(REPO, "tests", "golden", "manifest.json")
+        if args.quality == 50 and os.path.exists(mpath):
+            with open(mpath) as fh:
+                man = json.load(fh)["cases"]
         for f in range(n if args.verify < 0 else min(args.verify, n)):
-            if full.output(f) != O.cref_encode(frames[f % distinct], args.quality):
+            out = full.output(f)
+            want = man.get(f"config4_frame{f % distinct}")
+            if want is not None:
+                if (len(out), hashlib.sha256(out).hexdigest()) != (want["jpg_len"], want["jpg_sha256"]):
+                    raise SystemExit(f"bench config4: frame {f} differs from the reference's sha256")
+                golden += 1
+            elif out != O.cref_encode(frames[f % distinct], args.quality):
                 raise SystemExit(f"bench config4: frame {f} differs from the oracle")
             verified += 1
     px = W * H * n * args.steps
@@ -190,6 +204,7 @@ def run_config4(args, world, rank, local, dist):
                    "backend": dist.get_backend() if dist is not None else "none",
                    "protocol": "device-resident (mij_band_*_async)" if on_dev else "host arrays (gloo)"},
         "verified_frames": verified,
+        "verified_against_reference_sha": golden,
     }
     if phases:
         res["phases_ms"] = phases

@@ -28,7 +28,7 @@ hipError_t launch_tables(const EntArgs &a, hipStream_t s);
 hipError_t launch_ehuf_struct(const HuffCode *hc, uint32_t *ehuf, hipStream_t s);
 hipError_t launch_bits(const EntArgs &a, hipStream_t s);
 hipError_t launch_scan(const EntArgs &a, hipStream_t s);
-hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s);
+hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s, bool state_zeroed = false);
 hipError_t launch_emit(const EntArgs &a, hipStream_t s);
 hipError_t launch_or_words(uint32_t *dst, const uint32_t *src, long long n, hipStream_t s);
 hipError_t launch_move_pieces(uint32_t *raw, const Geom &g, uint32_t *dst,
@@ -41,8 +41,7 @@ hipError_t launch_gather_regions(uint8_t *dst, long long slot_bytes, int pitch, 
                                  hipStream_t s);
 hipError_t launch_mfma_probe(const int4 *A, const int4 *B, int4 *D, hipStream_t s);
 hipError_t launch_band_last(const int16_t *dc, const Geom &g, int n, int16_t *last, hipStream_t s);
-hipError_t launch_band_bound(const uint32_t *hist, const uint32_t *ehuf, int n, unsigned long long *acc,
-                             unsigned long long *bound, hipStream_t s);
+hipError_t launch_band_bound(const EntArgs &a, unsigned long long *acc, unsigned long long *bound, hipStream_t s);
 hipError_t launch_band_count(const unsigned long long *scan_bits, int n, unsigned long long *pieces,
                              unsigned long long *bits, hipStream_t s);
 hipError_t launch_or_shift_pieces(uint32_t *raw, const Geom &g, const uint32_t *src,
@@ -549,12 +548,12 @@ static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0, bool band = false
   // 16 on large low-Q batches (emit 0.247 -> 0.232 ms at config 3, Q=50),
   // 64 otherwise (Q=90: 0.62 at 64 against 0.68 at 16; a single frame needs
   // the width)
-  // 256 on frames of 8 Mpixels and more (config 4: few scans of hundreds of
+  // 512 on frames of 8 Mpixels and more (config 4: few scans of hundreds of
   // chunks each)
   static const int slots_env = getenv("MIJ_EMIT_SLOTS") ? atoi(getenv("MIJ_EMIT_SLOTS")) : 0;  // A/B
   a.emit_slots = slots_env > 0                           ? slots_env
                  : (nframes >= 43 && b->quality <= 60)   ? 16
-                 : ((long long)b->g.w * b->g.h >= (8 << 20)) ? 256
+                 : ((long long)b->g.w * b->g.h >= (8 << 20)) ? 512
                                                            : 64;
   if (f0) {  // sub-batch: frames f0.. of the batch (every per-frame array shifted)
     const Geom &g = b->g;
@@ -1526,7 +1525,7 @@ extern "C" int mij_band_tables_async(mij_batch *b, int n, const uint32_t *d_ghis
     HIP_TRY(dalloc(&b->d_bound_acc, 2));
     HIP_TRY(hipMemsetAsync(b->d_bound_acc, 0, 2 * sizeof(unsigned long long), b->stream));
   }
-  HIP_TRY(launch_band_bound(b->d_hist, b->d_ehuf, n, b->d_bound_acc, (unsigned long long *)d_bound, b->stream));
+  HIP_TRY(launch_band_bound(ent_args(b, n), b->d_bound_acc, (unsigned long long *)d_bound, b->stream));
   b->band_async_n = -n;  // tables built, not packed yet
   return MIJ_OK;
 }
@@ -1540,7 +1539,7 @@ extern "C" int mij_band_pack_async(mij_batch *b, int n, uint64_t *d_bits) {
   if (b->raw_dirty) HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->raw_dirty * b->g.raw_fs, b->stream));
   b->raw_dirty = n;
   EntArgs a = ent_args(b, n);
-  HIP_TRY(launch_pack_lb(a, b->stream));
+  HIP_TRY(launch_pack_lb(a, b->stream, true));  // (k_band_bound zeroed its state)
   HIP_TRY(launch_band_count((const unsigned long long *)b->d_scan_bits, n, b->d_pieces,
                             (unsigned long long *)d_bits, b->stream));
   b->band_async_n = n;

@@ -3539,8 +3539,15 @@ __global__ void k_band_assembly(const unsigned long long *allbits, int world, in
 // frame; the workgroups' sums meet in acc = {sum, arrivals}, which the last
 // workgroup to arrive reads, writes to bound[0] and leaves zeroed.
 __global__ __launch_bounds__(256) void k_band_bound(const uint32_t *hist, const uint32_t *ehuf, int n,
-                                                    unsigned long long *acc, unsigned long long *bound) {
+                                                    unsigned long long *acc, unsigned long long *bound,
+                                                    unsigned long long *pack_state, long long nstate,
+                                                    unsigned *pack_ticket) {
   __shared__ unsigned long long s_w[4];
+  // (k_pack_lb's look-back words and tickets zeroed here, saving two fills
+  // on the band stream's critical path)
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nstate; i += (long long)gridDim.x * 256)
+    pack_state[i] = 0;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < 3 * n; i += gridDim.x * 256) pack_ticket[i] = 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, f = blockIdx.x * 4 + w;
   unsigned long long words = 0;
   if (f < n) {
@@ -3754,9 +3761,12 @@ hipError_t launch_band_last(const int16_t *dc, const Geom &g, int n, int16_t *la
   hipLaunchKernelGGL(k_band_last, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, dc, g, n, last);
   return hipGetLastError();
 }
-hipError_t launch_band_bound(const uint32_t *hist, const uint32_t *ehuf, int n, unsigned long long *acc,
-                             unsigned long long *bound, hipStream_t s) {
-  hipLaunchKernelGGL(k_band_bound, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, hist, ehuf, n, acc, bound);
+hipError_t launch_band_bound(const EntArgs &a, unsigned long long *acc, unsigned long long *bound, hipStream_t s) {
+  const int n = a.nframes;
+  const long long nstate = (long long)n * ((a.g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((a.g.nsc + PACK_SEGS - 1) / PACK_SEGS));
+  const unsigned grid = (unsigned)std::max((n + 3) / 4, (int)std::min<long long>((nstate + 255) / 256, 64));
+  hipLaunchKernelGGL(k_band_bound, dim3(grid), dim3(256), 0, s, a.hist, a.ehuf, n, acc, bound, a.pack_state, nstate,
+                     a.pack_ticket);
   return hipGetLastError();
 }
 hipError_t launch_band_count(const unsigned long long *scan_bits, int n, unsigned long long *pieces,
@@ -3778,12 +3788,14 @@ hipError_t launch_or_shift_pieces(uint32_t *raw, const Geom &g, const uint32_t *
   return hipGetLastError();
 }
 
-hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s) {
+hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s, bool state_zeroed) {
   const int gy = (a.g.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (a.g.nsc + PACK_SEGS - 1) / PACK_SEGS;
   const long long groups = (long long)a.nframes * (gy + 2 * gc);
-  hipError_t e = hipMemsetAsync(a.pack_state, 0, sizeof(unsigned long long) * groups, s);
-  if (e == hipSuccess) e = hipMemsetAsync(a.pack_ticket, 0, sizeof(unsigned) * 3 * a.nframes, s);
-  if (e != hipSuccess) return e;
+  if (!state_zeroed) {
+    hipError_t e = hipMemsetAsync(a.pack_state, 0, sizeof(unsigned long long) * groups, s);
+    if (e == hipSuccess) e = hipMemsetAsync(a.pack_ticket, 0, sizeof(unsigned) * 3 * a.nframes, s);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(k_pack_lb, dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
   return hipGetLastError();
 }

@@ -160,6 +160,52 @@ def test_two_process_banded_encode_gloo():
     assert outs == [O.cref_encode(f) for f in frames]
 
 
+def _rank_full(rank, world, port, q):
+    """One rank of a two-process gloo band encode of config-4 frame 0 at full
+    size (7680x4320): its band only, host exchanges over gloo; rank 0
+    assembles and reports (length, sha256)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import hashlib
+    import torch.distributed as dist
+    import mijpeg
+    import recipes
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        frame = recipes.config4_frame(0)[None]
+        H, W = frame.shape[1:3]
+        r0, rows = sharding.band_rows(H, world, rank)
+        band = mijpeg.Batch(W, rows, 1)
+        band.upload(np.ascontiguousarray(frame[:, r0:r0 + rows]))
+        full = mijpeg.Batch(W, H, 1, assembler=True) if rank == 0 else None
+        sharding.encode_banded(band, 1, sharding.TorchExchange(dist, "cpu"), full)
+        if rank == 0:
+            out = full.output(0)
+            q.put((len(out), hashlib.sha256(out).hexdigest()))
+            full.close()
+        band.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_process_banded_encode_gloo_full_size(manifest):
+    """SURVEY §8(e) rehearsal at config 4's size: two processes, one band
+    each, gloo exchanges; the assembled frame is the reference's bytes for
+    config4_frame0 (tests/golden/manifest.json)."""
+    import multiprocessing as mp
+    want = manifest["config4_frame0"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_full, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got == (want["jpg_len"], want["jpg_sha256"])
+
+
 def _nccl_rank(port, q):
     # torch's HIP runtime first (as bench.py's dist_setup does): the bundled
     # runtime of torch does not initialise after the library's in one process
