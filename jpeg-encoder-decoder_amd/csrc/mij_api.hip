@@ -555,6 +555,11 @@ static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0, bool band = false
                  : (nframes >= 43 && b->quality <= 60)   ? 16
                  : ((long long)b->g.w * b->g.h >= (8 << 20)) ? 512
                                                            : 64;
+  // a 64-segment pack group at Q >= 85 outgrows a 4096-word window (config
+  // 5: Q=90 luma groups ~4.8k words): the double window keeps it on the
+  // one-window path (A/B: MIJ_PACK_WIDE=0/1)
+  static const int wide_env = getenv("MIJ_PACK_WIDE") ? atoi(getenv("MIJ_PACK_WIDE")) : -1;
+  a.pack_wide = wide_env >= 0 ? wide_env : (b->quality >= 85 ? 1 : 0);
   if (f0) {  // sub-batch: frames f0.. of the batch (every per-frame array shifted)
     const Geom &g = b->g;
     const long long F = f0, gpf = (g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((g.nsc + PACK_SEGS - 1) / PACK_SEGS);

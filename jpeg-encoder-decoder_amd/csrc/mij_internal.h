@@ -199,6 +199,7 @@ struct EntArgs {
   unsigned long long *dbg;         // diagnostics only (MIJ_PACK_TIME, diag build)
   const int2 *fdims;               // per-frame image size (region batches), null: the canvas
   int emit_slots;                  // k_emit_count / k_emit_write workgroups per scan (0: EMIT_SLOTS)
+  int pack_wide;                   // k_pack_lb with a 2 * PACK_WORDS window (high quality)
   int seg_dc;                      // k_tables: compute the segment-first DC tokens first (k_seg_dc)
 };
 

@@ -754,6 +754,9 @@ constexpr int k1_waves() {
   return k1_base(MODE) == K1M_TOK_OUT ? MIJ_K1_TOK_WAVES : (k1_wide<MODE>() ? 12 : 4);
 }
 
+#ifndef MIJ_K1_COOP_REPLAY
+#define MIJ_K1_COOP_REPLAY 1
+#endif
 template <int MODE>
 __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) void k_mcu_dct(K1Args a) {
   constexpr bool PIX = !(MODE & K1M_COEF_IN);
@@ -1204,16 +1207,81 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
           if (!DEFER && __ballot(hz != 0) && !(kflags & K1F_NO_REPLAY)) {
             // rare path: find the straddling coefficients (same arithmetic) and
             // recompute them in FP64 exactly as encoder.c:87-109
-            const uint8_t *Pb = L + (nt * 16 + bcol) * LDS_BLK;
             uint32_t mm = straddle_mask();
             nrep += (uint32_t)__popc(mm);
-            while (mm) {
-              const int k = __ffs(mm) - 1;
-              mm &= mm - 1u;
-              const int z = 16 * g + k;
-              const int v = ac_exact(Pb, z, s_qint[comp][z], s_cos, s_zz);
+            if constexpr (TOK && MIJ_K1_COOP_REPLAY) {
+              // The wave's straddles listed (lane << 4 | k, in the wave's
+              // token staging, free until this N-tile's tokens) and replayed
+              // 8 at a time: lane x of an 8-lane group sums column x of its
+              // block (the reference's inner loop, y order), the group's 8
+              // column sums meet by shuffles and every lane of it folds them
+              // in x order.  The FP64 operations are ac_exact's, in its order;
+              // a lane with several straddles no longer replays them one
+              // after another while the wave waits.
+              const int c = __popc(mm);
+              const int incl = (int)wave_scan64((uint32_t)c);
+              const int T = __builtin_amdgcn_readlane(incl, 63);
+              const int base = incl - c;
+              uint16_t *lst = (uint16_t *)&s_st[wave][0][0];
+              int *res = (int *)((uint8_t *)&s_st[wave][0][0] + 256);
+              for (int c0 = 0; c0 < T; c0 += 64) {
+                {
+                  uint32_t m2 = mm;
+                  for (int idx = base; m2; idx++) {
+                    const int k = __ffs(m2) - 1;
+                    m2 &= m2 - 1u;
+                    if (idx >= c0 && idx < c0 + 64) lst[idx - c0] = (uint16_t)(lane << 4 | k);
+                  }
+                }
+                wave_lds_sync();
+                const int nch = min(T - c0, 64);
+                for (int r = 0; r < nch; r += 8) {
+                  const int j = r + (lane >> 3), x = lane & 7;
+                  const int e = lst[j < nch ? j : 0];
+                  const int ol = e >> 4, k = e & 15;
+                  const int z = 16 * (ol >> 4) + k;
+                  const int rz = s_zz[z], v = rz >> 3, u = rz & 7;
+                  const uint8_t *Pb = L + (nt * 16 + (ol & 15)) * LDS_BLK;
+                  double in = 0.0;
 #pragma unroll
-              for (int j = 0; j < 16; j++) o[j] = j == k ? v : o[j];
+                  for (int y = 0; y < 8; y++)
+                    in = __dadd_rn(in, __dmul_rn((double)((int)Pb[y * 8 + x] - 128), s_cos[y * 8 + v]));
+                  double freq = 0.0;
+#pragma unroll
+                  for (int xx = 0; xx < 8; xx++)
+                    freq = __dadd_rn(freq, __dmul_rn(__shfl(in, (lane & ~7) + xx), s_cos[xx * 8 + u]));
+                  if (u == 0) freq = __dmul_rn(freq, SQRT1_2);
+                  if (v == 0) freq = __dmul_rn(freq, SQRT1_2);
+                  freq = __dmul_rn(freq, 0.25);
+                  int tq = (int)__ddiv_rn(freq, (double)s_qint[comp][z]);
+                  tq = tq < -2048 ? -2048 : (tq > 2047 ? 2047 : tq);
+                  if (x == 0 && j < nch) res[j] = tq;
+                }
+                wave_lds_sync();
+                {
+                  uint32_t m2 = mm;
+                  for (int idx = base; m2; idx++) {
+                    const int k = __ffs(m2) - 1;
+                    m2 &= m2 - 1u;
+                    if (idx >= c0 && idx < c0 + 64) {
+                      const int v = res[idx - c0];
+#pragma unroll
+                      for (int jj = 0; jj < 16; jj++) o[jj] = jj == k ? v : o[jj];
+                    }
+                  }
+                }
+                wave_lds_sync();
+              }
+            } else {
+              const uint8_t *Pb = L + (nt * 16 + bcol) * LDS_BLK;
+              while (mm) {
+                const int k = __ffs(mm) - 1;
+                mm &= mm - 1u;
+                const int z = 16 * g + k;
+                const int v = ac_exact(Pb, z, s_qint[comp][z], s_cos, s_zz);
+#pragma unroll
+                for (int j = 0; j < 16; j++) o[j] = j == k ? v : o[j];
+              }
             }
           }
           // token variants: the next tile's DMA has landed before the first
@@ -2783,8 +2851,15 @@ __device__ __forceinline__ void put_bits64_win(uint32_t *buf, uint32_t pos, unsi
   if (off + len > 64 && w + 2 >= wl && w + 2 < wh) atomicOr(&buf[w + 2 - wl], __builtin_amdgcn_alignbit(lo, 0u, off));
 }
 
+// PW: the LDS window in words (PACK_WORDS; high-quality batches, whose groups
+// outgrow it, get a double window -- fewer groups per CU, but no group on the
+// window-by-window path)
+#ifndef MIJ_PACK_WIDE_WORDS
+#define MIJ_PACK_WIDE_WORDS 6144
+#endif
+template <int PW>
 __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
-  __shared__ uint32_t buf[PACK_WORDS];
+  __shared__ uint32_t buf[PW];
   __shared__ uint32_t tab[2 * 256];
   __shared__ uint32_t s_bits[PACK_SEGS], s_off[PACK_SEGS];
   __shared__ unsigned long long s_prefix;
@@ -2988,7 +3063,7 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
   // takes its start bit first and packs window by window at absolute offsets.
   uint32_t *raw_scan = a.raw + (long long)f * G.raw_fs +
                        (comp == 0 ? 0 : G.raw_words[0] + (comp == 2 ? G.raw_words[1] : 0));
-  const bool rel = ((gbits + 31) >> 5) + 1 <= (uint32_t)PACK_WORDS;
+  const bool rel = ((gbits + 31) >> 5) + 1 <= (uint32_t)PW;
   // the group's words in the scan: [first, first + n)
   auto group_words = [&](unsigned long long gbase, uint32_t &n) -> unsigned long long {
     n = (uint32_t)(((gbase & 31) + gbits + 31) >> 5);
@@ -3007,8 +3082,8 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
     gw = group_words(s_prefix, nw);
   }
   LB_STAMP(2);
-  for (uint32_t w0 = 0; w0 < nw; w0 += PACK_WORDS) {
-    const uint32_t wn = min((uint32_t)PACK_WORDS, nw - w0);
+  for (uint32_t w0 = 0; w0 < nw; w0 += PW) {
+    const uint32_t wn = min((uint32_t)PW, nw - w0);
     const uint32_t lo_bit = w0 * 32, hi_bit = (w0 + wn) * 32;
     for (uint32_t i = tid; i < wn; i += LB_THREADS) buf[i] = 0;
     __syncthreads();
@@ -3796,7 +3871,8 @@ hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s, bool state_zeroed) {
     if (e == hipSuccess) e = hipMemsetAsync(a.pack_ticket, 0, sizeof(unsigned) * 3 * a.nframes, s);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_pack_lb, dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
+  if (a.pack_wide) hipLaunchKernelGGL(k_pack_lb<MIJ_PACK_WIDE_WORDS>, dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
+  else hipLaunchKernelGGL(k_pack_lb<PACK_WORDS>, dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_emit(const EntArgs &a0, hipStream_t s) {

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Q=50 / 90 config-3 steps, cooperative FP64 replay on/off (A/B), after the parity suite
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -q --timeout 280 --timeout-method thread tests/test_gpu_parity.py tests/test_tau_kernel.py > gpurun_out/t_q.log 2>&1 || { grep -E "^E |FAILED|Timeout|rror" gpurun_out/t_q.log | head; tail -3 gpurun_out/t_q.log; exit 1; }
+tail -1 gpurun_out/t_q.log
+for q in 90 50; do
+  for lib in ab/libmijpeg_coop0.so ab/libmijpeg_coop1.so ab/libmijpeg_coop0.so ab/libmijpeg_coop1.so; do
+    MIJ_LIB=$PWD/$lib timeout -k 10 150 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --coef-launches 0 --quality $q > gpurun_out/q.log 2>&1 || { tail -3 gpurun_out/q.log; exit 1; }
+    python3 -c "import json,sys;d=json.loads(open('gpurun_out/q.log').read().strip().splitlines()[-1]);s=d['stages_ms'];print('Q', sys.argv[2], sys.argv[1], d['ms_per_step'], 'K1', s['k1_colour_dct_quant'], 'pack', s['pack'], 'emit', s['emit'], d['verified_frames'])" $lib $q
+  done
+done
