@@ -1705,7 +1705,7 @@ __device__ __forceinline__ void top2_swap(unsigned long long &k1, unsigned long 
 #else
 #define TAB_T(k) do { } while (0)
 #endif
-__device__ void build_table_wave(const uint32_t *hist, const uint32_t *extra, HuffCode *hc, uint32_t *ehuf,
+__device__ __forceinline__ void build_table_wave(const uint32_t *hist, const uint32_t *extra, HuffCode *hc, uint32_t *ehuf,
                                  TabScratch *S, int lane, int *err, unsigned long long *tm = nullptr) {
   TAB_T(0);
   uint32_t f[5];
@@ -2062,6 +2062,7 @@ struct TabScratch2 {
       int scode[256];
     };
   };
+  int rec[256];  // narrow merge loop: per merge c1 | c2 << 10 | leaves(c1) << 20
   int par[514];  // node -> parent (0xFFFF: root), then pointer-jumping state
   int dep[514];
   int off[514];
@@ -2226,7 +2227,7 @@ __device__ __forceinline__ void bsort_level(unsigned long long (&k)[4], int lane
   if constexpr (K < 256) bsort_level<K * 2>(k, lane);
 }
 
-__device__ void build_table_wave2(const uint32_t *hist, const uint32_t *extra, HuffCode *hc, uint32_t *ehuf,
+__device__ __forceinline__ void build_table_wave2(const uint32_t *hist, const uint32_t *extra, HuffCode *hc, uint32_t *ehuf,
                                   TabScratch2 *S, int lane, int *err, unsigned long long *tm = nullptr) {
   TAB_T(0);
   uint32_t f[5];
@@ -2282,90 +2283,189 @@ __device__ void build_table_wave2(const uint32_t *hist, const uint32_t *extra, H
   wave_lds_sync();
   TAB_T(2);
   // the merges (encoder.c:196-226) on uniform values; v1 = the least key, v2
-  // the next; K = the merged node, queued at its key's place
-  // (keys as two 32-bit words -- freq, then label | leaves | node -- so the
-  // uniform compares stay on the scalar unit)
-  int lw = 0, mw = 0, lh = 0, mh = 0, mt = 0;
-  uint32_t wlh, wll, wmh = ~0u, wml = ~0u;
-  {
-    const unsigned long long v = S->ql[lane];
-    wlh = (uint32_t)(v >> 32);
-    wll = (uint32_t)v;
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-  }
-  uint32_t mlh = 0, mll = 0;  // the last appended key
+  // the next; K = the merged node, queued at its key's place.  Narrow keys
+  // when the table's whole count is below 2^23 (every frame up to ~4K at
+  // Q=50): count << 9 | (256 - label) in one 32-bit word, leaves << 10 |
+  // node beside it, one scalar compare per decision; the merge records stay
+  // in a register (one lane per merge) and go to LDS 64 at a time.
+  uint32_t fsum = 0;
+#pragma unroll
+  for (int r = 0; r < 4; r++) fsum += f[r];
+  const uint32_t total_count = __builtin_amdgcn_readlane((int)wave_scan64(fsum), 63) + 1u;
   int root_label = 256;
   uint32_t total = 1;
-  for (int step = 0; step + 1 < nl; step++) {
-    // (window reloads wait for their loads inside the branch, so the common
-    // path never waits for lane 0's queue and tree stores)
-    if (lh + 1 - lw > 63) {
-      lw = lh;
-      const unsigned long long v = S->ql[lw + lane];
+  if (total_count < (1u << 23)) {
+    int lw = 0, mw = 0, lh = 0, mh = 0, mt = 0;
+    uint32_t wlk, wla, wmk = ~0u, wma = ~0u, rec = 0;
+    auto split = [](unsigned long long v, uint32_t &key, uint32_t &aux) {
+      key = ((uint32_t)(v >> 32) << 9) | ((uint32_t)v >> 19);
+      aux = (uint32_t)v & 0x7FFFFu;
+    };
+    split(S->ql[lane], wlk, wla);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    uint32_t mlast = 0;  // the last appended key
+    const int nsteps = nl - 1;
+    for (int step = 0; step < nsteps; step++) {
+      if (lh + 1 - lw > 63) {
+        lw = lh;
+        split(S->ql[lw + lane], wlk, wla);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      }
+      if (mh + 1 - mw > 63) {
+        mw = mh;
+        split(S->qm[mw + lane], wmk, wma);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+      }
+      const int il = lh - lw, im = mh - mw;
+      const uint32_t ak = __builtin_amdgcn_readlane(wlk, il), bk = __builtin_amdgcn_readlane(wlk, il + 1);
+      const uint32_t ck = __builtin_amdgcn_readlane(wmk, im), dk = __builtin_amdgcn_readlane(wmk, im + 1);
+      const uint32_t aa = __builtin_amdgcn_readlane(wla, il), ba = __builtin_amdgcn_readlane(wla, il + 1);
+      const uint32_t ca = __builtin_amdgcn_readlane(wma, im), da = __builtin_amdgcn_readlane(wma, im + 1);
+      const bool ac = ak < ck;
+      const uint32_t k1 = ac ? ak : ck, k1a = ac ? aa : ca;
+      const uint32_t x = ac ? bk : ak, xa = ac ? ba : aa, y = ac ? ck : dk, ya = ac ? ca : da;
+      const bool bx = x < y;
+      const uint32_t k2 = bx ? x : y, k2a = bx ? xa : ya;
+      const int dlh = ac ? (bx ? 2 : 1) : (bx ? 1 : 0);
+      lh += dlh;
+      mh += 2 - dlh;
+      const uint32_t lab1 = k1 & 511u;  // 256 - v1
+      const uint32_t fs = (k1 >> 9) + (k2 >> 9);
+      const uint32_t sz1 = k1a >> 10, node = (uint32_t)(nl + step);
+      const uint32_t K = (fs << 9) | lab1, Ka = ((sz1 + (k2a >> 10)) << 10) | node;
+      // v2's chain follows v1's (:223-226): the merge's record
+      if (lane == (step & 63)) rec = (k1a & 1023u) | ((k2a & 1023u) << 10) | (sz1 << 20);
+      if ((step & 63) == 63) S->rec[step - 63 + lane] = (int)rec;
+      const unsigned long long K64 = ((unsigned long long)fs << 32) | (lab1 << 19) | Ka;
+      if (mt > mh && mlast > K) {
+        // (rare) an equal-count node with a smaller key is queued: insert
+        int pos = mt;
+        wave_lds_sync();
+        while (pos > mh && S->qm[pos - 1] > K64) {
+          if (lane == 0) S->qm[pos] = S->qm[pos - 1];
+          wave_lds_sync();
+          pos--;
+        }
+        if (lane == 0) S->qm[pos] = K64;
+        wave_lds_sync();
+        mw = mh;
+        split(S->qm[mw + lane], wmk, wma);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+      } else {
+        if (lane == 0) S->qm[mt] = K64;
+        if (lane == mt - mw) {
+          wmk = K;
+          wma = Ka;
+        }
+        mlast = K;
+      }
+      mt++;
+      root_label = 256 - (int)lab1;
+      total = fs;
+    }
+    // the last partial row of records, then the tree from all of them
+    {
+      const int b0 = nsteps & ~63;
+      if (b0 + lane < nsteps) S->rec[b0 + lane] = (int)rec;
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int j = lane + 64 * i;
+      if (j < nsteps) {
+        const uint32_t r = (uint32_t)S->rec[j];
+        const int c1 = (int)(r & 1023u), c2 = (int)((r >> 10) & 1023u), node = nl + j;
+        S->par[c1] = node;
+        S->par[c2] = node;
+        S->off[c1] = 0;
+        S->off[c2] = (int)(r >> 20);
+      }
+    }
+  } else {
+    // the merges (encoder.c:196-226) on uniform values; v1 = the least key, v2
+    // the next; K = the merged node, queued at its key's place
+    // (keys as two 32-bit words -- freq, then label | leaves | node -- so the
+    // uniform compares stay on the scalar unit)
+    int lw = 0, mw = 0, lh = 0, mh = 0, mt = 0;
+    uint32_t wlh, wll, wmh = ~0u, wml = ~0u;
+    {
+      const unsigned long long v = S->ql[lane];
       wlh = (uint32_t)(v >> 32);
       wll = (uint32_t)v;
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-    }
-    if (mh + 1 - mw > 63) {
-      mw = mh;
-      const unsigned long long v = S->qm[mw + lane];
-      wmh = (uint32_t)(v >> 32);
-      wml = (uint32_t)v;
       __builtin_amdgcn_s_waitcnt(0xC07F);
     }
-    const int il = lh - lw, im = mh - mw;
-    const uint32_t ah = __builtin_amdgcn_readlane(wlh, il), al = __builtin_amdgcn_readlane(wll, il);
-    const uint32_t bh = __builtin_amdgcn_readlane(wlh, il + 1), bl = __builtin_amdgcn_readlane(wll, il + 1);
-    const uint32_t ch = __builtin_amdgcn_readlane(wmh, im), cl0 = __builtin_amdgcn_readlane(wml, im);
-    const uint32_t dh = __builtin_amdgcn_readlane(wmh, im + 1), dl = __builtin_amdgcn_readlane(wml, im + 1);
-    const bool ac = ah < ch || (ah == ch && al < cl0);
-    const uint32_t k1h = ac ? ah : ch, k1l = ac ? al : cl0;
-    const uint32_t xh = ac ? bh : ah, xl = ac ? bl : al, yh = ac ? ch : dh, yl = ac ? cl0 : dl;
-    const bool bx = xh < yh || (xh == yh && xl < yl);
-    const uint32_t k2h = bx ? xh : yh, k2l = bx ? xl : yl;
-    const int dlh = ac ? (bx ? 2 : 1) : (bx ? 1 : 0);
-    lh += dlh;
-    mh += 2 - dlh;
-    const int lab1 = (int)(k1l >> 19);  // 256 - v1
-    const uint32_t fs = k1h + k2h;
-    const int sz1 = (int)((k1l >> 10) & 511), sz2 = (int)((k2l >> 10) & 511);
-    const int c1 = (int)(k1l & 1023), c2 = (int)(k2l & 1023), node = nl + step;
-    const uint32_t Kh = fs, Kl = ((uint32_t)lab1 << 19) | ((uint32_t)(sz1 + sz2) << 10) | (uint32_t)node;
-    if (lane == 0) {
-      S->par[c1] = node;
-      S->par[c2] = node;
-      S->off[c1] = 0;
-      S->off[c2] = sz1;  // v2's chain follows v1's (:223-226)
-    }
-    const unsigned long long K = ((unsigned long long)Kh << 32) | Kl;
-    if (mt > mh && (mlh > Kh || (mlh == Kh && mll > Kl))) {
-      // (rare) an equal-count node with a smaller key is queued: insert
-      int pos = mt;
-      wave_lds_sync();
-      while (pos > mh && S->qm[pos - 1] > K) {
-        if (lane == 0) S->qm[pos] = S->qm[pos - 1];
+    uint32_t mlh = 0, mll = 0;  // the last appended key
+    for (int step = 0; step + 1 < nl; step++) {
+      // (window reloads wait for their loads inside the branch, so the common
+      // path never waits for lane 0's queue and tree stores)
+      if (lh + 1 - lw > 63) {
+        lw = lh;
+        const unsigned long long v = S->ql[lw + lane];
+        wlh = (uint32_t)(v >> 32);
+        wll = (uint32_t)v;
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      }
+      if (mh + 1 - mw > 63) {
+        mw = mh;
+        const unsigned long long v = S->qm[mw + lane];
+        wmh = (uint32_t)(v >> 32);
+        wml = (uint32_t)v;
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+      }
+      const int il = lh - lw, im = mh - mw;
+      const uint32_t ah = __builtin_amdgcn_readlane(wlh, il), al = __builtin_amdgcn_readlane(wll, il);
+      const uint32_t bh = __builtin_amdgcn_readlane(wlh, il + 1), bl = __builtin_amdgcn_readlane(wll, il + 1);
+      const uint32_t ch = __builtin_amdgcn_readlane(wmh, im), cl0 = __builtin_amdgcn_readlane(wml, im);
+      const uint32_t dh = __builtin_amdgcn_readlane(wmh, im + 1), dl = __builtin_amdgcn_readlane(wml, im + 1);
+      const bool ac = ah < ch || (ah == ch && al < cl0);
+      const uint32_t k1h = ac ? ah : ch, k1l = ac ? al : cl0;
+      const uint32_t xh = ac ? bh : ah, xl = ac ? bl : al, yh = ac ? ch : dh, yl = ac ? cl0 : dl;
+      const bool bx = xh < yh || (xh == yh && xl < yl);
+      const uint32_t k2h = bx ? xh : yh, k2l = bx ? xl : yl;
+      const int dlh = ac ? (bx ? 2 : 1) : (bx ? 1 : 0);
+      lh += dlh;
+      mh += 2 - dlh;
+      const int lab1 = (int)(k1l >> 19);  // 256 - v1
+      const uint32_t fs = k1h + k2h;
+      const int sz1 = (int)((k1l >> 10) & 511), sz2 = (int)((k2l >> 10) & 511);
+      const int c1 = (int)(k1l & 1023), c2 = (int)(k2l & 1023), node = nl + step;
+      const uint32_t Kh = fs, Kl = ((uint32_t)lab1 << 19) | ((uint32_t)(sz1 + sz2) << 10) | (uint32_t)node;
+      if (lane == 0) {
+        S->par[c1] = node;
+        S->par[c2] = node;
+        S->off[c1] = 0;
+        S->off[c2] = sz1;  // v2's chain follows v1's (:223-226)
+      }
+      const unsigned long long K = ((unsigned long long)Kh << 32) | Kl;
+      if (mt > mh && (mlh > Kh || (mlh == Kh && mll > Kl))) {
+        // (rare) an equal-count node with a smaller key is queued: insert
+        int pos = mt;
         wave_lds_sync();
-        pos--;
+        while (pos > mh && S->qm[pos - 1] > K) {
+          if (lane == 0) S->qm[pos] = S->qm[pos - 1];
+          wave_lds_sync();
+          pos--;
+        }
+        if (lane == 0) S->qm[pos] = K;
+        wave_lds_sync();
+        mw = mh;
+        const unsigned long long v = S->qm[mw + lane];
+        wmh = (uint32_t)(v >> 32);
+        wml = (uint32_t)v;
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+      } else {
+        if (lane == 0) S->qm[mt] = K;
+        if (lane == mt - mw) {
+          wmh = Kh;
+          wml = Kl;
+        }
+        mlh = Kh;
+        mll = Kl;
       }
-      if (lane == 0) S->qm[pos] = K;
-      wave_lds_sync();
-      mw = mh;
-      const unsigned long long v = S->qm[mw + lane];
-      wmh = (uint32_t)(v >> 32);
-      wml = (uint32_t)v;
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-    } else {
-      if (lane == 0) S->qm[mt] = K;
-      if (lane == mt - mw) {
-        wmh = Kh;
-        wml = Kl;
-      }
-      mlh = Kh;
-      mll = Kl;
+      mt++;
+      root_label = 256 - lab1;
+      total = fs;
     }
-    mt++;
-    root_label = 256 - lab1;
-    total = fs;
   }
   const int nn = 2 * nl - 1, root = nn - 1;
   if (lane == 0) {
