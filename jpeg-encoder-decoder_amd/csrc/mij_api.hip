@@ -285,6 +285,8 @@ struct mij_batch {
   std::vector<unsigned long long> band_words;  // per frame x 3: packed words after mij_band_pack
   int band_async_n = 0;                        // frames of the last mij_band_pack_async
   int asm_tables_n = 0;                        // frames of the last mij_assemble_tables_async
+  int hist_zero_n = 0;  // frames 0..n-1 of d_hist left zeroed by the last encode's k_tables_1w
+  int hist_zero_after = 0;  // set by run_entropy: the frames its k_tables_1w zeroed
   unsigned long long *d_bound_acc = nullptr;   // k_band_bound: {sum, arrivals}, left zeroed by its last workgroup
   // region batches (mij_batch_set_frame_dims / _gather_regions): per-frame
   // image size inside the canvas slots; d_frame stages a host frame
@@ -517,6 +519,7 @@ extern "C" int mij_batch_set_input(mij_batch *b, const void *d_bgr, long long fr
 // start bits live in d_dcpred / d_bitbase; every other pipeline reads both as
 // 0 (null), so a band call leaves no state behind for the next encode
 static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0, bool band = false) {
+  b->hist_zero_n = 0;  // every path through here may write the histograms
   EntArgs a;
   memset(&a, 0, sizeof(a));
   a.g = b->g;
@@ -765,8 +768,10 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
               span / nframes, sw / (2.0 * nframes), ww / (2.0 * nframes), ent / nframes);
     }
   } else if (!tables_given) {
+    a.zero_pack = !a.seg_dc;  // one wave per table: it zeroes the pack state too
     HIP_TRY(launch_tables(a, st));
   }
+  b->hist_zero_after = (f0 == 0 && a.zero_pack) ? nframes : 0;
   if (t) HIP_TRY(hipEventRecord(b->ev[5], st));
   // segment bits, scan offsets and packing in one look-back pass
   if (b->raw_dirty) {
@@ -781,7 +786,7 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
     HIP_TRY(hipMalloc(&a.dbg, sizeof(unsigned long long) * 4 * ngroups));
     HIP_TRY(hipMemsetAsync(a.dbg, 0, sizeof(unsigned long long) * 4 * ngroups, st));
   }
-  HIP_TRY(launch_pack_lb(a, st));
+  HIP_TRY(launch_pack_lb(a, st, a.zero_pack != 0));
   if (ptime) {
     std::vector<unsigned long long> h(4 * ngroups);
     HIP_TRY(hipMemcpyAsync(h.data(), a.dbg, sizeof(unsigned long long) * 4 * ngroups, hipMemcpyDeviceToHost, st));
@@ -807,7 +812,9 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
 }
 
 static int encode_frames(mij_batch *b, int nframes) {
-  HIP_TRY(hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * nframes * 4 * 257, b->stream));
+  if (nframes > b->hist_zero_n)
+    HIP_TRY(hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * nframes * 4 * 257, b->stream));
+  b->hist_zero_n = 0;
   // region batches: K1 skips the canvas tiles outside a frame, so their
   // segments must read as empty
   if (b->use_fdims && b->rgb) return fail(MIJ_EINVAL, "encode: region batches read B, G, R frames");
@@ -843,7 +850,10 @@ static int encode_frames(mij_batch *b, int nframes) {
     if (run_k1(b, nframes, b->keep_coefs ? 3 : 2)) return g_err;  // events 1 and 2 (no fixer)
   }
   if (b->timing) HIP_TRY(hipEventRecord(b->ev[3], b->stream));
-  return run_entropy(b, nframes, !b->split, false);
+  if (run_entropy(b, nframes, !b->split, false)) return g_err;
+  // (run_entropy's k_tables_1w zeroed the counts it read)
+  b->hist_zero_n = b->hist_zero_after;
+  return MIJ_OK;
 }
 
 static void next_slot(mij_batch *b) {

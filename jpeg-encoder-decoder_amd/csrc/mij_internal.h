@@ -200,6 +200,7 @@ struct EntArgs {
   const int2 *fdims;               // per-frame image size (region batches), null: the canvas
   int emit_slots;                  // k_emit_count / k_emit_write workgroups per scan (0: EMIT_SLOTS)
   int pack_wide;                   // k_pack_lb with a 2 * PACK_WORDS window (high quality)
+  int zero_pack;                   // k_tables_1w also zeroes k_pack_lb's look-back words and tickets
   int seg_dc;                      // k_tables: compute the segment-first DC tokens first (k_seg_dc)
 };
 

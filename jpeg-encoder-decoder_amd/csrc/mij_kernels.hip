@@ -2739,12 +2739,19 @@ __global__ __launch_bounds__(256) void k_tables(EntArgs a) {
 __global__ __launch_bounds__(64) void k_tables_1w(EntArgs a) {
   __shared__ TabScratch2 S;
   const int f = blockIdx.x >> 2, t = blockIdx.x & 3, lane = threadIdx.x;
+  if (a.zero_pack) {  // (k_pack_lb runs next: its state, zeroed here instead of two fills)
+    const long long gpf = (a.g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((a.g.nsc + PACK_SEGS - 1) / PACK_SEGS);
+    for (long long i = 64 * t + lane; i < gpf; i += 256) a.pack_state[f * gpf + i] = 0;
+    if (t == 0 && lane < 3) a.pack_ticket[f * 3 + lane] = 0;
+  }
 #ifdef MIJ_K1_DIAG
   if (a.dbg && lane == 0) a.dbg[((long long)f * 4 + t) * 10 + 8] = __builtin_amdgcn_s_memtime();
 #endif
   build_table_wave2(a.hist + ((long long)f * 4 + t) * 257, nullptr, (HuffCode *)a.hc + (long long)f * 4 + t,
                     (uint32_t *)a.ehuf + ((long long)f * 4 + t) * 256, &S, lane, a.err + f,
                     a.dbg ? a.dbg + ((long long)f * 4 + t) * 10 : nullptr);
+  if (a.zero_pack)  // the counts are read: left zeroed for the next K1 (no fill before it)
+    for (int i = lane; i < 257; i += 64) a.hist[((long long)f * 4 + t) * 257 + i] = 0;
 }
 #endif
 
