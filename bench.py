@@ -941,7 +941,7 @@ def main():
         "verified_contents_pinned_to_reference_sha": pinned,
         # blocks re-encoded in FP64 by k_fix_blocks (split pipeline) or coefficients
         # replayed in place (fused pipeline), per frame
-        "fp64_fixups_per_frame": round(replays / (F * (args.warmup + args.steps)), 2),
+        "fp64_fixups_per_frame": round(replays / (F * (args.warmup + 2 * args.steps)), 2),  # timed + events pass
     }
     if coef_ms is not None:
         cb = px_step * 3 + coef_bytes + dc_bytes
