@@ -93,3 +93,23 @@ def test_assembler_refuses_pipeline_entry_points():
         with pytest.raises(mijpeg.MijError, match="an assembler only assembles"):
             c()
     a.close()
+
+
+def test_repeated_encodes_growing_and_shrinking_frame_counts():
+    """The encode path leaves the counts it read (and k_pack_lb's look-back
+    state) zeroed, and the next encode skips those fills only for the frames
+    known clean: 1 frame, then 3 (two never zeroed), then 3 again, then 2,
+    a band call in between (which writes the counts) and 3 again -- every
+    output the oracle's bytes."""
+    W, H = 320, 160
+    frames = np.stack([recipes.config3_frame(i + 20, H, W) for i in range(3)])
+    want = [O.cref_encode(f) for f in frames]
+    b = mijpeg.Batch(W, H, 3)
+    b.upload(frames)
+    for n in (1, 3, 3, 2):
+        b.encode(n)
+        assert [b.output(i) for i in range(n)] == want[:n], n
+    b.band_analyze(2)
+    b.encode(3)
+    assert [b.output(i) for i in range(3)] == want
+    b.close()

@@ -39,6 +39,10 @@ def cases():
     out.append(("pairs", live * np.repeat(rng.integers(1, 20, 128), 2)))
     out.append(("power law", live * (1e6 / (1 + np.arange(256)) ** 1.5).astype(np.int64)))
     out.append(("large counts", live * rng.integers(1 << 21, 1 << 22, 256)))
+    # counts of 2^23 and more: the 64-bit leaf sort and the wide merge keys
+    # (the whole table's count kept below 2^31, as the reference's int sums need)
+    out.append(("counts above 2^23", live * rng.integers(1 << 23, 1 << 24, 256) * (rng.random(256) < 0.15)))
+    out.append(("one count above 2^23", np.where(np.arange(256) == 3, (1 << 24) + 5, live * rng.integers(0, 9, 256))))
     out.append(("ac-like 162", np.where((np.arange(256) & 15) <= 10, rng.integers(0, 300, 256), 0)))
     out.append(("sparse ties", np.where(rng.random(256) < 0.2, rng.integers(1, 4, 256), 0)))
     out.append(("fibonacci 30", fib_hist(30)))
