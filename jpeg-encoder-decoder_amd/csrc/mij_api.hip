@@ -1567,7 +1567,9 @@ extern "C" int mij_band_words_async(mij_batch *b, int n, uint32_t *d_dst, size_t
   // the move table of mij_band_pack_async, words of frames 0..n-1 in (frame,
   // scan) order into d_dst (cap_words long: words beyond it are dropped, and
   // the root's assembly sees the overflow in the counts), zeroed behind
-  HIP_TRY(launch_move_pieces(b->d_raw, b->g, d_dst, b->d_pieces, n * 3, 64 * 1024, (long long)cap_words, b->stream));
+  // (no piece is longer than the caller's buffer: its length sizes the grid)
+  HIP_TRY(launch_move_pieces(b->d_raw, b->g, d_dst, b->d_pieces, n * 3, std::max<long long>((long long)cap_words, 1024),
+                             (long long)cap_words, b->stream));
   if (n >= b->raw_dirty) b->raw_dirty = 0;
   return MIJ_OK;
 }

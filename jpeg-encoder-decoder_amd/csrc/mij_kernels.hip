@@ -3643,9 +3643,21 @@ __global__ void k_move_pieces(uint32_t *raw, long long raw_fs, long long rw0, lo
   const long long fc = (long long)pc[0], n = (long long)pc[1], d0 = (long long)pc[2];
   const long long f = fc / 3, c = fc - 3 * f;
   uint32_t *src = raw + f * raw_fs + (c == 0 ? 0 : rw0 + (c == 2 ? rw1 : 0));
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    if (d0 + i < cap) dst[d0 + i] = src[i];  // (past the destination: dropped, still zeroed)
-    src[i] = 0u;
+  // four words per thread per round, loads first (a round costs one memory
+  // latency, not four)
+  const long long G = (long long)gridDim.x * blockDim.x;
+  for (long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += 4 * G) {
+    uint32_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[u] = i0 + u * G < n ? src[i0 + u * G] : 0u;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const long long i = i0 + u * G;
+      if (i < n) {
+        if (d0 + i < cap) dst[d0 + i] = v[u];  // (past the destination: dropped, still zeroed)
+        src[i] = 0u;
+      }
+    }
   }
 }
 // ---- one large frame in bands, device-resident control (mij_band_*_async):
@@ -3776,11 +3788,25 @@ __global__ void k_or_shift_pieces(uint32_t *raw, long long raw_fs, long long rw0
   const long long nsrc = (bits + 31) >> 5, ndst = (sh + bits + 31) >> 5;
   uint32_t *dst = raw + f * raw_fs + (c == 0 ? 0 : rw0 + (c == 2 ? rw1 : 0)) + (long long)(pc[1] >> 5);
   const uint32_t *sp = src + (long long)pc[2];
-  for (long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x; j < ndst; j += (long long)gridDim.x * blockDim.x) {
-    uint32_t v = j < nsrc ? sp[j] >> sh : 0u;
-    if (sh && j > 0) v |= sp[j - 1] << (32 - sh);
-    if (j == 0 || j == ndst - 1) atomicOr(&dst[j], v);
-    else dst[j] = v;
+  const long long G = (long long)gridDim.x * blockDim.x;
+  for (long long j0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; j0 < ndst; j0 += 4 * G) {
+    uint32_t hi[4], lo[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const long long j = j0 + u * G;
+      hi[u] = j < nsrc ? sp[j] : 0u;
+      lo[u] = j > 0 && j <= nsrc ? sp[j - 1] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const long long j = j0 + u * G;
+      if (j < ndst) {
+        uint32_t v = hi[u] >> sh;
+        if (sh) v |= lo[u] << (32 - sh);
+        if (j == 0 || j == ndst - 1) atomicOr(&dst[j], v);
+        else dst[j] = v;
+      }
+    }
   }
 }
 
@@ -3934,7 +3960,7 @@ hipError_t launch_move_pieces(uint32_t *raw, const Geom &g, uint32_t *dst,
                               hipStream_t s) {
   if (npieces <= 0 || max_words <= 0) return hipSuccess;
   const long long chunks = (max_words + 1023) / 1024;
-  hipLaunchKernelGGL(k_move_pieces, dim3((unsigned)(chunks < 64 ? chunks : 64), (unsigned)npieces), dim3(256), 0, s,
+  hipLaunchKernelGGL(k_move_pieces, dim3((unsigned)(chunks < 256 ? chunks : 256), (unsigned)npieces), dim3(256), 0, s,
                      raw, g.raw_fs, g.raw_words[0], g.raw_words[1], dst, d_pieces, cap);
   return hipGetLastError();
 }
@@ -3965,7 +3991,7 @@ hipError_t launch_or_shift_pieces(uint32_t *raw, const Geom &g, const uint32_t *
                                   const unsigned long long *d_pieces, int npieces, long long max_words, hipStream_t s) {
   if (npieces <= 0 || max_words <= 0) return hipSuccess;
   const long long chunks = (max_words + 1 + 1023) / 1024;
-  hipLaunchKernelGGL(k_or_shift_pieces, dim3((unsigned)(chunks < 64 ? chunks : 64), (unsigned)npieces), dim3(256), 0,
+  hipLaunchKernelGGL(k_or_shift_pieces, dim3((unsigned)(chunks < 256 ? chunks : 256), (unsigned)npieces), dim3(256), 0,
                      s, raw, g.raw_fs, g.raw_words[0], g.raw_words[1], src, d_pieces);
   return hipGetLastError();
 }
