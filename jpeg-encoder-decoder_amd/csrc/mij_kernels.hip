@@ -1595,84 +1595,17 @@ __global__ __launch_bounds__(MIJ_SEGDC_WG) void k_seg_dc(EntArgs a) {
 
 
 // ===========================================================================
-// k_tables: the four optimized Huffman tables of a frame (encoder.c:180-301),
-// one wave per table.  The reference's O(n^2) selection loop is restated as a
-// wave reduction: v1 = least frequency with ties to the highest index, v2 =
-// the next (exactly what the <= scan of :196-206 selects), merged chains are
-// tracked by root label (code_len += 1 for both chains, :213-227) and the
-// `next` links are kept so the whole huff_code struct matches.
+// k_tables / k_tables_1w: the four optimized Huffman tables of a frame
+// (encoder.c:180-301), one wave per table (build_table_wave2 below).
 // ===========================================================================
-// MIJ_TAB_QUEUE (default): the merge loop as the two-queue Huffman
-// construction -- the live nodes' keys (frequency, then the highest index
-// first: the <= scan of encoder.c:196-206) in two ascending queues, the
-// leaves sorted once (bitonic, in registers) and the merged nodes appended
-// in creation order (their frequencies never decrease; an equal-frequency
-// tie is inserted at its key's place), so v1 and v2 are always among the
-// four queue heads: O(1) per merge instead of a 64-lane top-2 reduction.
-// The queues live in LDS and every lane reads their heads (broadcast), so
-// each merge costs one LDS round trip and a few uniform VALU selects; the
-// code lengths come from the merge tree afterwards (pointer jumping).
-#ifndef MIJ_TAB_QUEUE
-#define MIJ_TAB_QUEUE 2
-#endif
-
-struct TabScratch {
-  int next[257];
-  int tail[257];
-  int sorted[256];
-  int clf[32];       // code_len_freq (all 257 symbols), then limited
-  int cnt[32];       // symbols 0..255 per unlimited length
-  int base[32];
-  int cum[18];       // cumulative limited counts
-  int first_code[18];
-  int slen[256];
-  int scode[256];
-  int n;
-  int err;
-#if MIJ_TAB_QUEUE
-  // the two-queue merge (build_table_wave): keys of the sorted leaves (symbol
-  // 256 first) and of the merged nodes, ~0 past their ends; the merge tree
-  // (leaves 0..256, merge j = node 257 + j) and each label's current node
-  unsigned long long ql[260], qm[260];
-  int parent[514];
-  int depth[514];
-  int cur[257];
-  int fin[257];  // sym_freq after the merges (:221-222)
-#endif
-};
-
-__device__ __forceinline__ void top2(unsigned long long &k1, unsigned long long &k2,
-                                     unsigned long long o1, unsigned long long o2) {
-  // merge sorted pairs (k1<=k2) and (o1<=o2) keeping the two smallest
-  const unsigned long long lo = k1 < o1 ? k1 : o1;
-  const unsigned long long hi = k1 < o1 ? o1 : k1;
-  const unsigned long long m2 = k2 < o2 ? k2 : o2;
-  k1 = lo;
-  k2 = hi < m2 ? hi : m2;
-}
-
-// One butterfly step of the wave's top-2 reduction with DPP instead of
-// ds_bpermute (__shfl_xor): each step exchanges the 64-bit keys with a lane of
-// a disjoint group (quad_perm [1,0,3,2], [2,3,0,1]; row_half_mirror,
-// row_mirror; then permlane16/32 swaps across rows), so after six steps every
-// lane holds the wave's two smallest keys.  VALU-latency steps instead of LDS
-// round trips on the merge loop's critical path (~160 iterations per AC table).
-#ifndef MIJ_TAB_DPP
-#define MIJ_TAB_DPP 1
-#endif
 template <int CTRL>
 __device__ __forceinline__ unsigned long long dpp_u64(unsigned long long x) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, 0xF, 0xF, false);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, false);
   return ((unsigned long long)hi << 32) | lo;
 }
-template <int CTRL>
-__device__ __forceinline__ void top2_dpp(unsigned long long &k1, unsigned long long &k2) {
-  const unsigned long long o1 = dpp_u64<CTRL>(k1), o2 = dpp_u64<CTRL>(k2);
-  top2(k1, k2, o1, o2);
-}
 // permlane16/32 swap of a 64-bit value: (a, b) = one lane's own value and its
-// partner's (which is which depends on the row; the merge is symmetric)
+// partner's (a in the odd rows / upper half, b in the others)
 template <int W>
 __device__ __forceinline__ void swap_u64(unsigned long long x, unsigned long long &a, unsigned long long &b) {
   const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
@@ -1688,351 +1621,16 @@ __device__ __forceinline__ void swap_u64(unsigned long long x, unsigned long lon
     b = ((unsigned long long)rh[1] << 32) | rl[1];
   }
 }
-template <int W>
-__device__ __forceinline__ void top2_swap(unsigned long long &k1, unsigned long long &k2) {
-  unsigned long long a1, b1, a2, b2;
-  swap_u64<W>(k1, a1, b1);
-  swap_u64<W>(k2, a2, b2);
-  k1 = a1;
-  k2 = a2;
-  top2(k1, k2, b1, b2);
-}
 
-// extra: DC class counts the caller adds to hist (the segment-first DCs), or null
 // (MIJ_K1_DIAG build, MIJ_TAB_TIME: tm != null gets the wave's phase clocks)
 #ifdef MIJ_K1_DIAG
 #define TAB_T(k) do { if (tm && lane == 0) tm[k] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define TAB_T(k) do { } while (0)
 #endif
-__device__ __forceinline__ void build_table_wave(const uint32_t *hist, const uint32_t *extra, HuffCode *hc, uint32_t *ehuf,
-                                 TabScratch *S, int lane, int *err, unsigned long long *tm = nullptr) {
-  TAB_T(0);
-  uint32_t f[5];
-  int cl[5], gr[5];
-#pragma unroll
-  for (int i = 0; i < 5; i++) {
-    const int s = lane + 64 * i;
-    f[i] = s < 256 ? hist[s] : (s == 256 ? 1u : 0u);  // :364-367
-    if (extra && i == 0 && lane < 16) f[i] += extra[lane];
-    cl[i] = 0;
-    gr[i] = s;
-    if (s < 257) {
-      S->next[s] = -1;
-      S->tail[s] = s;
-    }
-  }
-  if (lane < 32) { S->clf[lane] = 0; S->cnt[lane] = 0; }
-  wave_lds_sync();
-  TAB_T(1);
-#if MIJ_TAB_QUEUE
-  {
-    // the leaves: symbols 0..255 with a nonzero count, ascending by key
-    // (symbol 256 -- count 1, highest index -- is the smallest key of all and
-    // heads the queue); bitonic sort in registers, element i of the order in
-    // lane i & 63 of skey[i >> 6]
-    unsigned long long skey[4];
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int sy = lane + 64 * r;
-      skey[r] = f[r] ? ((unsigned long long)f[r] << 9) | (unsigned)(256 - sy) : ~0ull;
-    }
-#pragma unroll
-    for (int k = 2; k <= 256; k <<= 1)
-#pragma unroll
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        if (j >= 64) {
-#pragma unroll
-          for (int r = 0; r < 4; r++) {
-            const int rp = r ^ (j >> 6);
-            if (rp > r) {
-              const bool up = (((lane + 64 * r) & k) == 0);
-              const unsigned long long x = skey[r], y = skey[rp];
-              const unsigned long long lo = x < y ? x : y, hi = x < y ? y : x;
-              skey[r] = up ? lo : hi;
-              skey[rp] = up ? hi : lo;
-            }
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; r++) {
-            const unsigned long long o = __shfl_xor(skey[r], j);
-            const bool up = (((lane + 64 * r) & k) == 0), lower = (lane & j) == 0;
-            const unsigned long long lo = skey[r] < o ? skey[r] : o, hi = skey[r] < o ? o : skey[r];
-            skey[r] = lower == up ? lo : hi;
-          }
-        }
-      }
-    int nl = 1;  // leaves: symbol 256 + the nonzero counts of 0..255
-#pragma unroll
-    for (int r = 0; r < 4; r++) nl += __popcll(__ballot(f[r] != 0));
-#pragma unroll
-    for (int r = 0; r < 4; r++) S->ql[1 + lane + 64 * r] = skey[r];
-    if (lane == 0) S->ql[0] = 512ull;  // symbol 256: count 1, index 256
-    if (lane < 3) S->ql[257 + lane] = ~0ull;
-#pragma unroll
-    for (int i = 0; i < 5; i++) {
-      const int sy = lane + 64 * i;
-      if (sy < 260) S->qm[sy] = ~0ull;
-      if (sy < 257) {
-        S->cur[sy] = sy;
-        S->fin[sy] = (int)f[i];
-        S->parent[sy] = -1;
-      }
-    }
-    wave_lds_sync();
-    TAB_T(2);
-    // every lane runs the loop on the same (uniform) values; lane 0 alone
-    // writes.  v1 = the least key, v2 = the next (encoder.c:196-206)
-    int lh = 0, mh = 0, mt = 0;
-    unsigned long long mlast = 0;  // key of qm[mt - 1]
-    for (int step = 0; step + 1 < nl; step++) {
-      const unsigned long long a0 = S->ql[lh], b0 = S->ql[lh + 1], c0 = S->qm[mh], d0 = S->qm[mh + 1];
-      const bool ac = a0 < c0;
-      const unsigned long long k1 = ac ? a0 : c0, x = ac ? b0 : a0, y = ac ? c0 : d0;
-      const bool bx = x < y;  // x is a leaf, y a merged node
-      const unsigned long long k2 = bx ? x : y;
-      lh += (int)ac + (int)bx;
-      mh += 2 - (int)ac - (int)bx;
-      const int v1 = 256 - (int)(k1 & 511), v2 = 256 - (int)(k2 & 511);
-      const uint32_t fs = (uint32_t)(k1 >> 9) + (uint32_t)(k2 >> 9);
-      const unsigned long long K = ((unsigned long long)fs << 9) | (unsigned)(256 - v1);
-      // merged frequencies never decrease: an append, unless an equal-count
-      // node with a smaller key than K is already queued (rare)
-      int pos = mt;
-      if (mt > mh && mlast > K) {
-        while (pos > mh && S->qm[pos - 1] > K) {
-          if (lane == 0) S->qm[pos] = S->qm[pos - 1];
-          wave_lds_sync();
-          pos--;
-        }
-      }
-      if (lane == 0) {
-        S->qm[pos] = K;
-        S->fin[v1] = (int)fs;  // :221-222
-        S->fin[v2] = 0;
-        // :223-226: v2's chain joins v1's (next[tail(v1)] = v2), both one
-        // code bit longer -- the merge tree's node 257 + step
-        const int node = 257 + step;
-        S->parent[S->cur[v1]] = node;
-        S->parent[S->cur[v2]] = node;
-        S->parent[node] = -1;
-        S->cur[v1] = node;
-        const int t1 = S->tail[v1];
-        S->next[t1] = v2;
-        S->tail[v1] = S->tail[v2];
-      }
-      if (pos == mt) mlast = K;
-      mt++;
-      wave_lds_sync();
-    }
-    TAB_T(3);
-    // code lengths = leaf depths in the merge tree (pointer jumping: nine
-    // rounds cover <= 513 nodes)
-    const int nnodes = 257 + max(nl - 1, 0);
-    int dp[9], pp[9];
-#pragma unroll
-    for (int i = 0; i < 9; i++) {
-      const int nd = lane + 64 * i;
-      pp[i] = nd < nnodes ? S->parent[nd] : -1;
-      dp[i] = pp[i] >= 0 ? 1 : 0;
-      if (nd < nnodes) S->depth[nd] = dp[i];
-    }
-    wave_lds_sync();
-    for (int round = 0; round < 9; round++) {
-      int nd2[9], np2[9];
-#pragma unroll
-      for (int i = 0; i < 9; i++) {
-        nd2[i] = pp[i] >= 0 ? dp[i] + S->depth[pp[i]] : dp[i];
-        np2[i] = pp[i] >= 0 ? S->parent[pp[i]] : -1;
-      }
-      wave_lds_sync();
-#pragma unroll
-      for (int i = 0; i < 9; i++) {
-        const int nd = lane + 64 * i;
-        dp[i] = nd2[i];
-        pp[i] = np2[i];
-        if (nd < nnodes) {
-          S->depth[nd] = dp[i];
-          S->parent[nd] = pp[i];
-        }
-      }
-      wave_lds_sync();
-    }
-#pragma unroll
-    for (int i = 0; i < 5; i++) {
-      const int sy = lane + 64 * i;
-      if (sy < 257) {
-        cl[i] = dp[i];
-        f[i] = (uint32_t)S->fin[sy];
-      }
-    }
-  }
-#else
-  for (;;) {
-    unsigned long long k1 = ~0ull, k2 = ~0ull;
-#pragma unroll
-    for (int i = 0; i < 5; i++) {
-      const int s = lane + 64 * i;
-      if (s < 257 && f[i]) {
-        const unsigned long long key = ((unsigned long long)f[i] << 9) | (unsigned)(256 - s);
-        top2(k1, k2, key, ~0ull);
-      }
-    }
-#if MIJ_TAB_DPP
-    top2_dpp<0xB1>(k1, k2);   // quad_perm [1,0,3,2]
-    top2_dpp<0x4E>(k1, k2);   // quad_perm [2,3,0,1]
-    top2_dpp<0x141>(k1, k2);  // row_half_mirror
-    top2_dpp<0x140>(k1, k2);  // row_mirror
-    top2_swap<16>(k1, k2);
-    top2_swap<32>(k1, k2);
-#else
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      const unsigned long long o1 = __shfl_xor(k1, off);
-      const unsigned long long o2 = __shfl_xor(k2, off);
-      top2(k1, k2, o1, o2);
-    }
-#endif
-    if (k2 == ~0ull) break;
-    const int v1 = 256 - (int)(k1 & 511), v2 = 256 - (int)(k2 & 511);
-    const uint32_t fs = (uint32_t)(k1 >> 9) + (uint32_t)(k2 >> 9);
-#pragma unroll
-    for (int i = 0; i < 5; i++) {
-      const int s = lane + 64 * i;
-      if (s == v1) f[i] = fs;
-      if (s == v2) f[i] = 0;
-      if (gr[i] == v1 || gr[i] == v2) {
-        cl[i]++;
-        gr[i] = v1;
-      }
-    }
-    // (Measured and dropped: chain tails kept in registers and read with
-    // readlane instead of this LDS round trip + wave sync: 0.066 -> 0.088 ms
-    // per config-3 launch, the VALU->SGPR hand-offs cost more than the LDS.)
-    if (lane == 0) {
-      const int t1 = S->tail[v1];
-      S->next[t1] = v2;
-      S->tail[v1] = S->tail[v2];
-    }
-    wave_lds_sync();
-  }
-#endif
-  wave_lds_sync();
-  TAB_T(4);
-  int bad = 0;
-#pragma unroll
-  for (int i = 0; i < 5; i++) {
-    const int s = lane + 64 * i;
-    if (s < 257) {
-      hc->sym_freq[s] = (int)f[i];
-      hc->code_len[s] = cl[i];
-      hc->next[s] = S->next[s];
-      if (cl[i] >= 32) bad = 1;  // the reference indexes code_len_freq out of bounds
-      else if (cl[i]) {
-        atomicAdd(&S->clf[cl[i]], 1);
-        if (s < 256) atomicAdd(&S->cnt[cl[i]], 1);
-      }
-    }
-  }
-  if (__ballot(bad)) {
-    if (lane == 0) *err = 1;
-    return;
-  }
-  wave_lds_sync();
-  if (lane == 0) {
-    int *clf = S->clf;
-    int nl = 0;
-    for (int i = 1; i < 32; i++) nl += clf[i];
-    S->err = nl < 2;
-    if (!S->err) {
-      // :239-259 limit to 16 bits
-      int i = 31;
-      for (;;) {
-        if (clf[i] > 0) {
-          int j = i - 1;
-          do { j--; } while (clf[j] <= 0);
-          clf[i] -= 2;
-          clf[i - 1]++;
-          clf[j + 1] += 2;
-          clf[j]--;
-          continue;
-        }
-        i--;
-        if (i != 16) continue;
-        while (clf[i] == 0) i--;
-        clf[i]--;
-        break;
-      }
-      int acc = 0;
-      for (int L = 0; L < 32; L++) { S->base[L] = acc; acc += S->cnt[L]; }
-      S->n = acc;  // symbols 0..255 with a code
-      S->cum[0] = 0;
-      for (int L = 1; L <= 16; L++) S->cum[L] = S->cum[L - 1] + clf[L];
-      // :280-300 canonical codes
-      int code = 0, started = 0;
-      for (int L = 1; L <= 16; L++) {
-        if (started) code <<= 1;
-        S->first_code[L] = code;
-        if (clf[L]) started = 1;
-        code += clf[L];
-      }
-      if (S->cum[16] != S->n || S->n >= 255) S->err = 1;
-    }
-  }
-  wave_lds_sync();
-  TAB_T(5);
-  if (S->err) {
-    if (lane == 0) *err = 1;
-    return;
-  }
-  // :262-268 order symbols 0..255 by (unlimited length, value)
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const int s = lane + 64 * i;
-    for (int L = 1; L < 32; L++) {
-      const unsigned long long m = __ballot(cl[i] == L);
-      if (!m) continue;
-      if (cl[i] == L) {
-        const int pos = S->base[L] + __popcll(m & ((1ull << lane) - 1ull));
-        S->sorted[pos] = s;
-      }
-      if (lane == 0) S->base[L] += __popcll(m);
-      wave_lds_sync();
-    }
-  }
-  wave_lds_sync();
-  TAB_T(6);
-  const int n = S->n;
-  // every output address is written exactly once, from LDS staging
-  for (int k = lane; k < 256; k += 64) {
-    S->slen[k] = 0;
-    S->scode[k] = -1;
-  }
-  wave_lds_sync();
-  for (int k = lane; k < n; k += 64) {  // :271-276 and :280-300
-    int L = 1;
-    while (S->cum[L] <= k) L++;
-    const int s = S->sorted[k];
-    S->slen[s] = L;
-    S->scode[s] = S->first_code[L] + (k - S->cum[L - 1]);
-  }
-  wave_lds_sync();
-  if (lane < 32) hc->code_len_freq[lane] = S->clf[lane];
-  for (int k = lane; k < 256; k += 64) {
-    // sym_sorted: -1 past the end, except that the sentinel write of :277
-    // lands in sym_sorted[255] (it aliases sym_code_len[-1], structs.h:10-11)
-    hc->sym_sorted[k] = k < n ? S->sorted[k] : (k == 255 ? 0 : -1);
-    const int L = S->slen[k];
-    hc->sym_code_len[k] = L;
-    hc->sym_code[k] = S->scode[k];
-    ehuf[k] = L ? ((uint32_t)L << 16) | (uint32_t)S->scode[k] : 0u;
-  }
-  TAB_T(7);
-}
 
 // ---------------------------------------------------------------------------
-// build_table_wave2 (MIJ_TAB_QUEUE 2): the same tables, every phase without a
+// build_table_wave2: init_huff_table restated so that no phase is a
 // lane-serial LDS chain.
 //  - leaves sorted by a register bitonic network (DPP / permlane partners, no
 //    LDS round trips);
@@ -2671,11 +2269,7 @@ __device__ __forceinline__ void build_table_wave2(const uint32_t *hist, const ui
 // each, 32 segments in flight per lane) while the AC-table waves, the long
 // pole (~160 symbols to merge against <= 12), already build theirs.
 __global__ __launch_bounds__(256) void k_tables(EntArgs a) {
-#if MIJ_TAB_QUEUE == 2
   __shared__ TabScratch2 S[4];
-#else
-  __shared__ TabScratch S[4];
-#endif
   __shared__ uint32_t h[2][16];
   __shared__ uint32_t hs[32 * 32];  // seg_dc_store's spread counters
   __shared__ int s_done;
@@ -2722,17 +2316,11 @@ __global__ __launch_bounds__(256) void k_tables(EntArgs a) {
     wave_lds_sync();
     extra = h[t >> 1];
   }
-#if MIJ_TAB_QUEUE == 2
-  build_table_wave2(
-#else
-  build_table_wave(
-#endif
-                   a.hist + ((long long)f * 4 + t) * 257, extra, (HuffCode *)a.hc + (long long)f * 4 + t,
+  build_table_wave2(a.hist + ((long long)f * 4 + t) * 257, extra, (HuffCode *)a.hc + (long long)f * 4 + t,
                    (uint32_t *)a.ehuf + ((long long)f * 4 + t) * 256, &S[t], lane, a.err + f,
                    a.dbg ? a.dbg + ((long long)f * 4 + t) * 10 : nullptr);
 }
 
-#if MIJ_TAB_QUEUE == 2
 // The same tables one wave (workgroup) per table when the segment DCs ran on
 // their own (k_seg_dc): 14 KB of LDS per workgroup instead of 61 KB, so the
 // tables of one sub-batch fit beside the next sub-batch's K1 (overlap path).
@@ -2753,7 +2341,6 @@ __global__ __launch_bounds__(64) void k_tables_1w(EntArgs a) {
   if (a.zero_pack)  // the counts are read: left zeroed for the next K1 (no fill before it)
     for (int i = lane; i < 257; i += 64) a.hist[((long long)f * 4 + t) * 257 + i] = 0;
 }
-#endif
 
 // code tables from caller-owned huff_code structs (drop-in write_jpg)
 __global__ void k_ehuf_struct(const HuffCode *hc, uint32_t *ehuf) {
@@ -3918,12 +3505,10 @@ hipError_t launch_dc_diff(int16_t *coef, const int16_t *dc, const Geom &g, int n
   return hipGetLastError();
 }
 hipError_t launch_tables(const EntArgs &a, hipStream_t s) {
-#if MIJ_TAB_QUEUE == 2
   if (!a.seg_dc) {
     hipLaunchKernelGGL(k_tables_1w, dim3(a.nframes * 4), dim3(64), 0, s, a);
     return hipGetLastError();
   }
-#endif
   hipLaunchKernelGGL(k_tables, dim3(a.nframes), dim3(256), 0, s, a);
   return hipGetLastError();
 }
