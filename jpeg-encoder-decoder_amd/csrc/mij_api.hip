@@ -30,6 +30,7 @@ hipError_t launch_bits(const EntArgs &a, hipStream_t s);
 hipError_t launch_scan(const EntArgs &a, hipStream_t s);
 hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s, bool state_zeroed = false);
 hipError_t launch_emit(const EntArgs &a, hipStream_t s);
+hipError_t launch_seam_fix(const EntArgs &a, hipStream_t s);
 hipError_t launch_or_words(uint32_t *dst, const uint32_t *src, long long n, hipStream_t s);
 hipError_t launch_move_pieces(uint32_t *raw, const Geom &g, uint32_t *dst,
                               const unsigned long long *d_pieces, int npieces, long long max_words, long long cap,
@@ -266,6 +267,7 @@ struct mij_batch {
   unsigned *d_replays = nullptr;
   uint32_t *d_ffc = nullptr;      // k_emit_count: 0xFF bytes per scan chunk
   uint32_t *d_choff = nullptr;    // k_emit_scan: output offset per scan chunk
+  uint32_t *d_seam = nullptr;     // k_pack_lb -> k_seam_fix: shared first word per pack group
   unsigned long long *d_pack_state = nullptr;  // k_pack_lb look-back words, per pack group
   unsigned *d_pack_ticket = nullptr;
   uint16_t *d_fixmask = nullptr;  // K1 fix masks: per N-tile (tile * 3 + nt), zero between launches
@@ -330,7 +332,7 @@ static void batch_free(mij_batch *b) {
                   b->d_ehuf, b->d_raw, b->d_tok, b->d_tok0, b->d_seg_ntok, b->d_seg_bits, b->d_seg_off,
                   b->d_scan_bits, b->d_out_len, b->d_hc, b->d_out, b->d_err, b->d_replays,
                   b->d_dcpred, b->d_bitbase, b->d_stage, b->d_fixmask, b->d_audit, b->d_ffc, b->d_choff,
-                  b->d_pack_state, b->d_pack_ticket, b->d_fdims, b->d_frame, b->d_regions, b->d_pieces,
+                  b->d_seam, b->d_pack_state, b->d_pack_ticket, b->d_fdims, b->d_frame, b->d_regions, b->d_pieces,
                   b->d_bound_acc};
   for (void *p : ptrs)
     if (p) hipFree(p);
@@ -394,6 +396,7 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
     HIP_TRY(hipMemsetAsync(b->d_fixmask, 0, sizeof(uint16_t) * F * g.tiles_per_frame * 3, b->stream));
     HIP_TRY(dalloc(&b->d_pack_state, F * ((g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((g.nsc + PACK_SEGS - 1) / PACK_SEGS))));
     HIP_TRY(dalloc(&b->d_pack_ticket, F * 3));  // one per scan
+    HIP_TRY(dalloc(&b->d_seam, F * ((g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((g.nsc + PACK_SEGS - 1) / PACK_SEGS))));
     HIP_TRY(dalloc(&b->d_regions, F));
   }
   HIP_TRY(dalloc(&b->d_hist, F * 4 * 257));
@@ -774,7 +777,17 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   b->hist_zero_after = (f0 == 0 && a.zero_pack) ? nframes : 0;
   if (t) HIP_TRY(hipEventRecord(b->ev[5], st));
   // segment bits, scan offsets and packing in one look-back pass
-  if (b->raw_dirty) {
+  // Seam mode (default; MIJ_SEAM=0 for the A/B): every scan word is stored
+  // whole by one pack group; a group's first word, when shared with the group
+  // before it, goes to seam[] and k_seam_fix ORs it in after the packing --
+  // the scan buffers need not start zeroed (no atomics in k_pack_lb), and
+  // k_emit_write does not zero them after reading.  The other paths (bands,
+  // assembly) still OR onto zero: they clear what this leaves (raw_dirty).
+  static const int seam_env = getenv("MIJ_SEAM") ? atoi(getenv("MIJ_SEAM")) : 1;
+  if (seam_env && b->d_seam) {
+    a.seam = b->d_seam + (long long)f0 * ((b->g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((b->g.nsc + PACK_SEGS - 1) / PACK_SEGS));
+    b->raw_dirty = std::max(b->raw_dirty, f0 + nframes);
+  } else if (b->raw_dirty) {
     HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->raw_dirty * b->g.raw_fs, st));
     b->raw_dirty = 0;
   }
@@ -787,6 +800,7 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
     HIP_TRY(hipMemsetAsync(a.dbg, 0, sizeof(unsigned long long) * 4 * ngroups, st));
   }
   HIP_TRY(launch_pack_lb(a, st, a.zero_pack != 0));
+  if (a.seam) HIP_TRY(launch_seam_fix(a, st));
   if (ptime) {
     std::vector<unsigned long long> h(4 * ngroups);
     HIP_TRY(hipMemcpyAsync(h.data(), a.dbg, sizeof(unsigned long long) * 4 * ngroups, hipMemcpyDeviceToHost, st));

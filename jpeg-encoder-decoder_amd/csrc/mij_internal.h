@@ -198,6 +198,9 @@ struct EntArgs {
   unsigned int *pack_ticket;       // k_pack_lb: next group to claim, per scan
   unsigned long long *dbg;         // diagnostics only (MIJ_PACK_TIME, diag build)
   const int2 *fdims;               // per-frame image size (region batches), null: the canvas
+  uint32_t *seam;                  // per pack group: its first word when shared with the group
+                                   // before it (null: edge words OR-ed onto all-zero scan buffers;
+                                   // set: k_seam_fix ORs them in, nothing needs zeroed buffers)
   int emit_slots;                  // k_emit_count / k_emit_write workgroups per scan (0: EMIT_SLOTS)
   int pack_wide;                   // k_pack_lb with a 2 * PACK_WORDS window (high quality)
   int zero_pack;                   // k_tables_1w also zeroes k_pack_lb's look-back words and tickets

@@ -2480,11 +2480,15 @@ __device__ __forceinline__ void put_bits_window(uint32_t *buf, uint32_t pos, uin
 // into place.  Groups wider than one window (near worst-case entropy) take
 // the look-back first and pack window by window at absolute offsets.
 //
-// The scan buffers are all-zero when this kernel starts (k_emit_write zeroes
-// every word it consumes; the host clears them after the band paths), so a
-// group ORs its first and last word, which it may share with a neighbour
-// group, and stores its interior words plainly: no ordering between groups
-// beyond the prefix itself.  (Measured: staging a group's tokens in LDS to
+// Seam mode (EntArgs::seam, the frame encodes): a group stores every word it
+// reaches the end of plainly; its first word, when the group before it ends
+// inside that word, goes to seam[] for k_seam_fix -- the scan buffers may
+// hold anything when the kernel starts, and no word is written twice.  (A/B,
+// config 3: 0.72 ms against 0.80 for the OR-onto-zero form, which the band
+// paths keep: there the buffers are all-zero on entry -- k_emit_write zeroes
+// every word it consumes, the host clears them after the band paths -- and a
+// group ORs its first and last word, which it may share with a neighbour.)
+// No ordering between groups beyond the prefix itself.  (Measured: staging a group's tokens in LDS to
 // read them once ran 1.72 ms instead of 1.31 ms per config-3 step -- the
 // 48 KB staging cut residency from 8 to 3 groups per CU, and the kernel is
 // latency-bound; look-back before packing: 0.94-0.97 ms against 0.92 here.)
@@ -2889,10 +2893,14 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
       gw = group_words(s_prefix, n);
       const uint32_t sh = (uint32_t)(s_prefix & 31);
       uint32_t *raw = raw_scan + gw;
-      // the edge words may be shared with the neighbouring groups: OR (onto zero)
+      // the edge words may be shared with the neighbouring groups: OR (onto
+      // zero), or in seam mode (EntArgs::seam) the first word to the side
       for (uint32_t i = tid; i < n; i += LB_THREADS) {
         const uint32_t v = __builtin_amdgcn_alignbit(i ? buf[i - 1] : 0u, buf[i], sh);
-        if (i == 0 || i == n - 1) atomicOr(&raw[i], v);
+        if (a.seam) {  // every word stored whole; a shared first word goes to the seam
+          if (i == 0 && sh) a.seam[gid] = v;
+          else raw[i] = v;
+        } else if (i == 0 || i == n - 1) atomicOr(&raw[i], v);
         else raw[i] = v;
       }
     } else {
@@ -2900,7 +2908,10 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
       uint32_t *raw = raw_scan + gw;
       for (uint32_t i = tid; i < wn; i += LB_THREADS) {
         const uint32_t wi = w0 + i;
-        if (wi == 0 || wi == nw - 1) atomicOr(&raw[wi], buf[i]);
+        if (a.seam) {
+          if (wi == 0 && boff) a.seam[gid] = buf[i];
+          else raw[wi] = buf[i];
+        } else if (wi == 0 || wi == nw - 1) atomicOr(&raw[wi], buf[i]);
         else raw[wi] = buf[i];
       }
     }
@@ -2912,6 +2923,28 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
     for (int k = 0; k < 4; k++) a.dbg[(long long)gid * 4 + k] = tstamp[k];
 #endif
 #undef LB_STAMP
+}
+
+// k_seam_fix (seam mode, EntArgs::seam): k_pack_lb stored every scan word
+// whole, each by the one group that reaches its end, and left a group's first
+// word, when the group before it ends inside that word, in seam[]; this ORs
+// those words in (one thread per group; atomics only because the last, short
+// group of a scan may start inside the same word as the one before it).
+// Nothing then needs zeroed scan buffers: no OR-ing onto zero in the packing,
+// no zeroing in k_emit_write.
+__global__ __launch_bounds__(256) void k_seam_fix(EntArgs a) {
+  const Geom &G = a.g;
+  const int gy = (G.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (G.nsc + PACK_SEGS - 1) / PACK_SEGS, gpf = gy + 2 * gc;
+  const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (long long)a.nframes * gpf) return;
+  const int f = (int)(g / gpf), bq = (int)(g - (long long)f * gpf);
+  const int comp = bq < gy ? 0 : (bq < gy + gc ? 1 : 2);
+  const int q = bq - (comp == 0 ? 0 : (comp == 1 ? gy : gy + gc));
+  if (q == 0 || a.err[f]) return;  // (a failed frame is dropped by the assembly)
+  const unsigned long long start = a.pack_state[g - 1] & LB_VAL;  // the group's first bit
+  if (!(start & 31)) return;
+  uint32_t *raw = a.raw + (long long)f * G.raw_fs + (comp == 0 ? 0 : G.raw_words[0] + (comp == 2 ? G.raw_words[1] : 0));
+  atomicOr(&raw[start >> 5], a.seam[g]);
 }
 
 // ===========================================================================
@@ -2984,23 +3017,14 @@ __global__ __launch_bounds__(256) void k_emit_count(EntArgs a) {
   }
 }
 
-// k_emit_scan: one workgroup per frame.  Headers (encoder.c:549-600), the
-// SOS of each scan, the output offset of every chunk (exclusive scan of the
-// 0xFF counts), the pad bytes (:425-432), EOI and the frame's length.
-__global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
-  __shared__ int red[4];
-  const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (!emit_frame_ok(a, f)) {
-    if (tid == 0) a.out_len[f] = 0;
-    return;
-  }
-  uint8_t *out = a.out + (long long)f * a.g.out_cap;
+// Frame headers (encoder.c:549-600) into out[0, hlen); returns hlen.  Called
+// by a whole workgroup (s_n: 4 ints of LDS; one barrier inside).
+__device__ __forceinline__ int emit_headers(const EntArgs &a, int f, uint8_t *out, int *s_n) {
+  const int tid = threadIdx.x;
   const HuffCode *hc = a.hc + (long long)f * 4;
-  const long long nchmax = emit_chunks(a.g);
   // headers, one byte per thread (a single thread's byte loop is a chain of
   // dependent loads and stores: 40 us per launch): APP0 20 + DQT 2 x 69 +
   // DHT 4 x (21 + n_t) + SOF0 19
-  __shared__ int s_n[4];
   {
     int hn = tid < 64 ? hc[tid >> 4].code_len_freq[1 + (tid & 15)] : 0;
     for (int o = 8; o; o >>= 1) hn += __shfl_xor(hn, o);  // sums over 16 lanes
@@ -3038,6 +3062,23 @@ __global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
       out[i] = v;
     }
   }
+  return hlen;
+}
+
+// k_emit_scan: one workgroup per frame.  Headers (encoder.c:549-600), the
+// SOS of each scan, the output offset of every chunk (exclusive scan of the
+// 0xFF counts), the pad bytes (:425-432), EOI and the frame's length.
+__global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
+  __shared__ int red[4];
+  const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (!emit_frame_ok(a, f)) {
+    if (tid == 0) a.out_len[f] = 0;
+    return;
+  }
+  uint8_t *out = a.out + (long long)f * a.g.out_cap;
+  const long long nchmax = emit_chunks(a.g);
+  __shared__ int s_n[4];
+  const int hlen = emit_headers(a, f, out, s_n);
   unsigned long long pos = (unsigned long long)hlen;
   for (int comp = 0; comp < 3; comp++) {
     if (tid == 0) {  // SOS (encoder.c:601-620)
@@ -3095,15 +3136,18 @@ __global__ __launch_bounds__(256) void k_emit_write(EntArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // every scan-buffer word read here is zeroed after use: k_pack_lb needs
   // all-zero buffers (a failed frame's buffers are cleared whole)
+  // (seam mode: nothing is zeroed, k_pack_lb stores whole words)
   uint32_t *raw = (uint32_t *)scan_raw(a, f, comp);
+  const bool zero = a.seam == nullptr;
   if (!emit_frame_ok(a, f)) {
-    for (long long i = (long long)slot * 256 + tid; i < a.g.raw_words[comp]; i += a.emit_slots * 256) raw[i] = 0;
+    if (zero)
+      for (long long i = (long long)slot * 256 + tid; i < a.g.raw_words[comp]; i += a.emit_slots * 256) raw[i] = 0;
     return;
   }
   uint8_t *out = a.out + (long long)f * a.g.out_cap;
   const long long nchmax = emit_chunks(a.g);
   const unsigned long long nbits = a.scan_bits[f * 3 + comp], nbytes = nbits >> 3;
-  if (slot == 0 && tid < 2) {  // words past the last whole byte (the pad byte's bits)
+  if (zero && slot == 0 && tid < 2) {  // words past the last whole byte (the pad byte's bits)
     const unsigned long long w = ((nbytes + 3) >> 2) + tid;
     if (w < ((nbits + 31) >> 5)) raw[w] = 0;
   }
@@ -3132,9 +3176,11 @@ __global__ __launch_bounds__(256) void k_emit_write(EntArgs a) {
     }
 #pragma unroll
     for (int k = 0; k < WPW / 64; k++) wcnt += lims[k] ? ff_bytes(wds[k], lims[k]) : 0;
+    if (zero) {
 #pragma unroll
-    for (int k = 0; k < WPW / 64; k++)
-      if (lims[k]) raw[(wb0 + 4ull * (64 * k + lane)) >> 2] = 0u;
+      for (int k = 0; k < WPW / 64; k++)
+        if (lims[k]) raw[(wb0 + 4ull * (64 * k + lane)) >> 2] = 0u;
+    }
     for (int off = 32; off; off >>= 1) wcnt += __shfl_xor(wcnt, off);
     if (lane == 0) red[wave] = wcnt;
     __syncthreads();
@@ -3591,6 +3637,12 @@ hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s, bool state_zeroed) {
   }
   if (a.pack_wide) hipLaunchKernelGGL(k_pack_lb<MIJ_PACK_WIDE_WORDS>, dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
   else hipLaunchKernelGGL(k_pack_lb<PACK_WORDS>, dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_seam_fix(const EntArgs &a, hipStream_t s) {
+  const long long gpf = (a.g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((a.g.nsc + PACK_SEGS - 1) / PACK_SEGS);
+  const long long n = (long long)a.nframes * gpf;
+  hipLaunchKernelGGL(k_seam_fix, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_emit(const EntArgs &a0, hipStream_t s) {
