@@ -215,6 +215,31 @@ def test_random_shapes_vs_oracle(seed):
     b.close()
 
 
+def test_short_last_pack_group_seams():
+    """432x304: 513 chroma blocks, so each chroma scan's last pack group is one
+    segment of a single block.  Mostly flat frames make that group a few bits
+    long: it starts inside the word where the group before it ends and often
+    ends there too (seam mode: the word is the previous group's store OR-ed
+    with both groups' seams, and the pad byte comes from it)."""
+    W, H, n = 432, 304, 8
+    rng = np.random.default_rng(432)
+    frames = np.empty((n, H, W, 3), np.uint8)
+    for i in range(n):
+        frames[i] = rng.integers(0, 256, 3, dtype=np.uint8)
+        k = int(rng.integers(1, 40))  # a few busy 16x16 blocks in the first MCU row
+        for x in rng.choice(W // 16, size=min(k, W // 16), replace=False):
+            frames[i, :16, 16 * x:16 * x + 16] = rng.integers(0, 256, (16, 16, 3), dtype=np.uint8)
+        frames[i, -16:, -16:] = rng.integers(0, 256, 3, dtype=np.uint8)  # a last block of its own colour
+    b = mijpeg.Batch(W, H, n, 50)
+    b.upload(frames)
+    b.encode(n)
+    for i in range(n):
+        ref = O.cref_encode(frames[i], 50)
+        got = b.output(i)
+        assert got == ref, f"frame {i}: first diff {first_diff(got, ref)}"
+    b.close()
+
+
 def test_multi_frame_batch_independent_tables():
     rng = np.random.default_rng(11)
     frames = np.stack([rng.integers(0, 256, (64, 96, 3), dtype=np.uint8),
