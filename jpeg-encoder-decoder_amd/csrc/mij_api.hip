@@ -550,7 +550,8 @@ static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0, bool band = false
   a.pack_state = b->d_pack_state;
   a.pack_ticket = b->d_pack_ticket;
   a.fdims = b->use_fdims ? b->d_fdims : nullptr;
-  // JFIF-assembly workgroups per scan (A/B, profiles/r02/emit_slots_ab.txt):
+  // JFIF-assembly workgroups per frame (its chunks dealt round-robin over
+  // the three scans; A/B per scan in round 2, profiles/r02/emit_slots_ab.txt):
   // 16 on large low-Q batches (emit 0.247 -> 0.232 ms at config 3, Q=50),
   // 64 otherwise (Q=90: 0.62 at 64 against 0.68 at 16; a single frame needs
   // the width)
@@ -558,9 +559,9 @@ static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0, bool band = false
   // chunks each)
   static const int slots_env = getenv("MIJ_EMIT_SLOTS") ? atoi(getenv("MIJ_EMIT_SLOTS")) : 0;  // A/B
   a.emit_slots = slots_env > 0                           ? slots_env
-                 : (nframes >= 43 && b->quality <= 60)   ? 16
-                 : ((long long)b->g.w * b->g.h >= (8 << 20)) ? 512
-                                                           : 64;
+                 : (nframes >= 43 && b->quality <= 60)   ? 48
+                 : ((long long)b->g.w * b->g.h >= (8 << 20)) ? 1536
+                                                           : 192;
   // a 64-segment pack group at Q >= 85 outgrows a 4096-word window (config
   // 5: Q=90 luma groups ~4.8k words): the double window keeps it on the
   // one-window path (A/B: MIJ_PACK_WIDE=0/1)

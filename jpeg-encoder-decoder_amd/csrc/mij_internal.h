@@ -39,15 +39,18 @@ constexpr int PACK_WORDS = 4096;
 // k_pack_lb: tokens per lane loaded in one batch (16 lanes per segment)
 constexpr int PACK_BATCH = 16;
 // JFIF assembly: scans are written in EMIT_CH-byte chunks by EntArgs::
-// emit_slots workgroups per scan, EMIT_SLOTS when unset (A/B on config 3,
+// emit_slots workgroups per frame, EMIT_SLOTS when unset (round 2's A/B per scan on config 3,
 // emit = count + scan + write: 8 slots 0.260 ms, 16 0.232, 32 0.243,
-// 64 0.247, 128 0.269, 256 0.321; profiles/r02/emit_slots_ab.txt)
+// 64 0.247, 128 0.269, 256 0.321; profiles/r02/emit_slots_ab.txt).  Round 3
+// (seam mode, chunks dealt over the frame's scans, profiles/r03/seam/
+// emit_ab.txt): 8 KB chunks 0.190 ms at Q=50 and 0.549 at Q=90 against
+// 0.210 / 0.639 with 4 KB; 16 KB chunks 0.29 / 0.80.
 #ifndef MIJ_EMIT_CH
-#define MIJ_EMIT_CH 4096
+#define MIJ_EMIT_CH 8192
 #endif
 constexpr int EMIT_CH = MIJ_EMIT_CH;
 #ifndef MIJ_EMIT_SLOTS
-#define MIJ_EMIT_SLOTS 64
+#define MIJ_EMIT_SLOTS 192
 #endif
 constexpr int EMIT_SLOTS = MIJ_EMIT_SLOTS;
 
@@ -201,7 +204,7 @@ struct EntArgs {
   uint32_t *seam;                  // per pack group: its first word when shared with the group
                                    // before it (null: edge words OR-ed onto all-zero scan buffers;
                                    // set: k_seam_fix ORs them in, nothing needs zeroed buffers)
-  int emit_slots;                  // k_emit_count / k_emit_write workgroups per scan (0: EMIT_SLOTS)
+  int emit_slots;                  // k_emit_count / k_emit_write workgroups per frame (0: EMIT_SLOTS)
   int pack_wide;                   // k_pack_lb with a 2 * PACK_WORDS window (high quality)
   int zero_pack;                   // k_tables_1w also zeroes k_pack_lb's look-back words and tickets
   int seg_dc;                      // k_tables: compute the segment-first DC tokens first (k_seg_dc)

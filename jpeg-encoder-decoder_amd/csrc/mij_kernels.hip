@@ -2957,7 +2957,9 @@ __global__ __launch_bounds__(256) void k_seam_fix(EntArgs a) {
 // bytes of every chunk; k_emit_write then knows every chunk's output offset
 // (header + earlier scans + earlier chunks' stuffing) and writes the chunks
 // independently: the stuffed bytes are laid out in LDS and leave in
-// coalesced stores.  Workgroup (frame, comp, j) takes chunks j, j+a.emit_slots..
+// coalesced stores.  Workgroup (frame, j) takes chunks j, j + a.emit_slots, ..
+// of the frame's chunk list (scan 0's, then 1's, then 2's), so the luma
+// scan's chunks do not all queue behind a third of the workgroups.
 // ===========================================================================
 __device__ __forceinline__ bool emit_frame_ok(const EntArgs &a, int f) {
   unsigned long long need = 1024;  // headers, markers, pads
@@ -2992,14 +2994,20 @@ __device__ __forceinline__ int block_sum256(int v, int *red) {
 
 __global__ __launch_bounds__(256) void k_emit_count(EntArgs a) {
   __shared__ int red[4];
-  const int slot = blockIdx.x % a.emit_slots, fc = blockIdx.x / a.emit_slots;
-  const int f = fc / 3, comp = fc - f * 3;
-  const unsigned long long nbytes = a.scan_bits[f * 3 + comp] >> 3;
-  if (nbytes > 4ull * a.g.raw_words[comp]) return;  // k_emit_write drops the frame
-  const uint32_t *raw = scan_raw(a, f, comp);
-  const long long nch = (long long)((nbytes + EMIT_CH - 1) / EMIT_CH);
-  uint32_t *ffc = a.ffc + (long long)fc * emit_chunks(a.g);
-  for (long long c = slot; c < nch; c += a.emit_slots) {
+  const int slot = blockIdx.x % a.emit_slots, f = blockIdx.x / a.emit_slots;
+  long long nch[3];
+  unsigned long long nbs[3];
+#pragma unroll
+  for (int comp = 0; comp < 3; comp++) {
+    nbs[comp] = a.scan_bits[f * 3 + comp] >> 3;
+    nch[comp] = nbs[comp] > 4ull * a.g.raw_words[comp] ? 0 : (long long)((nbs[comp] + EMIT_CH - 1) / EMIT_CH);
+  }  // (a scan past its buffer: k_emit_write drops the frame)
+  // the frame's chunks, scan after scan, dealt round-robin to its workgroups
+  for (long long i = slot; i < nch[0] + nch[1] + nch[2]; i += a.emit_slots) {
+    const int comp = i < nch[0] ? 0 : (i < nch[0] + nch[1] ? 1 : 2);
+    const long long c = i - (comp == 0 ? 0 : (comp == 1 ? nch[0] : nch[0] + nch[1]));
+    const unsigned long long nbytes = nbs[comp];
+    const uint32_t *raw = scan_raw(a, f, comp);
     const unsigned long long b0 = (unsigned long long)c * EMIT_CH + threadIdx.x * (EMIT_CH / 256);
     int cnt = 0;
 #pragma unroll
@@ -3013,7 +3021,7 @@ __global__ __launch_bounds__(256) void k_emit_count(EntArgs a) {
       }
     }
     const int tot = block_sum256(cnt, red);
-    if (threadIdx.x == 0) ffc[c] = (uint32_t)tot;
+    if (threadIdx.x == 0) a.ffc[(long long)(f * 3 + comp) * emit_chunks(a.g) + c] = (uint32_t)tot;
   }
 }
 
@@ -3131,31 +3139,39 @@ __global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
 __global__ __launch_bounds__(256) void k_emit_write(EntArgs a) {
   __shared__ uint8_t s_out[2 * EMIT_CH];
   __shared__ int red[4];
-  const int slot = blockIdx.x % a.emit_slots, fc = blockIdx.x / a.emit_slots;
-  const int f = fc / 3, comp = fc - f * 3;
+  const int slot = blockIdx.x % a.emit_slots, f = blockIdx.x / a.emit_slots;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // every scan-buffer word read here is zeroed after use: k_pack_lb needs
-  // all-zero buffers (a failed frame's buffers are cleared whole)
-  // (seam mode: nothing is zeroed, k_pack_lb stores whole words)
-  uint32_t *raw = (uint32_t *)scan_raw(a, f, comp);
+  // all-zero buffers (a failed frame's buffers are cleared whole) -- except
+  // in seam mode, where k_pack_lb stores whole words and nothing is zeroed
   const bool zero = a.seam == nullptr;
   if (!emit_frame_ok(a, f)) {
+    uint32_t *rawf = a.raw + (long long)f * a.g.raw_fs;
     if (zero)
-      for (long long i = (long long)slot * 256 + tid; i < a.g.raw_words[comp]; i += a.emit_slots * 256) raw[i] = 0;
+      for (long long i = (long long)slot * 256 + tid; i < a.g.raw_fs; i += (long long)a.emit_slots * 256) rawf[i] = 0;
     return;
   }
   uint8_t *out = a.out + (long long)f * a.g.out_cap;
   const long long nchmax = emit_chunks(a.g);
-  const unsigned long long nbits = a.scan_bits[f * 3 + comp], nbytes = nbits >> 3;
-  if (zero && slot == 0 && tid < 2) {  // words past the last whole byte (the pad byte's bits)
-    const unsigned long long w = ((nbytes + 3) >> 2) + tid;
-    if (w < ((nbits + 31) >> 5)) raw[w] = 0;
+  long long nch[3];
+#pragma unroll
+  for (int comp = 0; comp < 3; comp++) {
+    const unsigned long long nbits = a.scan_bits[f * 3 + comp], nbytes = nbits >> 3;
+    nch[comp] = (long long)((nbytes + EMIT_CH - 1) / EMIT_CH);
+    if (zero && slot == 0 && tid < 2) {  // words past the last whole byte (the pad byte's bits)
+      const unsigned long long w = ((nbytes + 3) >> 2) + tid;
+      if (w < ((nbits + 31) >> 5)) ((uint32_t *)scan_raw(a, f, comp))[w] = 0;
+    }
   }
-  const long long nch = (long long)((nbytes + EMIT_CH - 1) / EMIT_CH);
-  const uint32_t *cnt = a.ffc + (long long)fc * nchmax;
-  const uint32_t *offs = a.choff + (long long)fc * nchmax;
   constexpr int WPW = EMIT_CH / 16;  // stream words per wave
-  for (long long c = slot; c < nch; c += a.emit_slots) {
+  // the frame's chunks, scan after scan, dealt round-robin to its workgroups
+  for (long long i = slot; i < nch[0] + nch[1] + nch[2]; i += a.emit_slots) {
+    const int comp = i < nch[0] ? 0 : (i < nch[0] + nch[1] ? 1 : 2);
+    const long long c = i - (comp == 0 ? 0 : (comp == 1 ? nch[0] : nch[0] + nch[1]));
+    const unsigned long long nbytes = a.scan_bits[f * 3 + comp] >> 3;
+    uint32_t *raw = (uint32_t *)scan_raw(a, f, comp);
+    const uint32_t *cnt = a.ffc + (long long)(f * 3 + comp) * nchmax;
+    const uint32_t *offs = a.choff + (long long)(f * 3 + comp) * nchmax;
     const unsigned long long cb = (unsigned long long)c * EMIT_CH;
     const unsigned long long o0 = offs[c];
     const int tot = (int)cnt[c];
@@ -3648,9 +3664,9 @@ hipError_t launch_seam_fix(const EntArgs &a, hipStream_t s) {
 hipError_t launch_emit(const EntArgs &a0, hipStream_t s) {
   EntArgs a = a0;
   if (a.emit_slots < 1) a.emit_slots = EMIT_SLOTS;
-  hipLaunchKernelGGL(k_emit_count, dim3(a.nframes * 3 * a.emit_slots), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_emit_count, dim3(a.nframes * a.emit_slots), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_emit_scan, dim3(a.nframes), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_emit_write, dim3(a.nframes * 3 * a.emit_slots), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_emit_write, dim3(a.nframes * a.emit_slots), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_gather_regions(uint8_t *dst, long long slot_bytes, int pitch, const uint8_t *src,
