@@ -411,6 +411,7 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
   HIP_TRY(dalloc(&b->d_replays, 1));
   HIP_TRY(dalloc(&b->d_ffc, F * 3 * emit_chunks(g)));
   HIP_TRY(dalloc(&b->d_choff, F * 3 * emit_chunks(g)));
+  HIP_TRY(hipMemsetAsync(b->d_ffc, 0, sizeof(uint32_t) * F * 3 * emit_chunks(g), b->stream));  // (ff_pack adds)
   HIP_TRY(hipMemsetAsync(b->d_replays, 0, sizeof(unsigned), b->stream));
   HIP_TRY(dalloc(&b->d_fdims, F));
   b->h_fdims.assign((size_t)F, make_int2(w, h));
@@ -787,6 +788,10 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   static const int seam_env = getenv("MIJ_SEAM") ? atoi(getenv("MIJ_SEAM")) : 1;
   if (seam_env && b->d_seam) {
     a.seam = b->d_seam + (long long)f0 * ((b->g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((b->g.nsc + PACK_SEGS - 1) / PACK_SEGS));
+    // the 0xFF bytes of every emit chunk counted as the words are stored
+    // (no k_emit_count pass over the scan words; A/B: MIJ_FF_PACK=0)
+    static const int ffp_env = getenv("MIJ_FF_PACK") ? atoi(getenv("MIJ_FF_PACK")) : 1;
+    a.ff_pack = ffp_env;
     b->raw_dirty = std::max(b->raw_dirty, f0 + nframes);
   } else if (b->raw_dirty) {
     HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->raw_dirty * b->g.raw_fs, st));

@@ -2549,13 +2549,32 @@ __device__ __forceinline__ void put_bits64_win(uint32_t *buf, uint32_t pos, unsi
   if (off + len > 64 && w + 2 >= wl && w + 2 < wh) atomicOr(&buf[w + 2 - wl], __builtin_amdgcn_alignbit(lo, 0u, off));
 }
 
+// 0xFF bytes among the first `lim` (0..4) bytes of a big-endian stream word
+__device__ __forceinline__ int ff_bytes(uint32_t w, int lim) {
+  const uint32_t x = ~w;
+  const uint32_t t = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // 0x80 per zero byte of x
+  const uint32_t keep = lim >= 4 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (8 * lim));
+  return __popc(t & keep);
+}
+
+// ff_pack: the 0xFF bytes of stream word W (bytes past the scan's whole bytes
+// nb do not count: the pad byte is written apart, never stuffed)
+__device__ __forceinline__ int ff_word(uint32_t v, uint32_t W, uint32_t nb) {
+  const uint32_t b = 4 * W;
+  return b >= nb ? 0 : ff_bytes(v, (int)min(nb - b, 4u));
+}
+constexpr int EMIT_CW = EMIT_CH / 4;  // stream words per emit chunk
+
 // PW: the LDS window in words (PACK_WORDS; high-quality batches, whose groups
 // outgrow it, get a double window -- fewer groups per CU, but no group on the
 // window-by-window path)
 #ifndef MIJ_PACK_WIDE_WORDS
 #define MIJ_PACK_WIDE_WORDS 6144
 #endif
-template <int PW>
+// FF: seam mode with the 0xFF bytes counted as the words are stored
+// (EntArgs::ff_pack; a compile-time variant: at 79 VGPRs the runtime checks
+// of both modes spilled)
+template <int PW, bool FF>
 __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
   __shared__ uint32_t buf[PW];
   __shared__ uint32_t tab[2 * 256];
@@ -2563,8 +2582,12 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
   __shared__ unsigned long long s_prefix;
   __shared__ uint32_t s_total;
   __shared__ int s_ticket;
+  constexpr int FFN = PW / EMIT_CW + 2;  // emit chunks one window's words can touch
+  __shared__ uint32_t s_ff[FFN];         // ff_pack: 0xFF bytes per chunk of the window
+  __shared__ uint32_t s_ffnb;            // ff_pack: the scan's whole bytes (its last group), else all
   const Geom &G = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (FF && tid < FFN) s_ff[tid] = 0;
 #ifdef MIJ_K1_DIAG
   unsigned long long tstamp[4];
 #define LB_STAMP(k) tstamp[k] = __builtin_amdgcn_s_memrealtime()
@@ -2752,6 +2775,7 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
       __hip_atomic_store(&stt[gid], LB_INC | (prefix + gbits), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (q == nq - 1) a.scan_bits[f * 3 + comp] = prefix + gbits;
       s_prefix = prefix;
+      if (FF) s_ffnb = q == nq - 1 ? (uint32_t)((prefix + gbits) >> 3) : ~0u;
     }
   };
   // ---- 3. pack the group's tokens.  A group that fits one LDS window (all
@@ -2770,6 +2794,13 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
       n = 0;
     }
     return gbase >> 5;
+  };
+  // ff_pack: a stored word's 0xFF bytes counted per emit chunk (c0: the
+  // chunk of the window's first word; nb: the scan's whole bytes, known to
+  // its last group, else all)
+  auto ff_add = [&](uint32_t v, uint32_t W, uint32_t c0) {
+    const int c = ff_word(v, W, s_ffnb);
+    if (c) atomicAdd(&s_ff[W / EMIT_CW - c0], (uint32_t)c);
   };
   uint32_t boff = 0, nw = ((gbits + 31) >> 5) + 1;  // relative: one spare word for the shift
   unsigned long long gw = 0;
@@ -2895,27 +2926,41 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
       uint32_t *raw = raw_scan + gw;
       // the edge words may be shared with the neighbouring groups: OR (onto
       // zero), or in seam mode (EntArgs::seam) the first word to the side
+      const uint32_t c0 = (uint32_t)gw / EMIT_CW;
       for (uint32_t i = tid; i < n; i += LB_THREADS) {
         const uint32_t v = __builtin_amdgcn_alignbit(i ? buf[i - 1] : 0u, buf[i], sh);
-        if (a.seam) {  // every word stored whole; a shared first word goes to the seam
-          if (i == 0 && sh) a.seam[gid] = v;
-          else raw[i] = v;
+        if (FF || a.seam) {  // every word stored whole; a shared first word goes to the seam
+          if (i == 0 && sh) {
+            a.seam[gid] = v;
+          } else {
+            raw[i] = v;
+            if (FF) ff_add(v, (uint32_t)gw + i, c0);
+          }
         } else if (i == 0 || i == n - 1) atomicOr(&raw[i], v);
         else raw[i] = v;
       }
     } else {
       __syncthreads();
       uint32_t *raw = raw_scan + gw;
+      const uint32_t c0 = ((uint32_t)gw + w0) / EMIT_CW;
       for (uint32_t i = tid; i < wn; i += LB_THREADS) {
         const uint32_t wi = w0 + i;
-        if (a.seam) {
-          if (wi == 0 && boff) a.seam[gid] = buf[i];
-          else raw[wi] = buf[i];
+        if (FF || a.seam) {
+          if (wi == 0 && boff) {
+            a.seam[gid] = buf[i];
+          } else {
+            raw[wi] = buf[i];
+            if (FF) ff_add(buf[i], (uint32_t)gw + wi, c0);
+          }
         } else if (wi == 0 || wi == nw - 1) atomicOr(&raw[wi], buf[i]);
         else raw[wi] = buf[i];
       }
     }
     __syncthreads();
+    if (FF && tid < FFN && s_ff[tid]) {  // the window's chunk counts out, zeroed for the next
+      atomicAdd(&a.ffc[(long long)(f * 3 + comp) * emit_chunks(G) + ((uint32_t)gw + (rel ? 0u : w0)) / EMIT_CW + tid], s_ff[tid]);
+      s_ff[tid] = 0;
+    }
   }
 #ifdef MIJ_K1_DIAG
   LB_STAMP(3);
@@ -2944,7 +2989,12 @@ __global__ __launch_bounds__(256) void k_seam_fix(EntArgs a) {
   const unsigned long long start = a.pack_state[g - 1] & LB_VAL;  // the group's first bit
   if (!(start & 31)) return;
   uint32_t *raw = a.raw + (long long)f * G.raw_fs + (comp == 0 ? 0 : G.raw_words[0] + (comp == 2 ? G.raw_words[1] : 0));
-  atomicOr(&raw[start >> 5], a.seam[g]);
+  const uint32_t sv = a.seam[g], old = atomicOr(&raw[start >> 5], sv);
+  if (a.ff_pack) {  // the 0xFF bytes the OR adds (an OR never removes one, so the adds telescope)
+    const uint32_t W = (uint32_t)(start >> 5), nb = (uint32_t)(a.scan_bits[f * 3 + comp] >> 3);
+    const int d = ff_word(old | sv, W, nb) - ff_word(old, W, nb);
+    if (d) atomicAdd(&a.ffc[(long long)(f * 3 + comp) * emit_chunks(G) + W / EMIT_CW], (uint32_t)d);
+  }
 }
 
 // ===========================================================================
@@ -2975,13 +3025,6 @@ __device__ __forceinline__ const uint32_t *scan_raw(const EntArgs &a, int f, int
          (comp == 0 ? 0 : a.g.raw_words[0] + (comp == 2 ? a.g.raw_words[1] : 0));
 }
 
-// 0xFF bytes among the first `lim` (0..4) bytes of a big-endian stream word
-__device__ __forceinline__ int ff_bytes(uint32_t w, int lim) {
-  const uint32_t x = ~w;
-  const uint32_t t = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // 0x80 per zero byte of x
-  const uint32_t keep = lim >= 4 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (8 * lim));
-  return __popc(t & keep);
-}
 
 __device__ __forceinline__ int block_sum256(int v, int *red) {
   for (int off = 32; off; off >>= 1) v += __shfl_xor(v, off);
@@ -3149,6 +3192,9 @@ __global__ __launch_bounds__(256) void k_emit_write(EntArgs a) {
     uint32_t *rawf = a.raw + (long long)f * a.g.raw_fs;
     if (zero)
       for (long long i = (long long)slot * 256 + tid; i < a.g.raw_fs; i += (long long)a.emit_slots * 256) rawf[i] = 0;
+    // the chunk counts left zeroed (ff_pack adds to them)
+    for (long long i = (long long)slot * 256 + tid; i < 3 * emit_chunks(a.g); i += (long long)a.emit_slots * 256)
+      a.ffc[(long long)f * 3 * emit_chunks(a.g) + i] = 0;
     return;
   }
   uint8_t *out = a.out + (long long)f * a.g.out_cap;
@@ -3200,6 +3246,7 @@ __global__ __launch_bounds__(256) void k_emit_write(EntArgs a) {
     for (int off = 32; off; off >>= 1) wcnt += __shfl_xor(wcnt, off);
     if (lane == 0) red[wave] = wcnt;
     __syncthreads();
+    if (tid == 0) a.ffc[(long long)(f * 3 + comp) * nchmax + c] = 0;  // read: left zeroed (ff_pack adds)
     int carry = wave * 4 * WPW;
     for (int q = 0; q < wave; q++) carry += red[q];
 #pragma unroll
@@ -3651,8 +3698,11 @@ hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s, bool state_zeroed) {
     if (e == hipSuccess) e = hipMemsetAsync(a.pack_ticket, 0, sizeof(unsigned) * 3 * a.nframes, s);
     if (e != hipSuccess) return e;
   }
-  if (a.pack_wide) hipLaunchKernelGGL(k_pack_lb<MIJ_PACK_WIDE_WORDS>, dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
-  else hipLaunchKernelGGL(k_pack_lb<PACK_WORDS>, dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
+  const bool ff = a.ff_pack && a.seam;
+  if (a.pack_wide && ff) hipLaunchKernelGGL((k_pack_lb<MIJ_PACK_WIDE_WORDS, true>), dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
+  else if (a.pack_wide) hipLaunchKernelGGL((k_pack_lb<MIJ_PACK_WIDE_WORDS, false>), dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
+  else if (ff) hipLaunchKernelGGL((k_pack_lb<PACK_WORDS, true>), dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
+  else hipLaunchKernelGGL((k_pack_lb<PACK_WORDS, false>), dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_seam_fix(const EntArgs &a, hipStream_t s) {
@@ -3664,7 +3714,8 @@ hipError_t launch_seam_fix(const EntArgs &a, hipStream_t s) {
 hipError_t launch_emit(const EntArgs &a0, hipStream_t s) {
   EntArgs a = a0;
   if (a.emit_slots < 1) a.emit_slots = EMIT_SLOTS;
-  hipLaunchKernelGGL(k_emit_count, dim3(a.nframes * a.emit_slots), dim3(256), 0, s, a);
+  if (!a.ff_pack)  // (ff_pack: the packing counted the 0xFF bytes)
+    hipLaunchKernelGGL(k_emit_count, dim3(a.nframes * a.emit_slots), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_emit_scan, dim3(a.nframes), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_emit_write, dim3(a.nframes * a.emit_slots), dim3(256), 0, s, a);
   return hipGetLastError();
