@@ -2574,8 +2574,24 @@ constexpr int EMIT_CW = EMIT_CH / 4;  // stream words per emit chunk
 // FF: seam mode with the 0xFF bytes counted as the words are stored
 // (EntArgs::ff_pack; a compile-time variant: at 79 VGPRs the runtime checks
 // of both modes spilled)
+// The wide-window variant (high quality: segments of several hundred tokens)
+// loads MIJ_LB_UNR_WIDE steps past the registers per round (one memory round
+// trip for them instead of one each), with the VGPRs of MIJ_LB_OCC_WIDE groups
+// per CU
+#ifndef MIJ_LB_UNR
+#define MIJ_LB_UNR 1
+#endif
+#ifndef MIJ_LB_UNR_WIDE
+#define MIJ_LB_UNR_WIDE 2
+#endif
+#ifndef MIJ_LB_OCC_WIDE
+#define MIJ_LB_OCC_WIDE 5
+#endif
+template <int PW>
+constexpr int lb_occ() { return PW > PACK_WORDS ? MIJ_LB_OCC_WIDE : MIJ_LB_OCC; }
 template <int PW, bool FF>
-__global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
+__global__ __launch_bounds__(LB_THREADS, lb_occ<PW>()) void k_pack_lb(EntArgs a) {
+  constexpr int UNR = PW > PACK_WORDS ? MIJ_LB_UNR_WIDE : MIJ_LB_UNR;
   __shared__ uint32_t buf[PW];
   __shared__ uint32_t tab[2 * 256];
   __shared__ uint32_t s_bits[PACK_SEGS], s_off[PACK_SEGS];
@@ -2701,13 +2717,17 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
   // row per round, their loads issued together (one memory round trip per
   // round, not per segment and step)
   const int ntmax = max(max(nt[0], nt[1]), max(nt[2], nt[3]));  // row-uniform
-  for (int i0 = 64 * nst; i0 < ntmax; i0 += 64) {
-    u4v tr[LB_SEGS_PER_ROW];
+  for (int i0 = 64 * nst; i0 < ntmax; i0 += 64 * UNR) {
+    u4v tr[UNR][LB_SEGS_PER_ROW];
 #pragma unroll
-    for (int k = 0; k < LB_SEGS_PER_ROW; k++) tr[k] = load_step(k, i0);
+    for (int u = 0; u < UNR; u++)
 #pragma unroll
-    for (int k = 0; k < LB_SEGS_PER_ROW; k++)
-      if (i0 < nt[k]) bk[k] += step_bits(tr[k], nt[k] - i0 - 4 * sub);
+      for (int k = 0; k < LB_SEGS_PER_ROW; k++) tr[u][k] = load_step(k, i0 + 64 * u);
+#pragma unroll
+    for (int u = 0; u < UNR; u++)
+#pragma unroll
+      for (int k = 0; k < LB_SEGS_PER_ROW; k++)
+        if (i0 + 64 * u < nt[k]) bk[k] += step_bits(tr[u][k], nt[k] - (i0 + 64 * u) - 4 * sub);
   }
 #pragma unroll
   for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
@@ -2879,13 +2899,17 @@ __global__ __launch_bounds__(LB_THREADS, MIJ_LB_OCC) void k_pack_lb(EntArgs a) {
       }
       // the steps past the registers again in rounds (segments beyond the
       // group have nt = 0)
-      for (int i0 = 64 * nst; i0 < ntmax; i0 += 64) {
-        u4v tr[LB_SEGS_PER_ROW];
+      for (int i0 = 64 * nst; i0 < ntmax; i0 += 64 * UNR) {
+        u4v tr[UNR][LB_SEGS_PER_ROW];
 #pragma unroll
-        for (int k = 0; k < LB_SEGS_PER_ROW; k++) tr[k] = load_step(k, i0);
+        for (int u = 0; u < UNR; u++)
 #pragma unroll
-        for (int k = 0; k < LB_SEGS_PER_ROW; k++)
-          if (i0 < nt[k]) fast_step(tr[k], nt[k] - i0 - 4 * sub, pos0[k]);
+          for (int k = 0; k < LB_SEGS_PER_ROW; k++) tr[u][k] = load_step(k, i0 + 64 * u);
+#pragma unroll
+        for (int u = 0; u < UNR; u++)
+#pragma unroll
+          for (int k = 0; k < LB_SEGS_PER_ROW; k++)
+            if (i0 + 64 * u < nt[k]) fast_step(tr[u][k], nt[k] - (i0 + 64 * u) - 4 * sub, pos0[k]);
       }
     }
     if (__ballot(slow)) {  // second pass over this wave's rows, tokens reloaded
