@@ -23,7 +23,9 @@ done <<'G'
 GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE
 GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES
 G
+# the bench line (rocprofv3 writes its own lines after it): the workload
+# the counters belong to, so bench.py attaches them only to a matching run
 python3 -c "
-import json; d=json.loads(open('$out/p1.log').read().strip().splitlines()[-1])
-json.dump(d['config'], open('$out/config.json','w'))"
+import json; d=json.loads([l for l in open('$out/p1.log').read().splitlines() if l.startswith('{')][-1])
+json.dump(d['config'], open('$out/config.json','w'))" || { echo "no bench line in pass 1"; exit 1; }
 python3 scripts/util.py "$out" "$out/util.json"

@@ -36,3 +36,16 @@ def test_util_counters_require_matching_workload(tmp_path, monkeypatch):
     # a util.json without a recorded workload is never attached
     (d / "util.json").write_text(json.dumps({"kernels": k}))
     assert b.util_counters("k_mcu_dct<2>", dict(cfg)) == (None, None)
+
+
+def test_committed_profiles_attach_to_the_default_bench():
+    """The newest committed util.json and traffic.json record the workload
+    they were measured on, and it is the default bench's (config 3), so the
+    driver's bench line carries mfma_util / valu_util and PMC traffic."""
+    b = _bench()
+    cfg = {"width": 3840, "height": 2160, "frames_per_gpu": 256, "quality": 50, "mode": "encode",
+           "pipeline": "fused"}
+    u, src = b.util_counters("k_mcu_dct<2>", dict(cfg))
+    assert u is not None, "no committed util.json matches the default workload"
+    assert 0 < u["mfma_util"] < 1 and 0 < u["valu_util"] < 1
+    assert b.pmc_traffic("k_mcu_dct<2>", dict(cfg))[0] is not None
