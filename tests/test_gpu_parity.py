@@ -354,7 +354,7 @@ def _luma_group_bits(Y, tabs, W, H, group, tiles_x):
 def test_pack_window_paths_in_one_scan(q):
     """k_pack_lb's two placement paths in one scan (both at Q=100, the
     single-window one alone at Q=50): a pack group whose bits fit one LDS
-    window (PACK_WORDS = 4096 words) is placed relative to its own
+    window (4096 words; the 6144-word variant at Q >= 85) is placed relative to its own
     first bit and stored after the look-back; a wider one (noise rows: its
     bits are asserted to exceed the window) takes the look-back first and is
     packed window by window at absolute offsets (put_bits64_win, tokens
@@ -369,10 +369,11 @@ def test_pack_window_paths_in_one_scan(q):
     # frame 0's first luma group (noise) is wider than one window at Q=100
     # (516k bits) and fits one at Q=50 (124k); frame 1's first (flat) fits
     Y, _, _, tabs, _ = O.cref_stages(frames[0], q)
-    wide = _luma_group_bits(Y, tabs, W, H, 0, (W + 127) // 128) > 4096 * 32
+    window = (6144 if q >= 85 else 4096) * 32  # the library's window at this quality (ent_args: pack_wide)
+    wide = _luma_group_bits(Y, tabs, W, H, 0, (W + 127) // 128) > window
     assert wide == (q == 100)
     Y1, _, _, tabs1, _ = O.cref_stages(frames[1], q)
-    assert _luma_group_bits(Y1, tabs1, W, H, 0, (W + 127) // 128) < 4096 * 32
+    assert _luma_group_bits(Y1, tabs1, W, H, 0, (W + 127) // 128) < window
     b = mijpeg.Batch(W, H, 2, q)
     b.upload(frames)
     b.encode(2)
