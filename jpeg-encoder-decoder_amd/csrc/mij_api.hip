@@ -22,6 +22,7 @@ hipError_t launch_colour_lut(uint32_t *lut, hipStream_t s);
 hipError_t launch_k1(const K1Args &a, int grid, int mode, hipStream_t s);
 hipError_t launch_fix_blocks(const K1Args &a, hipStream_t s);
 hipError_t launch_seg_dc(const EntArgs &a, hipStream_t s);
+hipError_t launch_segdc_actab(const EntArgs &a, hipStream_t s);
 hipError_t launch_dc_diff(int16_t *coef, const int16_t *dc, const Geom &g, int nframes,
                           const int2 *fd, hipStream_t s);
 hipError_t launch_tables(const EntArgs &a, hipStream_t s);
@@ -703,10 +704,22 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   // frame, 0.11 ms of a config-3 launch against a few us spread over the chip)
   static const bool segdc_fused = getenv("MIJ_SEGDC_FUSED") && atoi(getenv("MIJ_SEGDC_FUSED"));
   a.seg_dc = dc_fix && !tables_given && segdc_fused ? 1 | segdc_dbg : 0;
-  if (dc_fix && !a.seg_dc) HIP_TRY(launch_seg_dc(a, st));
-  if (t) HIP_TRY(hipEventRecord(b->ev[4], st));
   // diagnostics (MIJ_TAB_TIME with the diag build): per-wave phase clocks of k_tables
   static const bool ttime = getenv("MIJ_TAB_TIME") != nullptr;
+  // the AC tables beside the segment DCs (they need only K1's histograms),
+  // the DC tables after (A/B: MIJ_ACTAB=0; profiles/r03/qsweep/actab_ab.txt:
+  // segment DCs + tables 0.077 -> 0.062 ms at config 3 Q=50, 0.102 -> 0.075
+  // at Q=90).  Not on small batches: one frame's four tables take as long
+  // as its AC tables, and the DC tables after them add 10 us.
+  static const int actab_env = getenv("MIJ_ACTAB") ? atoi(getenv("MIJ_ACTAB")) : 1;
+  const bool actab = dc_fix && !a.seg_dc && !tables_given && !ttime && actab_env && nframes >= 16;
+  if (actab) {
+    a.zero_pack = 1;  // (the AC workgroups zero the counts they read)
+    HIP_TRY(launch_segdc_actab(a, st));
+  } else if (dc_fix && !a.seg_dc) {
+    HIP_TRY(launch_seg_dc(a, st));
+  }
+  if (t) HIP_TRY(hipEventRecord(b->ev[4], st));
   if (!tables_given && ttime) {
     EntArgs at = a;
     const size_t nt = (size_t)nframes * 4 * 10;
@@ -774,7 +787,9 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
     }
   } else if (!tables_given) {
     a.zero_pack = !a.seg_dc;  // one wave per table: it zeroes the pack state too
+    a.tab_dc_only = actab;
     HIP_TRY(launch_tables(a, st));
+    a.tab_dc_only = 0;
   }
   b->hist_zero_after = (f0 == 0 && a.zero_pack) ? nframes : 0;
   if (t) HIP_TRY(hipEventRecord(b->ev[5], st));

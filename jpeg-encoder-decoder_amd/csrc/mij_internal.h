@@ -208,6 +208,7 @@ struct EntArgs {
   int pack_wide;                   // k_pack_lb with a 2 * PACK_WORDS window (high quality)
   int zero_pack;                   // k_tables_1w also zeroes k_pack_lb's look-back words and tickets
   int seg_dc;                      // k_tables: compute the segment-first DC tokens first (k_seg_dc)
+  int tab_dc_only;                 // k_tables_1w: the DC tables only (k_segdc_actab built the AC ones)
   int ff_pack;                     // seam mode: k_pack_lb / k_seam_fix count the 0xFF bytes of every
                                    // EMIT_CH chunk into ffc as they store (k_emit_count not run;
                                    // k_emit_write leaves the counts zeroed)

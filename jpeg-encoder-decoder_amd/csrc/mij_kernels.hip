@@ -1576,11 +1576,12 @@ __device__ __forceinline__ void seg_dc_store(const EntArgs &a, int f, int s, con
 #endif
 // (MIJ_SEGDC_WG 64: one-wave workgroups, which fit beside a running 10-wave
 // K1 -- 256-thread ones wait for it to end; profiles/r03/overlap_trace.txt)
-__global__ __launch_bounds__(MIJ_SEGDC_WG) void k_seg_dc(EntArgs a) {
-  __shared__ uint32_t hs[32 * 32];
+// one workgroup's share (workgroup b of the launch's segment DCs; hs: 32 x
+// 32 words of LDS)
+__device__ __forceinline__ void seg_dc_block(const EntArgs &a, int b, uint32_t *hs) {
   const int per = (a.g.nseg + MIJ_SEGDC_WG - 1) / MIJ_SEGDC_WG;
-  const int f = blockIdx.x / per;
-  const int s = (blockIdx.x - f * per) * MIJ_SEGDC_WG + threadIdx.x;
+  const int f = b / per;
+  const int s = (b - f * per) * MIJ_SEGDC_WG + threadIdx.x;
   for (int i = threadIdx.x; i < 32 * 32; i += MIJ_SEGDC_WG) hs[i] = 0;
   __syncthreads();
   if (s < a.g.nseg) seg_dc_store(a, f, s, seg_dc_load(a, frame_geom(a.g, a.fdims, f), f, s), hs, threadIdx.x & 63);
@@ -1591,6 +1592,11 @@ __global__ __launch_bounds__(MIJ_SEGDC_WG) void k_seg_dc(EntArgs a) {
     if (v)
       atomicAdd(&a.hist[((long long)f * 4 + (threadIdx.x >= 16 ? 2 : 0)) * 257 + (threadIdx.x & 15)], v);
   }
+}
+
+__global__ __launch_bounds__(MIJ_SEGDC_WG) void k_seg_dc(EntArgs a) {
+  __shared__ uint32_t hs[32 * 32];
+  seg_dc_block(a, blockIdx.x, hs);
 }
 
 
@@ -2324,12 +2330,15 @@ __global__ __launch_bounds__(256) void k_tables(EntArgs a) {
 // The same tables one wave (workgroup) per table when the segment DCs ran on
 // their own (k_seg_dc): 14 KB of LDS per workgroup instead of 61 KB, so the
 // tables of one sub-batch fit beside the next sub-batch's K1 (overlap path).
+// (EntArgs::tab_dc_only: the two DC tables of each frame only, k_segdc_actab
+// built the AC tables)
 __global__ __launch_bounds__(64) void k_tables_1w(EntArgs a) {
   __shared__ TabScratch2 S;
-  const int f = blockIdx.x >> 2, t = blockIdx.x & 3, lane = threadIdx.x;
+  const int nt = a.tab_dc_only ? 2 : 4, lane = threadIdx.x;
+  const int f = blockIdx.x / nt, idx = blockIdx.x - f * nt, t = a.tab_dc_only ? 2 * idx : idx;
   if (a.zero_pack) {  // (k_pack_lb runs next: its state, zeroed here instead of two fills)
     const long long gpf = (a.g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((a.g.nsc + PACK_SEGS - 1) / PACK_SEGS);
-    for (long long i = 64 * t + lane; i < gpf; i += 256) a.pack_state[f * gpf + i] = 0;
+    for (long long i = 64 * idx + lane; i < gpf; i += 64 * nt) a.pack_state[f * gpf + i] = 0;
     if (t == 0 && lane < 3) a.pack_ticket[f * 3 + lane] = 0;
   }
 #ifdef MIJ_K1_DIAG
@@ -2339,6 +2348,27 @@ __global__ __launch_bounds__(64) void k_tables_1w(EntArgs a) {
                     (uint32_t *)a.ehuf + ((long long)f * 4 + t) * 256, &S, lane, a.err + f,
                     a.dbg ? a.dbg + ((long long)f * 4 + t) * 10 : nullptr);
   if (a.zero_pack)  // the counts are read: left zeroed for the next K1 (no fill before it)
+    for (int i = lane; i < 257; i += 64) a.hist[((long long)f * 4 + t) * 257 + i] = 0;
+}
+
+// The segment-first DCs (k_seg_dc) and, in the first 2 x nframes
+// workgroups, the frames' two AC tables, which do not depend on them: the
+// luma AC table's merge (the long pole of the table stage) runs beside the
+// segment DCs, and k_tables_1w builds only the DC tables after
+// (EntArgs::tab_dc_only).  One wave of an AC workgroup works.
+__global__ __launch_bounds__(MIJ_SEGDC_WG) void k_segdc_actab(EntArgs a) {
+  __shared__ TabScratch2 S;
+  __shared__ uint32_t hs[32 * 32];
+  const int nac = 2 * a.nframes;
+  if ((int)blockIdx.x >= nac) {
+    seg_dc_block(a, (int)blockIdx.x - nac, hs);
+    return;
+  }
+  if (threadIdx.x >= 64) return;
+  const int f = blockIdx.x >> 1, t = 1 + 2 * (blockIdx.x & 1), lane = threadIdx.x;
+  build_table_wave2(a.hist + ((long long)f * 4 + t) * 257, nullptr, (HuffCode *)a.hc + (long long)f * 4 + t,
+                    (uint32_t *)a.ehuf + ((long long)f * 4 + t) * 256, &S, lane, a.err + f, nullptr);
+  if (a.zero_pack)  // the counts are read: left zeroed for the next K1
     for (int i = lane; i < 257; i += 64) a.hist[((long long)f * 4 + t) * 257 + i] = 0;
 }
 
@@ -3637,9 +3667,14 @@ hipError_t launch_dc_diff(int16_t *coef, const int16_t *dc, const Geom &g, int n
                      nframes, fd);
   return hipGetLastError();
 }
+hipError_t launch_segdc_actab(const EntArgs &a, hipStream_t s) {
+  hipLaunchKernelGGL(k_segdc_actab, dim3(a.nframes * (2 + (a.g.nseg + MIJ_SEGDC_WG - 1) / MIJ_SEGDC_WG)),
+                     dim3(MIJ_SEGDC_WG), 0, s, a);
+  return hipGetLastError();
+}
 hipError_t launch_tables(const EntArgs &a, hipStream_t s) {
   if (!a.seg_dc) {
-    hipLaunchKernelGGL(k_tables_1w, dim3(a.nframes * 4), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_tables_1w, dim3(a.nframes * (a.tab_dc_only ? 2 : 4)), dim3(64), 0, s, a);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_tables, dim3(a.nframes), dim3(256), 0, s, a);
