@@ -596,10 +596,24 @@ constexpr uint32_t TOK_AC = 1u << 10;
 // a segment's first block depends on the previous segment: with first_pred
 // the caller supplies that block's predecessor DC (pred0), otherwise (token
 // variant fed from pixels) it is left for k_seg_dc.
+// token i of a frame's streams (MIJ_K1_TOKOFF: a wave-uniform frame base and
+// a 32-bit byte offset, so the store takes the SGPR-base form instead of a
+// 64-bit address add per token; A/B on config 3, 3 rounds: K1 3.280 -> 3.262
+// ms, profiles/r03/probe/k1_tokoff_ab.txt)
+#ifndef MIJ_K1_TOKOFF
+#define MIJ_K1_TOKOFF 1
+#endif
+__device__ __forceinline__ uint32_t &tok_at(uint32_t *base, uint32_t i) {
+#if MIJ_K1_TOKOFF
+  return *(uint32_t *)((char *)base + (i << 2));
+#else
+  return base[i];
+#endif
+}
 __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g, int bcol,
                                             bool valid, bool chroma, bool dc_diffed,
                                             bool first_pred, int pred0,
-                                            uint32_t *segtok, uint32_t *tok0, uint32_t *segcnt, uint32_t *hDC,
+                                            uint32_t *segtok, uint32_t segoff, uint32_t *tok0, uint32_t *segcnt, uint32_t *hDC,
                                             uint32_t *hAC, int16_t (*st)[16], int kflags = 0) {
   u4v c0, c1;
 #pragma unroll
@@ -664,10 +678,10 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
         // segment: written there it is a whole-line store, not a lone word)
         const uint32_t tk = (uint32_t)cls | (mag_bits(diff, cls) << 16);
         if (pos == 0) *tok0 = tk;
-        else segtok[base] = tk;
+        else tok_at(segtok, segoff + base) = tk;
         atomicAdd(&hDC[cls], 1u);
       }
-      if (eob) segtok[base + n - 1] = TOK_AC;
+      if (eob) tok_at(segtok, segoff + base + n - 1) = TOK_AC;
     }
   }
   {  // one histogram update for all of the wave's EOBs
@@ -693,7 +707,7 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
       const uint32_t cls = 32u - (uint32_t)__builtin_clz(a);  // a != 0
       const uint32_t mag = __builtin_amdgcn_ubfe((uint32_t)(cz + (cz >> 31)), 0u, cls);
       const uint32_t t = ((uint32_t)run << 4) | cls | TOK_AC;
-      if (!(kflags & K1F_NO_TOKSTORE)) segtok[(uint32_t)(base + 1 + rank)] = t | (mag << 16);
+      if (!(kflags & K1F_NO_TOKSTORE)) tok_at(segtok, segoff + (uint32_t)(base + 1 + rank)) = t | (mag << 16);
       if (!(kflags & K1F_NO_HIST)) {
         atomicAdd(&hAC[t & 255u], 1u);
         if (run >= 16) atomicAdd(&hAC[0xF0], (unsigned)(run >> 4));
@@ -1101,7 +1115,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
                                   : (int)a.dc[(long long)p.f * G.nblk + blk - 1];
           }
           emit_tokens(o, lane, g, bcol, valid, comp == 1, !PIX && a.dc_diffed, first_pred, pred0,
-                      a.tok + fs * SEG_TOK, a.tok0 + fs,
+                      a.tok + (long long)p.f * G.nseg * SEG_TOK, (uint32_t)seg * SEG_TOK, a.tok0 + fs,
                       a.seg_ntok + fs, s_hdc[TOK ? slot : 0][comp][bcol & (HREP - 1)],
                       s_hac[TOK ? slot : 0][comp][bcol & (HREP - 1)],
                       s_st[TOK ? wave : 0], kflags);
