@@ -583,6 +583,9 @@ constexpr uint32_t TOK_AC = 1u << 10;
 #endif
 // N-tile of the token K1 before whose stores the next tile's DMA is awaited
 // (A/B: 0, 1 and 2 measured equal, 3.36-3.39 ms)
+#ifndef MIJ_K1_SFFBH
+#define MIJ_K1_SFFBH 1
+#endif
 #ifndef MIJ_K1_DMAWAIT_NT
 #define MIJ_K1_DMAWAIT_NT 0
 #endif
@@ -703,9 +706,18 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
     auto token = [&](int z, int rank, int zp) {
       const int cz = sl[z ^ zsw];
       const int run = z - zp - 1;
-      const uint32_t a = (uint32_t)max(cz, -cz);
-      const uint32_t cls = 32u - (uint32_t)__builtin_clz(a);  // a != 0
-      const uint32_t mag = __builtin_amdgcn_ubfe((uint32_t)(cz + (cz >> 31)), 0u, cls);
+      // m = cz, or ~|cz| when negative (its low cls bits are the magnitude
+      // bits, encoder.c:456-458); its leading sign bits (v_ffbh_i32) are
+      // clz(|cz|), so cls = 32 - ffbh_i32(m) (cz != 0: m is neither 0 nor -1)
+      const int m = cz + (cz >> 31);
+#if MIJ_K1_SFFBH
+      uint32_t lead;  // (no builtin; __builtin_clrsb lowers to four instructions)
+      asm("v_ffbh_i32 %0, %1" : "=v"(lead) : "v"(m));
+      const uint32_t cls = 32u - lead;
+#else
+      const uint32_t cls = 32u - (uint32_t)__builtin_clz((uint32_t)max(cz, -cz));
+#endif
+      const uint32_t mag = __builtin_amdgcn_ubfe((uint32_t)m, 0u, cls);
       const uint32_t t = ((uint32_t)run << 4) | cls | TOK_AC;
       if (!(kflags & K1F_NO_TOKSTORE)) tok_at(segtok, segoff + (uint32_t)(base + 1 + rank)) = t | (mag << 16);
       if (!(kflags & K1F_NO_HIST)) {
