@@ -583,6 +583,9 @@ constexpr uint32_t TOK_AC = 1u << 10;
 #endif
 // N-tile of the token K1 before whose stores the next tile's DMA is awaited
 // (A/B: 0, 1 and 2 measured equal, 3.36-3.39 ms)
+#ifndef MIJ_K1_TOKFMT
+#define MIJ_K1_TOKFMT 1
+#endif
 #ifndef MIJ_K1_SFFBH
 #define MIJ_K1_SFFBH 1
 #endif
@@ -718,12 +721,25 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
       const uint32_t cls = 32u - (uint32_t)__builtin_clz((uint32_t)max(cz, -cz));
 #endif
       const uint32_t mag = __builtin_amdgcn_ubfe((uint32_t)m, 0u, cls);
+#if MIJ_K1_TOKFMT
+      // run + 64 shifted by 4 is TOK_AC | run << 4 (run <= 62): one shift-or
+      // for the symbol word, one for the token (zp here: 63 - the previous
+      // set bit, so run + 64 = z + zp is one add)
+      const uint32_t runp = (uint32_t)(z + zp);
+      const uint32_t t = (runp << 4) | cls;
+      if (!(kflags & K1F_NO_TOKSTORE)) tok_at(segtok, segoff + (uint32_t)(base + 1 + rank)) = t | (mag << 16);
+      if (!(kflags & K1F_NO_HIST)) {
+        atomicAdd(&hAC[t & 255u], 1u);
+        if (runp >= 80u) atomicAdd(&hAC[0xF0], (runp - 64u) >> 4);
+      }
+#else
       const uint32_t t = ((uint32_t)run << 4) | cls | TOK_AC;
       if (!(kflags & K1F_NO_TOKSTORE)) tok_at(segtok, segoff + (uint32_t)(base + 1 + rank)) = t | (mag << 16);
       if (!(kflags & K1F_NO_HIST)) {
         atomicAdd(&hAC[t & 255u], 1u);
         if (run >= 16) atomicAdd(&hAC[0xF0], (unsigned)(run >> 4));
       }
+#endif
     };
     const uint32_t cm = 0x11111111u << g;
     const int rank_lo = __popc(Mlo), zp_lo = 31 - __clz((int)(Mlo | 1u));
@@ -742,16 +758,40 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
       else mhi &= mhi - 1u;
     }
 #else
+#if MIJ_K1_TOKFMT
+#define MIJ_BELOW(M, z) __builtin_amdgcn_ubfe((M), 0u, (uint32_t)(z))  // bits of M below z: one v_bfe
+#else
+#define MIJ_BELOW(M, z) ((M) & ((1u << (z)) - 1u))
+#endif
+#if MIJ_K1_TOKFMT
+    // (token's zp argument: 63 - the previous set bit)
     for (uint32_t m = Mlo & cm; m; m &= m - 1u) {
       const int z = __builtin_ctz(m);
-      const uint32_t bef = Mlo & ((1u << z) - 1u);
+      const uint32_t bef = MIJ_BELOW(Mlo, z);
+      token(z, __popc(bef), 32 + __clz((int)(bef | 1u)));
+    }
+    for (uint32_t m = Mhi & cm; m; m &= m - 1u) {
+      const int zz = __builtin_ctz(m);
+      const uint32_t bef = MIJ_BELOW(Mhi, zz);
+      // v_ffbh_u32 of 0 is ~0u: the min picks 63 - zp_lo exactly when no
+      // bit of the high half lies below zz (no compare and select)
+      uint32_t lz;
+      asm("v_ffbh_u32 %0, %1" : "=v"(lz) : "v"(bef));
+      token(32 + zz, rank_lo + __popc(bef), (int)min(lz, (uint32_t)(63 - zp_lo)));
+    }
+#else
+    for (uint32_t m = Mlo & cm; m; m &= m - 1u) {
+      const int z = __builtin_ctz(m);
+      const uint32_t bef = MIJ_BELOW(Mlo, z);
       token(z, __popc(bef), 31 - __clz((int)(bef | 1u)));
     }
     for (uint32_t m = Mhi & cm; m; m &= m - 1u) {
       const int zz = __builtin_ctz(m);
-      const uint32_t bef = Mhi & ((1u << zz) - 1u);
+      const uint32_t bef = MIJ_BELOW(Mhi, zz);
       token(32 + zz, rank_lo + __popc(bef), bef ? 63 - __clz((int)bef) : zp_lo);
     }
+#endif
+#undef MIJ_BELOW
 #endif
   }
   wave_lds_sync();
