@@ -35,7 +35,10 @@ constexpr int PACK_SEGS = MIJ_PACK_SEGS;          // segments per k_pack workgro
 constexpr int MAX_BLOCK_BITS = 1729;              // 28 DC + 63 * 27 AC bits
 // k_pack assembles a group in LDS windows of PACK_WORDS words; a group wider
 // than one window (only near worst-case entropy) is packed in several passes.
-constexpr int PACK_WORDS = 4096;
+#ifndef MIJ_PACK_WORDS
+#define MIJ_PACK_WORDS 4096
+#endif
+constexpr int PACK_WORDS = MIJ_PACK_WORDS;
 // k_pack_lb: tokens per lane loaded in one batch (16 lanes per segment)
 constexpr int PACK_BATCH = 16;
 // JFIF assembly: scans are written in EMIT_CH-byte chunks by EntArgs::
