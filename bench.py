@@ -76,6 +76,9 @@ def parse():
                     help="regions workload: rectangles per frame (main.c's diffDims holds up to 100)")
     ap.add_argument("--region-frame", default="1920x1080",
                     help="regions workload: the frame the rectangles are cut from")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=V",
+                    help="entropy-stage variant for A/B timing (mij_batch_set_option, "
+                         "include/mijpeg.h MIJ_OPT_*; same bytes), repeatable")
     ap.add_argument("--verify", type=int, default=-1,
                     help="frames re-checked against the oracle after timing (-1: every frame "
                          "of the batch; config3 checks each distinct content with the oracle and "
@@ -112,8 +115,15 @@ def run_config4(args, world, rank, local, dist):
     exchanges of sharding.encode_banded (last DCs, histograms, bit counts,
     packed words to rank 0 -- RCCL when the backend is nccl)."""
     W, H, n = 7680, 4320, args.frames4
-    gpu = 0 if dist is not None and dist.get_backend() != "nccl" else local
-    if dist is None:  # one rank: the word buffer stays in HBM (torch's runtime first)
+    backend = dist.get_backend() if dist is not None else "none"
+    gpu = 0 if backend == "gloo" else local
+    # device-resident protocol (mij_band_*_async, sharding.encode_banded_dev):
+    # collectives on device tensors -- RCCL, or one rank; with gloo (several
+    # ranks sharing one GPU) the same protocol with every collective staged
+    # through host memory (sharding.StagedExchange), unless
+    # MIJ_BAND_PROTOCOL=host asks for the host-array protocol (encode_banded)
+    on_dev = not (backend == "gloo" and os.environ.get("MIJ_BAND_PROTOCOL") == "host")
+    if on_dev and backend != "nccl":  # torch's HIP runtime first (dist_setup did it for nccl)
         import torch
         torch.cuda.set_device(gpu)
     r0, rows = sharding.band_rows(H, world, rank)
@@ -125,13 +135,12 @@ def run_config4(args, world, rank, local, dist):
     # the root assembles on an assembler batch: tables, scan buffers and
     # outputs only (no whole-frame input, coefficient or token buffers)
     full = mijpeg.Batch(W, H, n, args.quality, device=gpu, assembler=True) if rank == 0 else None
-    # device-resident protocol (mij_band_*_async) when the collectives can run
-    # on device tensors -- one rank or RCCL; gloo rehearses the host protocol
-    on_dev = dist is None or dist.get_backend() == "nccl"
-    if on_dev:
-        xch = sharding.DeviceExchange(dist, f"cuda:{gpu}")
-    else:
+    if not on_dev:
         xch = sharding.TorchExchange(dist, dist_device(dist, local))
+    elif backend == "gloo":
+        xch = sharding.StagedExchange(dist, f"cuda:{gpu}")
+    else:
+        xch = sharding.DeviceExchange(dist, f"cuda:{gpu}")
 
     def step(events=None):
         if on_dev:
@@ -201,8 +210,10 @@ def run_config4(args, world, rank, local, dist):
                                f"exchanges and a packed-word gather to rank 0",
                    "frames_per_step": n, "width": W, "height": H, "quality": args.quality,
                    "parallelism": f"band-parallel x{world}",
-                   "backend": dist.get_backend() if dist is not None else "none",
-                   "protocol": "device-resident (mij_band_*_async)" if on_dev else "host arrays (gloo)"},
+                   "backend": backend,
+                   "protocol": ("host arrays (gloo)" if not on_dev else
+                                "device-resident (mij_band_*_async)" +
+                                (", collectives staged through host memory (gloo)" if backend == "gloo" else ""))},
         "verified_frames": verified,
         "verified_against_reference_sha": golden,
     }
@@ -587,7 +598,9 @@ def run_stream(args, world, rank, local, dist):
             "verified_files": verified, "verified_contents_pinned_to_reference_sha": pinned,
         }
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = stream_cpu_baseline(ins[:distinct], outs, W, H, args)
+            res["cpu_baseline"], par = stream_cpu_baseline(ins[:distinct], outs, W, H, args)
+            if par is not None:
+                res["cpu_baseline_parallel"] = par
         if rank == 0:
             print(json.dumps(res), flush=True)
     finally:
@@ -596,40 +609,61 @@ def run_stream(args, world, rank, local, dist):
         dist.destroy_process_group()
 
 
-def stream_cpu_baseline(ins, outs, W, H, args):
-    """The reference on the same files: utils/original.c's program (PPM file
-    -> .jpg file, byte-identical to main/encoder.c at Q=50; oracle/_ref,
-    compiled from the reference sources), one process per file, run
-    back to back on one core for ~--cpu-seconds; else the C restatement."""
-    import subprocess
+def _stream_cpu_worker(job):
+    """One process of the stream's CPU baseline: files -> .jpg files for
+    `seconds` (the reference's globals make it single-threaded per process)."""
+    ins, out_dir, seconds, quality, use_ref = job
     import oracle as O
-    if os.path.exists(O.REF_QUALITY):
-        work = os.path.join(os.path.dirname(ins[0]), "ref")
-        os.makedirs(os.path.join(work, "hisParts"), exist_ok=True)
-        n, t0 = 0, time.perf_counter()
-        while True:
-            subprocess.check_call([O.REF_QUALITY, ins[n % len(ins)], str(args.quality)], cwd=work,
-                                  stdout=subprocess.DEVNULL)
-            n += 1
-            el = time.perf_counter() - t0
-            if el >= args.cpu_seconds and n >= 2:
-                break
-        kind, what = "reference", "utils/original.c program (oracle/_ref/ref_quality), file -> file"
-    else:
-        import ppm
-        n, t0 = 0, time.perf_counter()
-        while True:
-            with open(ins[n % len(ins)], "rb") as f:
+    n, t0 = 0, time.perf_counter()
+    while True:
+        src = ins[n % len(ins)]
+        dst = os.path.join(out_dir, f"cpu_{os.getpid()}.jpg")
+        if use_ref:
+            if not O.ref_encode_file(src, dst):
+                raise SystemExit(f"bench stream: the reference failed on {src}")
+        else:
+            import ppm
+            with open(src, "rb") as f:
                 rgb = ppm.parse_ppm(f.read())
-            with open(os.path.join(os.path.dirname(ins[0]), "cref.jpg"), "wb") as f:
-                f.write(O.cref_encode(np.ascontiguousarray(rgb[:, :, ::-1]), args.quality))
-            n += 1
-            el = time.perf_counter() - t0
-            if el >= args.cpu_seconds and n >= 2:
-                break
-        kind, what = "port", "oracle/cpu_ref.c, file -> file"
-    return {"value": round(n * W * H / el / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": kind,
-            "sample": f"{n} files of {W}x{H} in {el:.1f} s, {what}"}
+            with open(dst, "wb") as f:
+                f.write(O.cref_encode(np.ascontiguousarray(rgb[:, :, ::-1]), quality))
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and n >= 2:
+            return n, el
+
+
+def stream_cpu_baseline(ins, outs, W, H, args):
+    """The reference on the same files, the way its caller runs it (main.c:
+    131-155 with the camera replaced by the PPM file): PPM read, the three
+    encoder.c entry points, write_jpg writing the .jpg file itself
+    (oracle/_ref ref_encode_file, compiled from the reference sources).  One
+    core, and frame-parallel over --cpu-workers processes.  encoder.c has no
+    quality knob, so at Q != 50 the C restatement (cpu_ref, file -> file)
+    stands in.  Returns (1-core entry, parallel entry or None)."""
+    import multiprocessing as mp
+    import oracle as O
+    use_ref = O.ref_available() and args.quality == 50
+    out_dir = os.path.dirname(outs[0])
+    what = ("reference main/encoder.c via oracle/_ref ref_encode_file (PPM read, rgb_to_dct, "
+            "init_huffman, write_jpg -> file)" if use_ref else "oracle/cpu_ref.c, PPM file -> .jpg file")
+    kind = "reference" if use_ref else "port"
+    n, el = _stream_cpu_worker((ins, out_dir, args.cpu_seconds, args.quality, use_ref))
+    one = {"value": round(n * W * H / el / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": kind,
+           "sample": f"{n} files of {W}x{H} in {el:.1f} s, {what}"}
+    par = None
+    if args.cpu_workers > 1:
+        ctx = mp.get_context("spawn")
+        jobs = [(ins[i % len(ins):] + ins[:i % len(ins)], out_dir, args.cpu_seconds, args.quality, use_ref)
+                for i in range(args.cpu_workers)]
+        with ctx.Pool(args.cpu_workers) as pool:
+            parts = pool.map(_stream_cpu_worker, jobs)
+        files = sum(p for p, _ in parts)
+        busy = max(e for _, e in parts)
+        par = {"value": round(files * W * H / busy / 1e6, 3), "unit": "Mpixels/s", "cores": args.cpu_workers,
+               "kind": kind, "sample": f"{args.cpu_workers} processes x >= {args.cpu_seconds:.0f} s, "
+                                       f"{files} files in all, {what}"}
+    return one, par
 
 
 def make_frames(args, rank):
@@ -825,6 +859,9 @@ def main():
     gpu = 0 if dist is not None and dist.get_backend() != "nccl" else local
     batch = mijpeg.Batch(W, H, F, args.quality, device=gpu)
     batch.set_split(args.split)
+    opts = dict(o.split("=", 1) for o in args.opt)
+    for k, v in opts.items():
+        batch.set_option(k, int(v))
     if args.overlap > 1:
         batch.set_overlap(args.overlap)
     for i in range(F):
@@ -924,7 +961,8 @@ def main():
                                f"Q={args.quality}, one independent JFIF per frame",
                    "frames_per_gpu": F, "width": W, "height": H, "quality": args.quality,
                    "mode": args.mode, "pipeline": "split" if args.split else "fused",
-                   "parallelism": f"frame-parallel x{world}"},
+                   "parallelism": f"frame-parallel x{world}",
+                   **({"options": {k: int(v) for k, v in opts.items()}} if opts else {})},
         "roofline": {"bound": "hbm", "kernel": f"{dom} ({dom_desc})",
                      "achieved": round(k1_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(k1_gbs / HBM_PEAK_GBS, 4), "traffic": None,

@@ -131,6 +131,37 @@ int mij_batch_set_split(mij_batch *b, int on);
  * concurrent with K1 of sub-batch k + 1.  Same output bytes; stage timing
  * then reports K1 over all sub-batches ([0]) and the whole encode ([7]). */
 int mij_batch_set_overlap(mij_batch *b, int nsub);
+/* Entropy-stage variants of the fused pipeline.  Every setting gives the
+ * same output bytes; the defaults are the measured-fastest ones and the
+ * others exist for A/B timing (bench.py --opt NAME=V) and are covered by
+ * tests/test_options.py.
+ *   MIJ_OPT_SEAM          1 (default): every scan word stored whole, shared
+ *                         group edge words ORed in afterwards; 0: edge words
+ *                         ORed onto zeroed scan buffers (the band paths' form)
+ *   MIJ_OPT_FF_PACK       1 (default, seam mode only): the packing counts the
+ *                         0xFF bytes of every output chunk; 0: a counting pass
+ *   MIJ_OPT_ACTAB         1 (default): on batches of >= 16 frames the AC
+ *                         tables are built beside the segment DCs; 0: after
+ *   MIJ_OPT_SEGDC_FUSED   0 (default); 1: the segment DCs inside the table
+ *                         kernel's DC waves
+ *   MIJ_OPT_PACK_WIDE     -1 (default: the wide window from quality 85);
+ *                         0 / 1 force the default / wide pack window
+ *   MIJ_OPT_EMIT_SLOTS    0 (default: chosen from frame count, size and Q);
+ *                         > 0: JFIF-assembly workgroups per frame
+ *   MIJ_OPT_OVERLAP_PRIO  1 (default): the overlap stream (set_overlap) at
+ *                         the highest priority; 0: the lowest */
+enum {
+  MIJ_OPT_SEAM = 0,
+  MIJ_OPT_FF_PACK = 1,
+  MIJ_OPT_ACTAB = 2,
+  MIJ_OPT_SEGDC_FUSED = 3,
+  MIJ_OPT_PACK_WIDE = 4,
+  MIJ_OPT_EMIT_SLOTS = 5,
+  MIJ_OPT_OVERLAP_PRIO = 6,
+  MIJ_OPT_COUNT = 7
+};
+int mij_batch_set_option(mij_batch *b, int opt, int value);
+int mij_batch_get_option(mij_batch *b, int opt);
 /* input frames in R, G, B byte order (PPM files, brain.c:25-42) instead of the
  * encoder's B, G, R (encoder.c:133); the channels are swapped inside K1, at no
  * cost.  Both pipelines. */
@@ -164,7 +195,8 @@ int mij_batch_stage_history(mij_batch *b, float *ms, int steps);
 /* symbol tokens K1 emitted for the last encode of nframes frames (4 bytes
  * each; used for the bandwidth accounting of the fused kernel) */
 unsigned long long mij_batch_token_count(mij_batch *b, int nframes);
-/* {w, h, 8x8 blocks per frame, segments per frame, K1 tiles per frame} */
+/* {w, h, 8x8 blocks per frame, segments per frame, K1 tiles per frame,
+ *  the pack kernel's LDS window in words at the batch's quality}: the first n */
 int mij_batch_geometry(mij_batch *b, long long *out, int n);
 /* FP64 fix-ups since creation: blocks re-encoded by the fix-up kernel after
  * K1 (split pipeline) plus coefficients replayed in place (fused pipeline) */

@@ -86,6 +86,20 @@ int mij_fail(int code, const char *fmt, ...) {
 }
 void mij_clear_error() { g_err = MIJ_OK; }
 
+// Diagnostic switches (per-wave clocks, K1 attribution flags, timing dumps)
+// read from the environment in the diagnostic build only (make diag); the
+// product library ignores them.
+#ifdef MIJ_K1_DIAG
+static int diag_env(const char *name, int dflt) {
+  const char *e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+static const char *diag_str(const char *name) { return getenv(name); }
+#else
+static constexpr int diag_env(const char *, int dflt) { return dflt; }
+static constexpr const char *diag_str(const char *) { return nullptr; }
+#endif
+
 #define HIP_TRY(x)                                                          \
   do {                                                                      \
     hipError_t e_ = (x);                                                    \
@@ -313,6 +327,8 @@ struct mij_batch {
   hipStream_t stream2 = nullptr;
   hipEvent_t ov_k1[16] = {}, ov_done = nullptr;
   bool timing = false;
+  // mij_batch_set_option (include/mijpeg.h): entropy-stage variants
+  int opt[MIJ_OPT_COUNT] = {1, 1, 1, 0, -1, 0, 1};
   static constexpr int HIST = 64;
   hipEvent_t evh[HIST][MIJ_NSTAGES] = {};  // per-step events while timing is on
   hipEvent_t *ev = evh[0];       // current step's events
@@ -520,6 +536,14 @@ extern "C" int mij_batch_set_input(mij_batch *b, const void *d_bgr, long long fr
   return MIJ_OK;
 }
 
+// a 64-segment pack group at Q >= 85 outgrows a 4096-word window (config
+// 5: Q=90 luma groups ~4.8k words): the wider window keeps it on the
+// one-window path (A/B: MIJ_PACK_WIDE=0/1)
+static int ent_args_pack_wide(const mij_batch *b) {
+  const int v = b->opt[MIJ_OPT_PACK_WIDE];
+  return v >= 0 ? v : (b->quality >= PACK_WIDE_MIN_Q ? 1 : 0);
+}
+
 // band: the mij_band_* calls, whose per-frame DC predictors and in-word scan
 // start bits live in d_dcpred / d_bitbase; every other pipeline reads both as
 // 0 (null), so a band call leaves no state behind for the next encode
@@ -559,16 +583,12 @@ static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0, bool band = false
   // the width)
   // 512 on frames of 8 Mpixels and more (config 4: few scans of hundreds of
   // chunks each)
-  static const int slots_env = getenv("MIJ_EMIT_SLOTS") ? atoi(getenv("MIJ_EMIT_SLOTS")) : 0;  // A/B
-  a.emit_slots = slots_env > 0                           ? slots_env
+  const int slots_opt = b->opt[MIJ_OPT_EMIT_SLOTS];
+  a.emit_slots = slots_opt > 0                           ? slots_opt
                  : (nframes >= 43 && b->quality <= 60)   ? 48
                  : ((long long)b->g.w * b->g.h >= (8 << 20)) ? 1536
                                                            : 192;
-  // a 64-segment pack group at Q >= 85 outgrows a 4096-word window (config
-  // 5: Q=90 luma groups ~4.8k words): the double window keeps it on the
-  // one-window path (A/B: MIJ_PACK_WIDE=0/1)
-  static const int wide_env = getenv("MIJ_PACK_WIDE") ? atoi(getenv("MIJ_PACK_WIDE")) : -1;
-  a.pack_wide = wide_env >= 0 ? wide_env : (b->quality >= 85 ? 1 : 0);
+  a.pack_wide = ent_args_pack_wide(b);
   if (f0) {  // sub-batch: frames f0.. of the batch (every per-frame array shifted)
     const Geom &g = b->g;
     const long long F = f0, gpf = (g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((g.nsc + PACK_SEGS - 1) / PACK_SEGS);
@@ -602,6 +622,9 @@ static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0, bool band = false
 // 4 coefficient planes in)
 static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int seg_dc_inline = 0, int f0 = 0,
                   bool stage_events = true) {
+  // a token-emitting K1 (modes 2, 3, 6: the band calls too) adds onto d_hist:
+  // the next encode must zero it again
+  if (mode & 2) b->hist_zero_n = 0;
   K1Args k;
   memset(&k, 0, sizeof(k));
   k.in = b->d_in;
@@ -633,7 +656,7 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int se
     k.hist += F * 4 * 257;
     if (k.fdims) k.fdims += F;
   }
-  static const int k1_flags = getenv("MIJ_K1_FLAGS") ? atoi(getenv("MIJ_K1_FLAGS")) : 0;
+  static const int k1_flags = diag_env("MIJ_K1_FLAGS", 0);
   k.flags = k1_flags;
   const long long ntiles = (long long)nframes * b->g.tiles_per_frame;
   long long grid = k1_grid(b->dev, ntiles, mode);
@@ -646,7 +669,7 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int se
   // the coefficient variant marks hazard blocks in the fix masks;
   // k_fix_blocks recomputes them in FP64 right after it, on the same stream
   // diagnostics (MIJ_K1_WTIME with the diag build): per-wave lifetimes of K1
-  static const bool wtime = getenv("MIJ_K1_WTIME") != nullptr;
+  static const bool wtime = diag_env("MIJ_K1_WTIME", 0) != 0;
   unsigned long long *d_wt = nullptr;
   const long long nw = grid * 16;
   if (wtime && (mode == 1 || mode == 2)) {
@@ -672,7 +695,7 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int se
       sum += d; smin = std::min(smin, d); smax = std::max(smax, d); n++; tiles += (long long)h[WW * i + 2];
       for (int k = 0; k < 5; k++) ph[k] += (double)h[WW * i + 3 + k];
     }
-    if (const char *path = getenv("MIJ_K1_WTIME_DUMP")) {  // raw per-wave records
+    if (const char *path = diag_str("MIJ_K1_WTIME_DUMP")) {  // raw per-wave records
       if (FILE *fp = fopen(path, "ab")) { fwrite(h.data(), sizeof(unsigned long long), WW * nw, fp); fclose(fp); }
     }
     // s_memrealtime ticks at 100 MHz; the phases are s_memtime (shader clock) per tile
@@ -699,20 +722,19 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   if (!st) st = b->stream;
   // segment-first DC tokens: inside k_tables (its DC-table waves), or on
   // their own when the caller's tables are given
-  static const int segdc_dbg = getenv("MIJ_SEGDC_DBG") ? atoi(getenv("MIJ_SEGDC_DBG")) : 0;  // diag build
-  // (A/B: MIJ_SEGDC_FUSED=1 runs them in k_tables' DC waves -- two waves per
-  // frame, 0.11 ms of a config-3 launch against a few us spread over the chip)
-  static const bool segdc_fused = getenv("MIJ_SEGDC_FUSED") && atoi(getenv("MIJ_SEGDC_FUSED"));
+  static const int segdc_dbg = diag_env("MIJ_SEGDC_DBG", 0);  // diag build
+  // (A/B: MIJ_OPT_SEGDC_FUSED=1 runs them in k_tables' DC waves -- two waves
+  // per frame, 0.11 ms of a config-3 launch against a few us spread over the chip)
+  const bool segdc_fused = b->opt[MIJ_OPT_SEGDC_FUSED] != 0;
   a.seg_dc = dc_fix && !tables_given && segdc_fused ? 1 | segdc_dbg : 0;
   // diagnostics (MIJ_TAB_TIME with the diag build): per-wave phase clocks of k_tables
-  static const bool ttime = getenv("MIJ_TAB_TIME") != nullptr;
+  static const bool ttime = diag_env("MIJ_TAB_TIME", 0) != 0;
   // the AC tables beside the segment DCs (they need only K1's histograms),
-  // the DC tables after (A/B: MIJ_ACTAB=0; profiles/r03/qsweep/actab_ab.txt:
+  // the DC tables after (A/B: MIJ_OPT_ACTAB=0; profiles/r03/qsweep/actab_ab.txt:
   // segment DCs + tables 0.077 -> 0.062 ms at config 3 Q=50, 0.102 -> 0.075
   // at Q=90).  Not on small batches: one frame's four tables take as long
   // as its AC tables, and the DC tables after them add 10 us.
-  static const int actab_env = getenv("MIJ_ACTAB") ? atoi(getenv("MIJ_ACTAB")) : 1;
-  const bool actab = dc_fix && !a.seg_dc && !tables_given && !ttime && actab_env && nframes >= 16;
+  const bool actab = dc_fix && !a.seg_dc && !tables_given && !ttime && b->opt[MIJ_OPT_ACTAB] && nframes >= 16;
   if (actab) {
     a.zero_pack = 1;  // (the AC workgroups zero the counts they read)
     HIP_TRY(launch_segdc_actab(a, st));
@@ -794,26 +816,24 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   b->hist_zero_after = (f0 == 0 && a.zero_pack) ? nframes : 0;
   if (t) HIP_TRY(hipEventRecord(b->ev[5], st));
   // segment bits, scan offsets and packing in one look-back pass
-  // Seam mode (default; MIJ_SEAM=0 for the A/B): every scan word is stored
+  // Seam mode (default; MIJ_OPT_SEAM=0 for the A/B): every scan word is stored
   // whole by one pack group; a group's first word, when shared with the group
   // before it, goes to seam[] and k_seam_fix ORs it in after the packing --
   // the scan buffers need not start zeroed (no atomics in k_pack_lb), and
   // k_emit_write does not zero them after reading.  The other paths (bands,
   // assembly) still OR onto zero: they clear what this leaves (raw_dirty).
-  static const int seam_env = getenv("MIJ_SEAM") ? atoi(getenv("MIJ_SEAM")) : 1;
-  if (seam_env && b->d_seam) {
+  if (b->opt[MIJ_OPT_SEAM] && b->d_seam) {
     a.seam = b->d_seam + (long long)f0 * ((b->g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((b->g.nsc + PACK_SEGS - 1) / PACK_SEGS));
     // the 0xFF bytes of every emit chunk counted as the words are stored
-    // (no k_emit_count pass over the scan words; A/B: MIJ_FF_PACK=0)
-    static const int ffp_env = getenv("MIJ_FF_PACK") ? atoi(getenv("MIJ_FF_PACK")) : 1;
-    a.ff_pack = ffp_env;
+    // (no k_emit_count pass over the scan words; A/B: MIJ_OPT_FF_PACK=0)
+    a.ff_pack = b->opt[MIJ_OPT_FF_PACK] != 0;
     b->raw_dirty = std::max(b->raw_dirty, f0 + nframes);
   } else if (b->raw_dirty) {
     HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->raw_dirty * b->g.raw_fs, st));
     b->raw_dirty = 0;
   }
   // diagnostics (MIJ_PACK_TIME with the diag build): per-group phase times of k_pack_lb
-  static const bool ptime = getenv("MIJ_PACK_TIME") != nullptr;
+  static const bool ptime = diag_env("MIJ_PACK_TIME", 0) != 0;
   const long long ngroups = (long long)nframes * ((b->g.nsy + PACK_SEGS - 1) / PACK_SEGS +
                                                   2 * ((b->g.nsc + PACK_SEGS - 1) / PACK_SEGS));
   if (ptime) {
@@ -1044,13 +1064,30 @@ extern "C" int mij_batch_set_overlap(mij_batch *b, int nsub) {
     // the CU room the running K1 leaves before the next K1's do
     int lo = 0, hi = 0;
     HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    static const int prio_env = getenv("MIJ_OVERLAP_PRIO") ? atoi(getenv("MIJ_OVERLAP_PRIO")) : 1;  // A/B
-    HIP_TRY(hipStreamCreateWithPriority(&b->stream2, hipStreamNonBlocking, prio_env ? hi : lo));
+    HIP_TRY(hipStreamCreateWithPriority(&b->stream2, hipStreamNonBlocking, b->opt[MIJ_OPT_OVERLAP_PRIO] ? hi : lo));
     for (auto &e : b->ov_k1) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&b->ov_done, hipEventDisableTiming));
   }
   b->overlap = nsub;
   return MIJ_OK;
+}
+
+extern "C" int mij_batch_set_option(mij_batch *b, int opt, int value) {
+  if (pipe_check(b, "set_option")) return g_err;
+  if (opt < 0 || opt >= MIJ_OPT_COUNT) return fail(MIJ_EINVAL, "set_option: unknown option %d", opt);
+  const bool binary = opt != MIJ_OPT_PACK_WIDE && opt != MIJ_OPT_EMIT_SLOTS;
+  if ((binary && value != 0 && value != 1) || (opt == MIJ_OPT_PACK_WIDE && (value < -1 || value > 1)) ||
+      (opt == MIJ_OPT_EMIT_SLOTS && (value < 0 || value > 4096)))
+    return fail(MIJ_EINVAL, "set_option: value %d out of range for option %d", value, opt);
+  if (opt == MIJ_OPT_OVERLAP_PRIO && b->stream2)
+    return fail(MIJ_EINVAL, "set_option: the overlap stream exists already (set the priority before set_overlap)");
+  b->opt[opt] = value;
+  return MIJ_OK;
+}
+
+extern "C" int mij_batch_get_option(mij_batch *b, int opt) {
+  if (!b || opt < 0 || opt >= MIJ_OPT_COUNT) return fail(MIJ_EINVAL, "get_option: bad args"), -2;
+  return b->opt[opt];
 }
 
 extern "C" int mij_batch_dct(mij_batch *b, int nframes) {
@@ -1154,8 +1191,11 @@ extern "C" unsigned long long mij_batch_token_count(mij_batch *b, int nframes) {
 
 extern "C" int mij_batch_geometry(mij_batch *b, long long *out, int n) {
   if (!b || !out) return fail(MIJ_EINVAL, "geometry: bad args");
-  const long long v[] = {b->g.w, b->g.h, b->g.nblk, b->g.nseg, b->g.tiles_per_frame};
-  for (int i = 0; i < n && i < 5; i++) out[i] = v[i];
+  // ... then k_pack_lb's LDS window (words) at this batch's quality
+  const long long win = ent_args_pack_wide(b) ? PACK_WIDE_WORDS : PACK_WORDS;
+  const long long v[] = {b->g.w, b->g.h, b->g.nblk, b->g.nseg, b->g.tiles_per_frame, win};
+  const int nv = (int)(sizeof(v) / sizeof(v[0]));
+  for (int i = 0; i < n && i < nv; i++) out[i] = v[i];
   return MIJ_OK;
 }
 

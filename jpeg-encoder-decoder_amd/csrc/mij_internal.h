@@ -39,6 +39,13 @@ constexpr int MAX_BLOCK_BITS = 1729;              // 28 DC + 63 * 27 AC bits
 #define MIJ_PACK_WORDS 4096
 #endif
 constexpr int PACK_WORDS = MIJ_PACK_WORDS;
+// the window of the high-quality variant (EntArgs::pack_wide, Q >= 85)
+#ifndef MIJ_PACK_WIDE_WORDS
+#define MIJ_PACK_WIDE_WORDS 6144
+#endif
+constexpr int PACK_WIDE_WORDS = MIJ_PACK_WIDE_WORDS;
+static_assert(PACK_WIDE_WORDS > PACK_WORDS, "the wide pack window must be wider than the default one");
+constexpr int PACK_WIDE_MIN_Q = 85;  // qualities from which the wide window is launched
 // k_pack_lb: tokens per lane loaded in one batch (16 lanes per segment)
 constexpr int PACK_BATCH = 16;
 // JFIF assembly: scans are written in EMIT_CH-byte chunks by EntArgs::

@@ -2662,11 +2662,8 @@ __device__ __forceinline__ int ff_word(uint32_t v, uint32_t W, uint32_t nb) {
 constexpr int EMIT_CW = EMIT_CH / 4;  // stream words per emit chunk
 
 // PW: the LDS window in words (PACK_WORDS; high-quality batches, whose groups
-// outgrow it, get a double window -- fewer groups per CU, but no group on the
-// window-by-window path)
-#ifndef MIJ_PACK_WIDE_WORDS
-#define MIJ_PACK_WIDE_WORDS 6144
-#endif
+// outgrow it, get the wider PACK_WIDE_WORDS window -- fewer groups per CU,
+// but no group on the window-by-window path; both in mij_internal.h)
 // FF: seam mode with the 0xFF bytes counted as the words are stored
 // (EntArgs::ff_pack; a compile-time variant: at 79 VGPRs the runtime checks
 // of both modes spilled)
@@ -3523,6 +3520,7 @@ __global__ void k_band_assembly(const unsigned long long *allbits, int world, in
                                 unsigned long long *pieces, unsigned long long *scan_bits, int *over) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   for (int i = 0; i < 3 * n; i++) scan_bits[i] = 0;
+  bool overflow = false;
   for (int r = 0; r < world; r++) {
     const unsigned long long *rb = allbits + (long long)r * (3 * n + 1);
     unsigned long long at = 0;
@@ -3536,8 +3534,15 @@ __global__ void k_band_assembly(const unsigned long long *allbits, int world, in
       at += (bits + 31) >> 5;
       scan_bits[i] = off + bits;
     }
-    if (at > stride)  // a band's words beyond its row: fail the frames, assemble nothing wrong
-      for (int f = 0; f < n; f++) over[f] = 1;
+    overflow |= at > stride;
+  }
+  // a band's words beyond its row (the gather dropped them): fail the frames
+  // and give every piece 0 bits, so k_or_shift_pieces reads and writes
+  // nothing (its source offsets would run past the band's row, and for the
+  // last band past the gathered buffer)
+  if (overflow) {
+    for (int f = 0; f < n; f++) over[f] = 1;
+    for (long long k = 0; k < (long long)world * 3 * n; k++) pieces[4 * k + 3] = 0;
   }
 }
 
@@ -3670,8 +3675,12 @@ int k1_grid(int device, long long ntiles, int mode) {
     hipDeviceProp_t prop;
     cus = hipGetDeviceProperties(&prop, device) == hipSuccess ? prop.multiProcessorCount : 256;
   }
-  // MIJ_K1_GRID_MULT (A/B timing): workgroups per resident slot
+  // MIJ_K1_GRID_MULT (diag build, A/B timing): workgroups per resident slot
+#ifdef MIJ_K1_DIAG
   static const int mult = getenv("MIJ_K1_GRID_MULT") ? atoi(getenv("MIJ_K1_GRID_MULT")) : 1;
+#else
+  constexpr int mult = 1;
+#endif
   long long want = (ntiles + nw - 1) / nw;
   long long cap = (long long)cus * per_cu * (mult > 0 ? mult : 1);
   return (int)(want < cap ? want : cap);

@@ -22,7 +22,7 @@ EXPORTS = [
     "mij_set_input_stride", "mij_set_quality", "mij_last_error", "mij_strerror", "mij_last_message",
     "mij_max_jpg_bytes", "mij_encode",
     "mij_batch_create", "mij_batch_destroy", "mij_batch_upload", "mij_batch_set_input",
-    "mij_batch_encode", "mij_batch_keep_coefs", "mij_batch_set_split", "mij_batch_set_overlap", "mij_batch_dct", "mij_batch_sync", "mij_batch_output",
+    "mij_batch_encode", "mij_batch_keep_coefs", "mij_batch_set_split", "mij_batch_set_overlap", "mij_batch_set_option", "mij_batch_get_option", "mij_batch_dct", "mij_batch_sync", "mij_batch_output",
     "mij_batch_lengths", "mij_batch_coefs", "mij_batch_tables", "mij_batch_set_timing",
     "mij_batch_stage_ms", "mij_batch_stage_history", "mij_batch_token_count", "mij_batch_geometry", "mij_batch_replays", "mij_batch_stream", "mij_batch_audit", "mij_batch_build_tables",
     "mij_band_analyze", "mij_band_histograms", "mij_band_tables", "mij_band_pack", "mij_band_words",
@@ -68,6 +68,11 @@ class MijError(RuntimeError):
     pass
 
 
+# mij_batch_set_option (include/mijpeg.h: MIJ_OPT_*)
+OPTIONS = {"seam": 0, "ff_pack": 1, "actab": 2, "segdc_fused": 3, "pack_wide": 4, "emit_slots": 5,
+           "overlap_prio": 6}
+
+
 _lib = None
 
 
@@ -106,6 +111,8 @@ def load() -> C.CDLL:
     lib.mij_batch_keep_coefs.argtypes = [p, i]
     lib.mij_batch_set_split.argtypes = [p, i]
     lib.mij_batch_set_overlap.argtypes = [p, i]
+    lib.mij_batch_set_option.argtypes = [p, i, i]
+    lib.mij_batch_get_option.argtypes = [p, i]
     lib.mij_batch_dct.argtypes = [p, i]
     lib.mij_batch_audit.argtypes = [p, i, p]
     lib.mij_band_analyze_async.argtypes = [p, i, p]
@@ -338,6 +345,13 @@ class Batch:
         """fused pipeline in nsub sub-batches, entropy of one beside K1 of the next"""
         _check(self.lib.mij_batch_set_overlap(self.h_, int(nsub)), "set_overlap")
 
+    def set_option(self, name: str, value: int) -> None:
+        """entropy-stage variant (include/mijpeg.h MIJ_OPT_*; same bytes)"""
+        _check(self.lib.mij_batch_set_option(self.h_, OPTIONS[name], int(value)), f"set_option({name})")
+
+    def get_option(self, name: str) -> int:
+        return int(self.lib.mij_batch_get_option(self.h_, OPTIONS[name]))
+
     def set_rgb(self, on: bool) -> None:
         """frames in R, G, B byte order (PPM) instead of the encoder's B, G, R"""
         _check(self.lib.mij_batch_set_rgb(self.h_, int(on)), "set_rgb")
@@ -434,9 +448,10 @@ class Batch:
         return int(self.lib.mij_batch_token_count(self.h_, n))
 
     def geometry(self) -> dict:
-        g = np.zeros(5, np.int64)
-        _check(self.lib.mij_batch_geometry(self.h_, _ptr(g), 5), "geometry")
-        return dict(zip(["w", "h", "nblk", "nseg", "tiles_per_frame"], [int(v) for v in g]))
+        keys = ["w", "h", "nblk", "nseg", "tiles_per_frame", "pack_window_words"]
+        g = np.zeros(len(keys), np.int64)
+        _check(self.lib.mij_batch_geometry(self.h_, _ptr(g), len(keys)), "geometry")
+        return dict(zip(keys, [int(v) for v in g]))
 
     def audit(self, n: int) -> np.ndarray:
         """K1's fast-path keep/replay decisions (mij_batch_audit): uint64 per

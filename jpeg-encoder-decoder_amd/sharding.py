@@ -259,6 +259,46 @@ class DeviceExchange:
         return None
 
 
+class StagedExchange(DeviceExchange):
+    """DeviceExchange's collectives over a host backend (gloo): each one
+    copies its device tensor to the host on the current stream (the band
+    batch's stream inside encode_banded_dev, so the copy waits for the
+    library's kernels), runs the gloo collective there and copies the result
+    back to the device on the same stream.  encode_banded_dev then runs with
+    world > 1 on one GPU -- several processes sharing it -- with exactly the
+    indexing the RCCL run uses (the prefix bands' last DCs, the bounds, the
+    [world, 3n + 1] bits, the gathered [world, stride] words)."""
+
+    def __init__(self, dist, device="cuda:0"):
+        super().__init__(dist, device)
+        if dist is None:
+            raise ValueError("StagedExchange needs a process group")
+
+    def _host(self, t):
+        return t.contiguous().cpu()  # blocking copy: waits for the current stream
+
+    def all_gather(self, t):
+        h = self._host(t)
+        out = self.torch.empty((self.world,) + tuple(h.shape), dtype=h.dtype)
+        self.dist.all_gather(list(out.unbind(0)), h)
+        return out.to(t.device)
+
+    def all_reduce_sum(self, t):
+        h = self._host(t)
+        self.dist.all_reduce(h, op=self.dist.ReduceOp.SUM)
+        t.copy_(h)
+        return t
+
+    def gather(self, buf):
+        h = self._host(buf)
+        if self.rank == 0:
+            out = self.torch.empty((self.world, h.numel()), dtype=h.dtype)
+            self.dist.gather(h, gather_list=list(out.unbind(0)), dst=0)
+            return out.to(buf.device)
+        self.dist.gather(h, dst=0)
+        return None
+
+
 def encode_banded_dev(band, n: int, xch, frame_batch=None, events=None):
     """encode_banded with the device-resident protocol: the last DCs (int16
     [n, 4], gathered as int32 pairs), the histograms (summed in place), the

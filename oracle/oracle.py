@@ -97,9 +97,30 @@ def ref() -> C.CDLL:
         lib.ref_stage_dct.argtypes = [p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                       p, p, p]
         lib.ref_cos_bits.argtypes = [p]
+        lib.ref_encode_file.restype = C.c_size_t
+        lib.ref_encode_file.argtypes = [C.c_char_p, C.c_char_p, p, C.c_size_t, p, p, p, p]
         lib.ref_huff_size.restype = C.c_size_t
         _ref = lib
     return _ref
+
+
+_file_bufs = {}
+
+
+def ref_encode_file(ppm_path: str, jpg_path: str, max_px: int = 3840 * 2160) -> int:
+    """The reference encoder.c on a file (oracle/_ref ref_encode_file): PPM
+    read + RGB->BGR + rgb_to_dct + init_huffman + write_jpg into jpg_path.
+    Returns the .jpg size (0: unreadable file).  Buffers are kept per size,
+    as main.c keeps its buffers static."""
+    lib = ref()
+    bufs = _file_bufs.get(max_px)
+    if bufs is None:
+        bufs = (np.zeros(max_px * 3, np.uint8), np.zeros(max_px, np.int16), np.zeros(max_px // 4, np.int16),
+                np.zeros(max_px // 4, np.int16), np.zeros(max_jpg_bytes(16, max_px // 16), np.uint8))
+        _file_bufs[max_px] = bufs
+    bgr, Y, Cb, Cr, jpg = bufs
+    return int(lib.ref_encode_file(ppm_path.encode(), jpg_path.encode(), _ptr(bgr), bgr.size, _ptr(Y),
+                                   _ptr(Cb), _ptr(Cr), _ptr(jpg)))
 
 
 _ref_brain = None

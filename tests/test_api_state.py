@@ -112,4 +112,9 @@ def test_repeated_encodes_growing_and_shrinking_frame_counts():
     b.band_analyze(2)
     b.encode(3)
     assert [b.output(i) for i in range(3)] == want
+    # the skip path after a band call: encode(3) leaves 3 frames' counts
+    # zeroed, band_analyze writes counts again, encode(2 <= 3) must refill
+    b.band_analyze(2)
+    b.encode(2)
+    assert [b.output(i) for i in range(2)] == want[:2]
     b.close()

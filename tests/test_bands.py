@@ -425,3 +425,90 @@ def test_device_resident_band_protocol():
     assert all(isinstance(o, str) for o in res["short"]), res["short"]
     assert res["nccl"] == [want, want]
     assert res["phases"] == ["start", "analyze", "histograms", "pack", "words", "assemble"]
+
+
+# ---------------------------------------------------------------------------
+# encode_banded_dev with world > 1: several processes share GPU 0, the
+# collectives of the device protocol staged through host memory over gloo
+# (sharding.StagedExchange) -- the indexing the RCCL run uses at N > 1
+# (the previous band's last DCs, the word bounds, the [world, 3n + 1] bits,
+# the gathered [world, stride] words) runs exactly as there
+# ---------------------------------------------------------------------------
+
+def _staged_rank(rank, world, port, q, spec):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import hashlib
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)  # torch's HIP runtime before the library's
+    import mijpeg
+    import recipes
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        W, H, kind = spec
+        if kind == "small":
+            frames = np.stack([recipes.config3_frame(7, H, W), recipes.noise(H, W, 12),
+                               recipes.config3_frame(8, H, W)])
+        else:
+            frames = recipes.config4_frame(0)[None]
+        n = frames.shape[0]
+        r0, rows = sharding.band_rows(H, world, rank)
+        band = mijpeg.Batch(W, rows, n)
+        band.upload(np.ascontiguousarray(frames[:, r0:r0 + rows]))
+        full = mijpeg.Batch(W, H, n, assembler=True) if rank == 0 else None
+        xch = sharding.StagedExchange(dist, "cuda:0")
+        outs = []
+        for _ in range(2):  # twice: the second step reuses every buffer
+            sharding.encode_banded_dev(band, n, xch, full)
+            band.sync()
+            if full is not None:
+                full.sync()
+                got = [full.output(f) for f in range(n)]
+                outs.append(got if kind == "small" else
+                            [(len(g), hashlib.sha256(g).hexdigest()) for g in got])
+            dist.barrier()
+        band.close()
+        if full is not None:
+            full.close()
+            q.put(outs)
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_staged(world, spec):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_staged_rank, args=(r, world, port, q, spec)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return outs
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_device_protocol_multi_rank_staged(world):
+    """encode_banded_dev over 2 and 3 ranks (processes on one GPU, gloo
+    collectives staged through host memory): each band's first DC predicted
+    from the previous rank's last DC, histograms summed, every band packed
+    from bit 0 and shifted into place by the root -- the reference's bytes,
+    twice in a row."""
+    import oracle as O
+    import recipes
+    W, H = 480, 320
+    outs = _run_staged(world, (W, H, "small"))
+    want = [O.cref_encode(recipes.config3_frame(7, H, W)), O.cref_encode(recipes.noise(H, W, 12)),
+            O.cref_encode(recipes.config3_frame(8, H, W))]
+    assert outs == [want, want]
+
+
+def test_device_protocol_two_ranks_full_size(manifest):
+    """The same at config 4's size: 7680x4320 frame 0 in two bands, against
+    the reference build's sha256 (tests/golden/manifest.json)."""
+    want = manifest["config4_frame0"]
+    outs = _run_staged(2, (7680, 4320, "full"))
+    assert outs == [[(want["jpg_len"], want["jpg_sha256"])]] * 2

@@ -368,13 +368,15 @@ def test_pack_window_paths_in_one_scan(q):
     frames = np.stack([img, img[::-1].copy()])
     # frame 0's first luma group (noise) is wider than one window at Q=100
     # (516k bits) and fits one at Q=50 (124k); frame 1's first (flat) fits
+    b = mijpeg.Batch(W, H, 2, q)
+    # the library's window at this quality (mij_batch_geometry: ent_args'
+    # pack_wide choice, whatever MIJ_PACK_WORDS / MIJ_PACK_WIDE_WORDS it was built with)
+    window = b.geometry()["pack_window_words"] * 32
     Y, _, _, tabs, _ = O.cref_stages(frames[0], q)
-    window = (6144 if q >= 85 else 4096) * 32  # the library's window at this quality (ent_args: pack_wide)
     wide = _luma_group_bits(Y, tabs, W, H, 0, (W + 127) // 128) > window
     assert wide == (q == 100)
     Y1, _, _, tabs1, _ = O.cref_stages(frames[1], q)
     assert _luma_group_bits(Y1, tabs1, W, H, 0, (W + 127) // 128) < window
-    b = mijpeg.Batch(W, H, 2, q)
     b.upload(frames)
     b.encode(2)
     for i in range(2):
