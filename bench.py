@@ -525,6 +525,8 @@ def run_stream(args, world, rank, local, dist):
     import ppm
     W, H, n = args.width, args.height, args.stream_files
     gpu = 0 if dist is not None and dist.get_backend() != "nccl" else local
+    import torch  # its HIP runtime before the library's (the PCIe probe below uses it)
+    torch.cuda.set_device(gpu)
     tmp = tempfile.mkdtemp(prefix=f"mij_stream_r{rank}_", dir=os.environ.get("TMPDIR", "/tmp"))
     try:
         distinct = min(n, args.distinct)
@@ -597,6 +599,26 @@ def run_stream(args, world, rank, local, dist):
             "input_GB_per_s": round(agg["bytes_in"] / el / 1e9, 2),
             "verified_files": verified, "verified_contents_pinned_to_reference_sha": pinned,
         }
+        # the PCIe ceiling of a host-fed stream: pinned host -> HBM copies of
+        # one chunk's bytes (torch on this GPU, after the stream is closed)
+        try:
+            nb = W * H * 3 * args.stream_chunk
+            src = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
+            dst = torch.empty(nb, dtype=torch.uint8, device=f"cuda:{gpu}")
+            dst.copy_(src, non_blocking=True)
+            torch.cuda.synchronize(gpu)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(3):
+                dst.copy_(src, non_blocking=True)
+            e1.record()
+            torch.cuda.synchronize(gpu)
+            h2d = 3 * nb / (e0.elapsed_time(e1) * 1e-3) / 1e9
+            res["pcie_h2d_GB_per_s"] = round(h2d, 1)
+            res["pcie_ceiling_Mpix_s"] = round(h2d * 1e9 / 3 / 1e6, 1)
+            del src, dst
+        except Exception as e:  # noqa: BLE001 (a report field, not the measurement)
+            res["pcie_h2d_GB_per_s"] = f"unmeasured: {e}"
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"], par = stream_cpu_baseline(ins[:distinct], outs, W, H, args)
             if par is not None:

@@ -9,6 +9,9 @@
 //   is uploaded, encoded, its lengths fetched, its bytes copied back and
 //   written out by host threads, overlapped with the other batch's chunk.
 //   Frames stay in PPM byte order (R, G, B): K1 swaps channels as it loads.
+//   Three pinned input buffers: the reader threads fill chunk k+1 while chunk
+//   k uploads and the bytes of chunk k-1 are written, so the PCIe upload
+//   (the bound of a host-fed stream) runs back to back.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>
@@ -130,12 +133,15 @@ extern "C" int mij_ppm_read(const char *path, uint8_t *dst, size_t cap, int dst_
       return mij_fail(MIJ_EHIP, "%s: %s", #x, hipGetErrorString(e_));         \
   } while (0)
 
+constexpr int NIN = 3;  // pinned input buffers
+
 struct mij_stream {
   int dev = 0, w = 0, h = 0, chunk = 0, threads = 1;
   size_t fbytes = 0;
   mij_batch *b[2] = {nullptr, nullptr};
   hipStream_t st[2] = {nullptr, nullptr};
-  uint8_t *h_in[2] = {nullptr, nullptr};
+  uint8_t *h_in[NIN] = {nullptr, nullptr, nullptr};
+  hipEvent_t ev_up[NIN] = {};  // the upload out of h_in[i] has completed
   uint64_t *h_len[2] = {nullptr, nullptr};
   int *h_err[2] = {nullptr, nullptr};
   uint8_t *h_out[2] = {nullptr, nullptr};
@@ -148,10 +154,13 @@ struct mij_stream {
 static void stream_free(mij_stream *s) {
   if (!s) return;
   hipSetDevice(s->dev);
+  for (int i = 0; i < NIN; i++) {
+    if (s->h_in[i]) hipHostFree(s->h_in[i]);
+    if (s->ev_up[i]) hipEventDestroy(s->ev_up[i]);
+  }
   for (int i = 0; i < 2; i++) {
     if (s->st[i]) hipStreamSynchronize(s->st[i]);
     if (s->b[i]) mij_batch_destroy(s->b[i]);
-    if (s->h_in[i]) hipHostFree(s->h_in[i]);
     if (s->h_len[i]) hipHostFree(s->h_len[i]);
     if (s->h_err[i]) hipHostFree(s->h_err[i]);
     if (s->h_out[i]) hipHostFree(s->h_out[i]);
@@ -175,8 +184,11 @@ static int stream_init(mij_stream *s, int device, int w, int h, int chunk, int q
     s->st[i] = (hipStream_t)mij_batch_stream(s->b[i]);
   }
   S_TRY(hipSetDevice(device));
-  for (int i = 0; i < 2; i++) {
+  for (int i = 0; i < NIN; i++) {
     S_TRY(hipHostMalloc((void **)&s->h_in[i], s->fbytes * chunk, hipHostMallocDefault));
+    S_TRY(hipEventCreateWithFlags(&s->ev_up[i], hipEventDisableTiming));
+  }
+  for (int i = 0; i < 2; i++) {
     S_TRY(hipHostMalloc((void **)&s->h_len[i], sizeof(uint64_t) * chunk, hipHostMallocDefault));
     S_TRY(hipHostMalloc((void **)&s->h_err[i], sizeof(int) * chunk, hipHostMallocDefault));
     s->h_out_cap[i] = std::max<size_t>(1 << 20, s->fbytes / 4 * chunk);  // grows on demand
@@ -248,18 +260,43 @@ static int stream_run(mij_stream *s, int n, const FillFn &fill, const DrainFn &d
   const double t_start = now_s();
   const int nchunks = (n + s->chunk - 1) / s->chunk;
   auto count = [&](int k) { return std::min(s->chunk, n - k * s->chunk); };
+  // reader and writer pools share the host threads (writes are small)
+  const int wthreads = std::max(1, s->threads / 4), rthreads = std::max(1, s->threads - wthreads);
+
+  // chunk k's files into pinned buffer k % NIN (its previous upload, of chunk
+  // k - NIN, has completed: the caller waited for that event); runs on its
+  // own thread, ahead of the GPU work
+  struct Read {
+    std::thread th;
+    int rc = MIJ_OK, bad = -1;
+    double secs = 0.0;
+  } rd[NIN];
+  auto start_read = [&](int k) {
+    Read &r = rd[k % NIN];
+    r.rc = MIJ_OK;
+    r.bad = -1;
+    r.th = std::thread([&, k]() {
+      const int first = k * s->chunk, cnt = count(k);
+      uint8_t *dst = s->h_in[k % NIN];
+      const double t0 = now_s();
+      r.rc = parallel_for(cnt, rthreads, [&](int i) { return fill(first + i, dst + (size_t)i * s->fbytes); }, &r.bad);
+      if (r.rc && r.bad >= 0) r.bad += first;
+      r.secs = now_s() - t0;
+    });
+  };
+  auto join_read = [&](int k) -> int {
+    Read &r = rd[k % NIN];
+    if (r.th.joinable()) r.th.join();
+    s->stats[1] += r.secs;
+    if (r.rc && failed) *failed = r.bad;
+    return r.rc;
+  };
 
   auto enqueue = [&](int k) -> int {
-    const int sl = k & 1, first = k * s->chunk, cnt = count(k);
-    const double t0 = now_s();
-    int bad = -1;
-    int rc = parallel_for(cnt, s->threads, [&](int i) { return fill(first + i, s->h_in[sl] + (size_t)i * s->fbytes); }, &bad);
-    s->stats[1] += now_s() - t0;
-    if (rc) {
-      if (failed) *failed = first + bad;
-      return rc;
-    }
-    if ((rc = mij_batch_upload_async(s->b[sl], s->h_in[sl], cnt))) return rc;
+    const int sl = k & 1, cnt = count(k);
+    int rc;
+    if ((rc = mij_batch_upload_async(s->b[sl], s->h_in[k % NIN], cnt))) return rc;
+    S_TRY(hipEventRecord(s->ev_up[k % NIN], s->st[sl]));
     S_TRY(hipEventRecord(s->ev_t0[sl], s->st[sl]));
     if ((rc = mij_batch_encode(s->b[sl], cnt))) return rc;
     S_TRY(hipEventRecord(s->ev_t1[sl], s->st[sl]));
@@ -297,7 +334,7 @@ static int stream_run(mij_stream *s, int n, const FillFn &fill, const DrainFn &d
     s->stats[3] += ms * 1e-3;
     const double t0 = now_s();
     int bad = -1;
-    const int rc = parallel_for(cnt, s->threads,
+    const int rc = parallel_for(cnt, wthreads,
                                 [&](int i) { return drain(first + i, s->h_out[sl] + off[i], off[i + 1] - off[i]); }, &bad);
     s->stats[2] += now_s() - t0;
     s->stats[4] += cnt;
@@ -306,15 +343,27 @@ static int stream_run(mij_stream *s, int n, const FillFn &fill, const DrainFn &d
     return rc;
   };
 
-  int rc = nchunks ? enqueue(0) : MIJ_OK;
+  // chunk k: read (reader thread, one chunk ahead) -> upload + encode + lengths
+  // (batch k & 1's stream) -> D2H + file writes (this thread, after chunk
+  // k + 1 is enqueued).  Buffer k % NIN is refilled with chunk k + NIN only
+  // after its upload event.
+  int rc = MIJ_OK;
+  if (nchunks) start_read(0);
   for (int k = 0; k < nchunks && !rc; k++) {
-    if (k + 1 < nchunks) rc = enqueue(k + 1);  // chunk k+1 is read while the GPU works on chunk k
-    const int rc2 = finish(k);
-    if (!rc) rc = rc2;
-    if (rc && k + 1 < nchunks) {  // drain what is still queued before returning
-      hipStreamSynchronize(s->st[0]);
-      hipStreamSynchronize(s->st[1]);
+    rc = join_read(k);
+    if (!rc && k + 1 < nchunks) {
+      if (k + 1 >= NIN) S_TRY(hipEventSynchronize(s->ev_up[(k + 1) % NIN]));
+      start_read(k + 1);
     }
+    if (!rc) rc = enqueue(k);
+    if (!rc && k >= 1) rc = finish(k - 1);  // chunk k - 1 drains while k uploads and k + 1 is read
+  }
+  if (!rc && nchunks) rc = finish(nchunks - 1);
+  for (auto &r : rd)
+    if (r.th.joinable()) r.th.join();  // (an error left a read running)
+  if (rc) {  // drain what is still queued before returning
+    hipStreamSynchronize(s->st[0]);
+    hipStreamSynchronize(s->st[1]);
   }
   s->stats[0] = now_s() - t_start;
   if (!rc) mij_clear_error();

@@ -25,7 +25,13 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef unsigned u4v __attribute__((ext_vector_type(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
 
-template <int NW, int DEPTH, int SH>
+template <bool NT>
+__device__ __forceinline__ void st16(u4v v, u4v *p) {
+  if (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+template <int NW, int DEPTH, int SH, bool NTL = true, bool NTS = true>
 __global__ __launch_bounds__(64 * NW, 1) void k_stream(const uint8_t *in, short *coef, int nframes, int per_wg,
                                                        int spin1, int spin2, int store, unsigned *sink) {
   // SH 0: 128x16 tiles (16 rows x 384 B); SH 1: 256x8 tiles (8 rows x 768 B);
@@ -50,6 +56,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_stream(const uint8_t *in, short 
     const uint8_t *s = (const uint8_t *)(uintptr_t)(((unsigned long long)hi << 32) | lo);
     const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_t *)s_raw[wave][slot]);
     if (lane < 48) {
+      if (NTL)
       asm volatile(
           "s_mov_b32 m0, %8\n\tglobal_load_lds_dwordx4 %0, %9 nt\n\t"
           "s_add_u32 m0, %8, 768\n\tglobal_load_lds_dwordx4 %1, %9 nt\n\t"
@@ -59,6 +66,20 @@ __global__ __launch_bounds__(64 * NW, 1) void k_stream(const uint8_t *in, short 
           "s_add_u32 m0, %8, 3840\n\tglobal_load_lds_dwordx4 %5, %9 nt\n\t"
           "s_add_u32 m0, %8, 4608\n\tglobal_load_lds_dwordx4 %6, %9 nt\n\t"
           "s_add_u32 m0, %8, 5376\n\tglobal_load_lds_dwordx4 %7, %9 nt"
+          :
+          : "v"(o), "v"(o + rs), "v"(o + 2 * rs), "v"(o + 3 * rs), "v"(o + 4 * rs),
+            "v"(o + 5 * rs), "v"(o + 6 * rs), "v"(o + 7 * rs), "s"(lds0), "s"(s)
+          : "memory", "m0", "scc");
+      else
+      asm volatile(
+          "s_mov_b32 m0, %8\n\tglobal_load_lds_dwordx4 %0, %9\n\t"
+          "s_add_u32 m0, %8, 768\n\tglobal_load_lds_dwordx4 %1, %9\n\t"
+          "s_add_u32 m0, %8, 1536\n\tglobal_load_lds_dwordx4 %2, %9\n\t"
+          "s_add_u32 m0, %8, 2304\n\tglobal_load_lds_dwordx4 %3, %9\n\t"
+          "s_add_u32 m0, %8, 3072\n\tglobal_load_lds_dwordx4 %4, %9\n\t"
+          "s_add_u32 m0, %8, 3840\n\tglobal_load_lds_dwordx4 %5, %9\n\t"
+          "s_add_u32 m0, %8, 4608\n\tglobal_load_lds_dwordx4 %6, %9\n\t"
+          "s_add_u32 m0, %8, 5376\n\tglobal_load_lds_dwordx4 %7, %9"
           :
           : "v"(o), "v"(o + rs), "v"(o + 2 * rs), "v"(o + 3 * rs), "v"(o + 4 * rs),
             "v"(o + 5 * rs), "v"(o + 6 * rs), "v"(o + 7 * rs), "s"(lds0), "s"(s)
@@ -105,8 +126,8 @@ __global__ __launch_bounds__(64 * NW, 1) void k_stream(const uint8_t *in, short 
       short *lin = coef + (long long)tc * 3072 + 8 * lane;
       for (int nt = 0; nt < 3; nt++) {
         u4v d1 = a + (unsigned)nt, d2 = b ^ c;
-        __builtin_nontemporal_store(d1, (u4v *)(lin + 1024 * nt));
-        __builtin_nontemporal_store(d2, (u4v *)(lin + 1024 * nt + 512));
+        st16<NTS>(d1, (u4v *)(lin + 1024 * nt));
+        st16<NTS>(d2, (u4v *)(lin + 1024 * nt + 512));
       }
     } else if (store) {
       const int f = tc / TPFs, r = tc - f * TPFs, ty = r / TXs, tx = r - ty * TXs;
@@ -122,8 +143,8 @@ __global__ __launch_bounds__(64 * NW, 1) void k_stream(const uint8_t *in, short 
           b2 = b1 + NC;
         }
         u4v d1 = a + (unsigned)nt, d2 = b ^ c;
-        __builtin_nontemporal_store(d1, (u4v *)(fc + b1 * 64 + off));
-        __builtin_nontemporal_store(d2, (u4v *)(fc + b2 * 64 + off));
+        st16<NTS>(d1, (u4v *)(fc + b1 * 64 + off));
+        st16<NTS>(d2, (u4v *)(fc + b2 * 64 + off));
       }
     } else {
       x ^= a.x ^ b.y ^ c.z;
@@ -136,12 +157,43 @@ __global__ __launch_bounds__(64 * NW, 1) void k_stream(const uint8_t *in, short 
 }
 
 
-// calibration: plain grid-stride copy, 16 B per lane, of the same byte count
-__global__ void k_copy(const u4v *in, u4v *out, long long n) {
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
-    __builtin_nontemporal_store(__builtin_nontemporal_load(in + i), out + i);
+// calibration: grid-stride copies, 16 B per lane, of the same byte count.
+// U independent 16-B loads per lane are issued before their stores (U = 1:
+// one load in flight per lane); NTL / NTS: non-temporal loads / stores.
+template <int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void k_copy(const u4v *in, u4v *out, long long n) {
+  const long long G = (long long)gridDim.x * blockDim.x;
+  for (long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += U * G) {
+    u4v v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const long long i = i0 + u * G;
+      if (i < n) v[u] = NTL ? __builtin_nontemporal_load(in + i) : in[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const long long i = i0 + u * G;
+      if (i < n) st16<NTS>(v[u], out + i);
+    }
+  }
 }
-template <int NW, int DEPTH, int SH = 0>
+template <int U, bool NTL, bool NTS>
+float run_copy(const uint8_t *in, short *coef, long long bytes, int blocks, int reps) {
+  const long long n = bytes / 16;
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  hipLaunchKernelGGL((k_copy<U, NTL, NTS>), dim3(blocks), dim3(256), 0, 0, (const u4v *)in, (u4v *)coef, n);
+  CHECK(hipEventRecord(e0));
+  for (int r = 0; r < reps; r++)
+    hipLaunchKernelGGL((k_copy<U, NTL, NTS>), dim3(blocks), dim3(256), 0, 0, (const u4v *)in, (u4v *)coef, n);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / reps;
+}
+template <int NW, int DEPTH, int SH = 0, bool NTL = true, bool NTS = true>
 float run(const uint8_t *in, short *coef, unsigned *sink, int F, int spin1, int spin2, int store, int reps) {
   int ncu = 256;
   const long long ntiles = (long long)F * TPF;  // same count for both shapes
@@ -149,15 +201,18 @@ float run(const uint8_t *in, short *coef, unsigned *sink, int F, int spin1, int 
   long long per_wg = (ntiles + grid - 1) / grid;
   if (per_wg > TPF) per_wg = TPF;
   if (getenv("PER_WG")) per_wg = atoi(getenv("PER_WG"));
+  if (getenv("GRID_MULT")) {  // more workgroups than CUs: smaller ranges per workgroup
+    per_wg = (ntiles + (long long)ncu * atoi(getenv("GRID_MULT")) - 1) / ((long long)ncu * atoi(getenv("GRID_MULT")));
+  }
   grid = (ntiles + per_wg - 1) / per_wg;
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  hipLaunchKernelGGL((k_stream<NW, DEPTH, SH>), dim3(grid), dim3(64 * NW), 0, 0, in, coef, F, (int)per_wg, spin1, spin2, store, sink);
+  hipLaunchKernelGGL((k_stream<NW, DEPTH, SH, NTL, NTS>), dim3(grid), dim3(64 * NW), 0, 0, in, coef, F, (int)per_wg, spin1, spin2, store, sink);
   CHECK(hipDeviceSynchronize());
   CHECK(hipEventRecord(e0));
   for (int r = 0; r < reps; r++)
-    hipLaunchKernelGGL((k_stream<NW, DEPTH, SH>), dim3(grid), dim3(64 * NW), 0, 0, in, coef, F, (int)per_wg, spin1, spin2, store, sink);
+    hipLaunchKernelGGL((k_stream<NW, DEPTH, SH, NTL, NTS>), dim3(grid), dim3(64 * NW), 0, 0, in, coef, F, (int)per_wg, spin1, spin2, store, sink);
   CHECK(hipEventRecord(e1));
   CHECK(hipEventSynchronize(e1));
   float ms;
@@ -182,29 +237,31 @@ int main(int argc, char **argv) {
     fflush(stdout);
   };
   const int R = 5;
-  {
-    const long long n = (long long)in_b / 16;
-    hipEvent_t e0, e1;
-    CHECK(hipEventCreate(&e0));
-    CHECK(hipEventCreate(&e1));
-    hipLaunchKernelGGL(k_copy, dim3(256 * 16), dim3(256), 0, 0, (const u4v *)in, (u4v *)coef, n);
-    CHECK(hipEventRecord(e0));
-    for (int r = 0; r < R; r++) hipLaunchKernelGGL(k_copy, dim3(256 * 16), dim3(256), 0, 0, (const u4v *)in, (u4v *)coef, n);
-    CHECK(hipEventRecord(e1));
-    CHECK(hipEventSynchronize(e1));
-    float ms;
-    CHECK(hipEventElapsedTime(&ms, e0, e1));
-    ms /= R;
-    printf("plain 16-B copy of the input bytes: %.3f ms = %.0f GB/s (read + write)\n", ms, 2.0 * in_b / (ms * 1e-3) / 1e9);
-  }
-  // (256x8 tiles only with contiguous writes: K1's block layout needs 16-row tiles)
-  rep("12 waves depth1", run<12, 1>(in, coef, sink, F, 0, 0, 1, R));
+  // copy calibration (read + write = 2 x the input bytes; the guide's float4
+  // copy: 6.29 TB/s).  Only the best of these is the calibration.
+  auto cp = [&](const char *name, float ms) {
+    printf("copy %-40s %7.3f ms = %6.0f GB/s (read + write)\n", name, ms, 2.0 * in_b / (ms * 1e-3) / 1e9);
+    fflush(stdout);
+  };
+  cp("U1 plain, 4096 x 256", run_copy<1, false, false>(in, coef, in_b, 4096, R));
+  cp("U1 nt/nt, 4096 x 256", run_copy<1, true, true>(in, coef, in_b, 4096, R));
+  cp("U4 plain, 2048 x 256", run_copy<4, false, false>(in, coef, in_b, 2048, R));
+  cp("U4 plain, 8192 x 256", run_copy<4, false, false>(in, coef, in_b, 8192, R));
+  cp("U4 plain load, nt store, 2048 x 256", run_copy<4, false, true>(in, coef, in_b, 2048, R));
+  cp("U4 nt/nt, 2048 x 256", run_copy<4, true, true>(in, coef, in_b, 2048, R));
+  cp("U8 plain, 1024 x 256", run_copy<8, false, false>(in, coef, in_b, 1024, R));
+  cp("U8 plain, 2048 x 256", run_copy<8, false, false>(in, coef, in_b, 2048, R));
+  // K1's pattern (6.0625 B/px algorithmic) under each cache policy
+  rep("12 waves depth1 (nt DMA, nt stores: K1)", run<12, 1>(in, coef, sink, F, 0, 0, 1, R));
+  rep("12 waves depth1 plain DMA, nt stores", run<12, 1, 0, false, true>(in, coef, sink, F, 0, 0, 1, R));
+  rep("12 waves depth1 nt DMA, plain stores", run<12, 1, 0, true, false>(in, coef, sink, F, 0, 0, 1, R));
+  rep("12 waves depth1 plain DMA, plain stores", run<12, 1, 0, false, false>(in, coef, sink, F, 0, 0, 1, R));
+  rep("12 waves depth2 plain DMA, plain stores", run<12, 2, 0, false, false>(in, coef, sink, F, 0, 0, 1, R));
   rep("12 waves depth1 contiguous 6 KB writes", run<12, 1>(in, coef, sink, F, 0, 0, 2, R));
-  rep("12 waves depth1 256x8 tiles, contiguous writes", run<12, 1, 1>(in, coef, sink, F, 0, 0, 2, R));
-  rep("12 waves depth2 256x8 tiles, contiguous writes", run<12, 2, 1>(in, coef, sink, F, 0, 0, 2, R));
-  rep("12 waves depth1 spin 32+64", run<12, 1>(in, coef, sink, F, 32, 64, 1, R));
-  rep("12 waves depth1 spin 40+80", run<12, 1>(in, coef, sink, F, 40, 80, 1, R));
-  rep("16 waves depth1 spin 40+80", run<16, 1>(in, coef, sink, F, 40, 80, 1, R));
-  rep("12 waves depth1 spin 40+80 contiguous writes", run<12, 1>(in, coef, sink, F, 40, 80, 2, R));
+  rep("12 waves depth1 read only (nt DMA)", run<12, 1>(in, coef, sink, F, 0, 0, 0, R));
+  rep("12 waves depth1 read only (plain DMA)", run<12, 1, 0, false, true>(in, coef, sink, F, 0, 0, 0, R));
+  rep("16 waves depth1 plain DMA, plain stores", run<16, 1, 0, false, false>(in, coef, sink, F, 0, 0, 1, R));
+  rep("8 waves depth2 plain DMA, plain stores", run<8, 2, 0, false, false>(in, coef, sink, F, 0, 0, 1, R));
+  rep("12 waves depth1 spin 40+80 (K1-like compute)", run<12, 1>(in, coef, sink, F, 40, 80, 1, R));
   return 0;
 }
