@@ -72,6 +72,9 @@ def parse():
                     help="stream: PPM files per step (config-3 recipe contents, 16 distinct)")
     ap.add_argument("--stream-chunk", type=int, default=16, help="stream: frames per device batch")
     ap.add_argument("--frames4", type=int, default=8, help="config4 frames per step")
+    ap.add_argument("--band-emit", choices=["auto", "root", "bands"], default="auto",
+                    help="config4: JFIF byte emission on the root alone, or distributed over the bands "
+                         "(each band stuffs its own bytes; auto: bands when there is more than one rank)")
     ap.add_argument("--regions", type=int, default=100,
                     help="regions workload: rectangles per frame (main.c's diffDims holds up to 100)")
     ap.add_argument("--region-frame", default="1920x1080",
@@ -142,9 +145,11 @@ def run_config4(args, world, rank, local, dist):
     else:
         xch = sharding.DeviceExchange(dist, f"cuda:{gpu}")
 
+    emit = args.band_emit if args.band_emit != "auto" else ("bands" if world > 1 else "root")
+
     def step(events=None):
         if on_dev:
-            sharding.encode_banded_dev(band, n, xch, full, events=events)
+            sharding.encode_banded_dev(band, n, xch, full, events=events, emit=emit)
         else:
             sharding.encode_banded(band, n, xch, full)
 
@@ -211,6 +216,7 @@ def run_config4(args, world, rank, local, dist):
                    "frames_per_step": n, "width": W, "height": H, "quality": args.quality,
                    "parallelism": f"band-parallel x{world}",
                    "backend": backend,
+                   "emit": emit if on_dev else "root",
                    "protocol": ("host arrays (gloo)" if not on_dev else
                                 "device-resident (mij_band_*_async)" +
                                 (", collectives staged through host memory (gloo)" if backend == "gloo" else ""))},

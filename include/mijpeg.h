@@ -350,6 +350,23 @@ int mij_band_words_async(mij_batch *b, int n, uint32_t *d_dst, size_t cap_words)
 int mij_assemble_tables_async(mij_batch *b, int n, const uint32_t *d_ghist);
 int mij_assemble_async(mij_batch *b, int n, const uint64_t *d_allbits, int world, const uint32_t *d_src,
                        size_t stride_words);
+/* Distributed JFIF emission (the config-4 bands, sharding.encode_banded_dev
+ * with emit="bands"): after mij_band_pack_async and the all-gather of every
+ * band's d_bits into d_allbits [world][3n + 1], band `rank` stuffs the bytes
+ * of the final scans that lie wholly inside it (encoder.c:403-408) into
+ * d_dst (cap bytes), frames and scans in order; d_rec [n][3][4] (u64) gets
+ * per scan {stuffed bytes, band bits, head bits << 8 | head count, tail bits
+ * << 8 | tail count} (head: the <= 7 bits completing the byte the bands
+ * before began; tail: the bits after the last whole byte) and *d_total the
+ * band's stuffed bytes.  The band's scan words are consumed. */
+int mij_band_stuff_async(mij_batch *b, int n, const uint64_t *d_allbits, int world, int rank,
+                         uint64_t *d_rec, uint64_t *d_total, uint8_t *d_dst, size_t cap);
+/* root, after mij_assemble_tables_async: frames 0..n-1 from every band's
+ * records d_allrec [world][n][3][4] and stuffed bytes d_src [world][stride]:
+ * headers, the seam bytes between bands (stuffed when 0xFF), the pads
+ * (encoder.c:425-432), EOI, the interiors copied into place */
+int mij_assemble_stuffed_async(mij_batch *b, int n, const uint64_t *d_allrec, int world,
+                               const uint8_t *d_src, size_t stride);
 
 /* ---- diagnostics used by the test-suite -----------------------------------*/
 /* 16x16x64 i8 MFMA layout probe: A, B are 64 lanes x 16 int8, D 64 x 4 int32 */

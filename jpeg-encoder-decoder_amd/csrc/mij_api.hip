@@ -48,6 +48,11 @@ hipError_t launch_band_count(const unsigned long long *scan_bits, int n, unsigne
                              unsigned long long *bits, hipStream_t s);
 hipError_t launch_or_shift_pieces(uint32_t *raw, const Geom &g, const uint32_t *src,
                                   const unsigned long long *d_pieces, int npieces, long long max_words, hipStream_t s);
+hipError_t launch_band_stuff(const EntArgs &a, const unsigned long long *allbits, int world, int rank,
+                             unsigned long long *rec, unsigned long long *total, uint8_t *dst, unsigned long long cap,
+                             hipStream_t s);
+hipError_t launch_band_join(const EntArgs &a, const unsigned long long *allrec, int world, unsigned long long stride,
+                            unsigned long long *pieces, const uint8_t *src, hipStream_t s);
 hipError_t launch_band_assembly(const unsigned long long *allbits, int world, int n, unsigned long long stride,
                                 unsigned long long *pieces, unsigned long long *scan_bits, int *over, hipStream_t s);
 }  // namespace mij
@@ -1677,6 +1682,38 @@ extern "C" int mij_assemble_async(mij_batch *b, int n, const uint64_t *d_allbits
                                  b->stream));
   HIP_TRY(launch_emit(a, b->stream));  // k_emit_write zeroes the words it reads
   if (n >= b->raw_dirty) b->raw_dirty = 0;
+  b->asm_tables_n = 0;
+  b->last_frames = n;
+  return MIJ_OK;
+}
+
+// Distributed JFIF emission (include/mijpeg.h): the band's interiors stuffed
+// on its own GPU, the root joins them (k_band_* in mij_kernels.hip)
+extern "C" int mij_band_stuff_async(mij_batch *b, int n, const uint64_t *d_allbits, int world, int rank,
+                                    uint64_t *d_rec, uint64_t *d_total, uint8_t *d_dst, size_t cap) {
+  if (band_check(b, n, "band_stuff_async")) return g_err;
+  if (!d_allbits || !d_rec || !d_total || !d_dst || world < 1 || rank < 0 || rank >= world)
+    return fail(MIJ_EINVAL, "band_stuff_async: bad arguments");
+  if (n != b->band_async_n) return fail(MIJ_EINVAL, "band_stuff_async: needs mij_band_pack_async of the same frames first");
+  EntArgs a = ent_args(b, n, 0, true);  // (bit_base: the heads' shifts)
+  a.ff_pack = 0;
+  HIP_TRY(launch_band_stuff(a, (const unsigned long long *)d_allbits, world, rank, (unsigned long long *)d_rec,
+                            (unsigned long long *)d_total, d_dst, (unsigned long long)cap, b->stream));
+  b->band_async_n = 0;  // the scan words are consumed (zeroed)
+  if (n >= b->raw_dirty) b->raw_dirty = 0;
+  return MIJ_OK;
+}
+
+extern "C" int mij_assemble_stuffed_async(mij_batch *b, int n, const uint64_t *d_allrec, int world,
+                                          const uint8_t *d_src, size_t stride) {
+  if (band_check(b, n, "assemble_stuffed_async", true)) return g_err;
+  if (!d_allrec || !d_src || world < 1) return fail(MIJ_EINVAL, "assemble_stuffed_async: bad arguments");
+  if (n != b->asm_tables_n)
+    return fail(MIJ_EINVAL, "assemble_stuffed_async: needs mij_assemble_tables_async of the same frames first");
+  if (ensure_pieces(b, (size_t)world * n * 3)) return g_err;
+  EntArgs a = ent_args(b, n);
+  HIP_TRY(launch_band_join(a, (const unsigned long long *)d_allrec, world, (unsigned long long)stride, b->d_pieces,
+                           d_src, b->stream));
   b->asm_tables_n = 0;
   b->last_frames = n;
   return MIJ_OK;

@@ -3295,12 +3295,90 @@ __global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
   }
 }
 
+// The stuffed bytes (encoder.c:403-408: 0x00 after every 0xFF) of chunk
+// [cb, cb + EMIT_CH) of a byte stream nbytes long whose big-endian word w is
+// word(w), written at out + o0; tot = the chunk's 0xFF bytes.  after_load(w)
+// runs once per loaded word, after the load (k_emit_write zeroes the scan
+// word there).  Called by a whole 256-thread workgroup; s_out: 2 * EMIT_CH
+// bytes, red: 4 ints of LDS.
+template <class WordFn, class AfterFn>
+__device__ __forceinline__ void stuff_chunk(const WordFn &word, const AfterFn &after_load, unsigned long long nbytes,
+                                            unsigned long long cb, unsigned long long o0, int tot, uint8_t *out,
+                                            uint8_t *s_out, int *red) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int WPW = EMIT_CH / 16;  // stream words per wave
+  // Stuffed bytes into LDS, chunk-relative.  Wave v takes stream words
+  // [WPW v, WPW v + WPW) of the chunk, lane l word 64 k + l of it in round
+  // k: consecutive lanes write consecutive bytes (no LDS bank conflicts).
+  // All of the lane's words are loaded at once; a word's offset is 4 w +
+  // the 0xFF bytes before it (wave totals through LDS, a wave scan per round).
+  const unsigned long long wb0 = cb + (unsigned long long)wave * (4 * WPW);
+  uint32_t wds[WPW / 64];
+  int lims[WPW / 64];
+  int wcnt = 0;
+#pragma unroll
+  for (int k = 0; k < WPW / 64; k++) {
+    const unsigned long long mb = wb0 + 4ull * (64 * k + lane);
+    lims[k] = mb < nbytes ? (int)min(nbytes - mb, 4ull) : 0;
+    wds[k] = lims[k] ? word(mb >> 2) : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < WPW / 64; k++) wcnt += lims[k] ? ff_bytes(wds[k], lims[k]) : 0;
+#pragma unroll
+  for (int k = 0; k < WPW / 64; k++)
+    if (lims[k]) after_load((wb0 + 4ull * (64 * k + lane)) >> 2);
+  for (int off = 32; off; off >>= 1) wcnt += __shfl_xor(wcnt, off);
+  if (lane == 0) red[wave] = wcnt;
+  __syncthreads();
+  int carry = wave * 4 * WPW;
+  for (int q = 0; q < wave; q++) carry += red[q];
+#pragma unroll
+  for (int k = 0; k < WPW / 64; k++) {
+    const int lim = lims[k];
+    const uint32_t wd = wds[k];
+    const int cf = lim ? ff_bytes(wd, lim) : 0;
+    const int incl = (int)wave_scan64((uint32_t)(lim + cf));
+    int op = carry + incl - (lim + cf);
+    carry += __shfl(incl, 63);
+    if (cf == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (j < lim) s_out[op + j] = (uint8_t)(wd >> (24 - 8 * j));
+    } else {
+      for (int j = 0; j < lim; j++) {
+        const uint8_t byte = (uint8_t)(wd >> (24 - 8 * j));
+        s_out[op++] = byte;
+        if (byte == 0xFF) s_out[op++] = 0x00;
+      }
+    }
+  }
+  __syncthreads();
+  // copy out: head bytes up to a 4-byte boundary, whole words (re-aligned
+  // from LDS words with v_alignbyte), tail bytes; every byte of
+  // [o0, o0 + clen) belongs to this chunk alone
+  const int clen = (int)min((unsigned long long)EMIT_CH, nbytes - cb) + tot;
+  const int head = min(clen, (int)((4 - (o0 & 3)) & 3));
+  const int nwd = (clen - head) >> 2;
+  if (tid < head) out[o0 + tid] = s_out[tid];
+  const int tl = clen - head - 4 * nwd;
+  if (tid < tl) out[o0 + head + 4 * nwd + tid] = s_out[head + 4 * nwd + tid];
+  const uint32_t *s32 = (const uint32_t *)s_out;
+  uint32_t *d32 = (uint32_t *)(out + o0 + head);
+  const int sh = head & 3;  // LDS byte offset of output word j = head + 4j
+  for (int j = tid; j < nwd; j += 256) {
+    const int m = (head >> 2) + j;
+    const uint32_t lo = s32[m];
+    d32[j] = sh ? __builtin_amdgcn_alignbyte(s32[m + 1], lo, sh) : lo;
+  }
+  __syncthreads();
+}
+
 // k_emit_write: the stuffed bytes of every chunk at the offset k_emit_scan gave.
 __global__ __launch_bounds__(256) void k_emit_write(EntArgs a) {
   __shared__ uint8_t s_out[2 * EMIT_CH];
   __shared__ int red[4];
   const int slot = blockIdx.x % a.emit_slots, f = blockIdx.x / a.emit_slots;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x;
   // every scan-buffer word read here is zeroed after use: k_pack_lb needs
   // all-zero buffers (a failed frame's buffers are cleared whole) -- except
   // in seam mode, where k_pack_lb stores whole words and nothing is zeroed
@@ -3326,86 +3404,287 @@ __global__ __launch_bounds__(256) void k_emit_write(EntArgs a) {
       if (w < ((nbits + 31) >> 5)) ((uint32_t *)scan_raw(a, f, comp))[w] = 0;
     }
   }
-  constexpr int WPW = EMIT_CH / 16;  // stream words per wave
   // the frame's chunks, scan after scan, dealt round-robin to its workgroups
   for (long long i = slot; i < nch[0] + nch[1] + nch[2]; i += a.emit_slots) {
     const int comp = i < nch[0] ? 0 : (i < nch[0] + nch[1] ? 1 : 2);
     const long long c = i - (comp == 0 ? 0 : (comp == 1 ? nch[0] : nch[0] + nch[1]));
     const unsigned long long nbytes = a.scan_bits[f * 3 + comp] >> 3;
     uint32_t *raw = (uint32_t *)scan_raw(a, f, comp);
-    const uint32_t *cnt = a.ffc + (long long)(f * 3 + comp) * nchmax;
-    const uint32_t *offs = a.choff + (long long)(f * 3 + comp) * nchmax;
-    const unsigned long long cb = (unsigned long long)c * EMIT_CH;
-    const unsigned long long o0 = offs[c];
-    const int tot = (int)cnt[c];
-    // Stuffed bytes into LDS, chunk-relative.  Wave v takes stream words
-    // [WPW v, WPW v + WPW) of the chunk, lane l word 64 k + l of it in round
-    // k: consecutive lanes write consecutive bytes (no LDS bank conflicts).
-    // All of the lane's words are loaded at once; a word's offset is 4 w +
-    // the 0xFF bytes before it (wave totals through LDS, a wave scan per round).
-    const unsigned long long wb0 = cb + (unsigned long long)wave * (4 * WPW);
-    uint32_t wds[WPW / 64];
-    int lims[WPW / 64];
-    int wcnt = 0;
-#pragma unroll
-    for (int k = 0; k < WPW / 64; k++) {
-      const unsigned long long mb = wb0 + 4ull * (64 * k + lane);
-      lims[k] = mb < nbytes ? (int)min(nbytes - mb, 4ull) : 0;
-      wds[k] = lims[k] ? raw[mb >> 2] : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < WPW / 64; k++) wcnt += lims[k] ? ff_bytes(wds[k], lims[k]) : 0;
-    if (zero) {
-#pragma unroll
-      for (int k = 0; k < WPW / 64; k++)
-        if (lims[k]) raw[(wb0 + 4ull * (64 * k + lane)) >> 2] = 0u;
-    }
-    for (int off = 32; off; off >>= 1) wcnt += __shfl_xor(wcnt, off);
-    if (lane == 0) red[wave] = wcnt;
-    __syncthreads();
-    if (tid == 0) a.ffc[(long long)(f * 3 + comp) * nchmax + c] = 0;  // read: left zeroed (ff_pack adds)
-    int carry = wave * 4 * WPW;
-    for (int q = 0; q < wave; q++) carry += red[q];
-#pragma unroll
-    for (int k = 0; k < WPW / 64; k++) {
-      const int lim = lims[k];
-      const uint32_t wd = wds[k];
-      const int cf = lim ? ff_bytes(wd, lim) : 0;
-      const int incl = (int)wave_scan64((uint32_t)(lim + cf));
-      int op = carry + incl - (lim + cf);
-      carry += __shfl(incl, 63);
-      if (cf == 0) {
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-          if (j < lim) s_out[op + j] = (uint8_t)(wd >> (24 - 8 * j));
-      } else {
-        for (int j = 0; j < lim; j++) {
-          const uint8_t byte = (uint8_t)(wd >> (24 - 8 * j));
-          s_out[op++] = byte;
-          if (byte == 0xFF) s_out[op++] = 0x00;
-        }
-      }
-    }
-    __syncthreads();
-    // copy out: head bytes up to a 4-byte boundary, whole words (re-aligned
-    // from LDS words with v_alignbyte), tail bytes; every byte of
-    // [o0, o0 + clen) belongs to this chunk alone
-    const int clen = (int)min((unsigned long long)EMIT_CH, nbytes - cb) + tot;
-    const int head = min(clen, (int)((4 - (o0 & 3)) & 3));
-    const int nwd = (clen - head) >> 2;
-    if (tid < head) out[o0 + tid] = s_out[tid];
-    const int tl = clen - head - 4 * nwd;
-    if (tid < tl) out[o0 + head + 4 * nwd + tid] = s_out[head + 4 * nwd + tid];
-    const uint32_t *s32 = (const uint32_t *)s_out;
-    uint32_t *d32 = (uint32_t *)(out + o0 + head);
-    const int sh = head & 3;  // LDS byte offset of output word j = head + 4j
-    for (int j = tid; j < nwd; j += 256) {
-      const int m = (head >> 2) + j;
-      const uint32_t lo = s32[m];
-      d32[j] = sh ? __builtin_amdgcn_alignbyte(s32[m + 1], lo, sh) : lo;
-    }
-    __syncthreads();
+    const long long ci = (long long)(f * 3 + comp) * nchmax + c;
+    const int tot = (int)a.ffc[ci];
+    const unsigned long long o0 = a.choff[ci];
+    stuff_chunk([&](unsigned long long w) { return raw[w]; },
+                [&](unsigned long long w) {
+                  if (zero) raw[w] = 0u;
+                },
+                nbytes, (unsigned long long)c * EMIT_CH, o0, tot, out, s_out, red);
+    if (tid == 0) a.ffc[ci] = 0;  // read: left zeroed (ff_pack adds)
   }
+}
+
+// ===========================================================================
+// Distributed JFIF emission of one large frame in bands (config 4, SURVEY.md
+// §8(e)).  After every band packed its scans from bit 0 and the bands' bit
+// counts were all-gathered, band r knows where each of its scans starts in
+// the frame's scan: bit B = the bits of bands 0..r-1 (encoder.c:462-502's
+// running bit position).  The final stream's bytes that lie wholly inside
+// the band (its "interior", from the first byte boundary at or after B) are
+// stuffed here, on the band's own GPU (k_emit_count on the band's words read
+// shifted by the head, k_band_stuff_scan, k_band_write); the bits before
+// that boundary (the head, <= 7, completing the byte the previous band
+// started) and after the last whole interior byte (the tail) go to the root
+// in a per-scan record.  The root then only writes headers, the seam bytes
+// (previous tail | head, stuffed when 0xFF), the pads and EOI, and copies the
+// bands' stuffed interiors into place (k_band_join, k_copy_bytes).
+// Record per (frame, scan), four u64: stuffed interior bytes; bits; head
+// bits << 8 | head count; tail bits << 8 | tail count.
+// ===========================================================================
+constexpr int BREC = 4;
+
+// per (frame, scan): the band's start offset and head/tail, the interior's
+// byte count into scan_bits (as bits, for k_emit_count and the writer) and
+// the head shift into bit_base; one thread per scan
+__global__ void k_band_stuff_prep(EntArgs a, const unsigned long long *allbits, int world, int rank,
+                                  unsigned long long *rec) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // f * 3 + comp
+  if (i >= 3 * a.nframes) return;
+  const int f = i / 3, comp = i - 3 * f;
+  unsigned long long B = 0;
+  for (int r = 0; r < rank; r++) B += allbits[(long long)r * (3 * a.nframes + 1) + i];
+  const unsigned long long bits = allbits[(long long)rank * (3 * a.nframes + 1) + i];
+  const uint32_t *raw = scan_raw(a, f, comp);
+  const uint32_t h0 = (uint32_t)((8 - (B & 7)) & 7);
+  const uint32_t h = bits < h0 ? (uint32_t)bits : h0;  // head: completes the byte before
+  const unsigned long long ni = (bits - h) >> 3;        // whole bytes after the head
+  const uint32_t t = (uint32_t)((bits - h) & 7);        // tail bits
+  // bit j of the band's stream (big-endian words)
+  auto bits_at = [&](unsigned long long j, uint32_t n) -> uint32_t {  // n <= 8, j + n <= bits
+    if (!n) return 0u;
+    const unsigned long long w = j >> 5;
+    const uint32_t o = (uint32_t)(j & 31);
+    const uint64_t two = ((uint64_t)raw[w] << 32) | (o + n > 32 ? raw[w + 1] : 0u);
+    return (uint32_t)(two >> (64 - o - n)) & ((1u << n) - 1u);
+  };
+  unsigned long long *rc = rec + (long long)i * BREC;
+  rc[1] = bits;
+  rc[2] = ((unsigned long long)bits_at(0, h) << 8) | h;
+  rc[3] = ((unsigned long long)bits_at(h + 8 * ni, t) << 8) | t;
+  a.scan_bits[i] = 8 * ni;
+  const_cast<uint32_t *>(a.bit_base)[f * 4 + comp] = h;
+}
+
+// the band's interiors in (frame, scan) order into dst: every chunk's output
+// offset (an exclusive scan of the 0xFF counts, frames and scans in order),
+// the stuffed bytes per scan into rec[0] and the band's total into *total;
+// one workgroup
+__global__ __launch_bounds__(256) void k_band_stuff_scan(EntArgs a, unsigned long long *rec,
+                                                         unsigned long long *total) {
+  __shared__ int red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long long nchmax = emit_chunks(a.g);
+  unsigned long long pos = 0;
+  for (int i = 0; i < 3 * a.nframes; i++) {
+    const unsigned long long nbytes = a.scan_bits[i] >> 3;
+    const long long nch = (long long)((nbytes + EMIT_CH - 1) / EMIT_CH);
+    const uint32_t *cnt = a.ffc + (long long)i * nchmax;
+    uint32_t *off = a.choff + (long long)i * nchmax;
+    unsigned long long carry = 0;
+    for (long long c0 = 0; c0 < nch; c0 += 256) {
+      const long long c = c0 + tid;
+      const int v = c < nch ? (int)cnt[c] : 0;
+      const int incl = (int)wave_scan64((uint32_t)v);
+      if (lane == 63) red[wave] = incl;
+      __syncthreads();
+      int wb = 0, tot = 0;
+      for (int q = 0; q < 4; q++) {
+        if (q < wave) wb += red[q];
+        tot += red[q];
+      }
+      __syncthreads();
+      if (c < nch) off[c] = (uint32_t)(pos + (unsigned long long)c * EMIT_CH + carry + wb + incl - v);
+      carry += tot;
+    }
+    if (tid == 0) rec[(long long)i * BREC] = nbytes + carry;
+    pos += nbytes + carry;
+  }
+  if (tid == 0) *total = pos;
+}
+
+// the band's word w of scan (f, comp) read shifted left by its head
+__device__ __forceinline__ uint32_t shifted_word(const uint32_t *raw, unsigned long long w, uint32_t h) {
+  return h ? __builtin_amdgcn_alignbit(raw[w], raw[w + 1], 32 - h) : raw[w];
+}
+
+// k_emit_count on the shifted interiors
+__global__ __launch_bounds__(256) void k_band_count_ff(EntArgs a) {
+  __shared__ int red[4];
+  const int slot = blockIdx.x % a.emit_slots, f = blockIdx.x / a.emit_slots;
+  long long nch[3];
+  unsigned long long nbs[3];
+#pragma unroll
+  for (int comp = 0; comp < 3; comp++) {
+    nbs[comp] = a.scan_bits[f * 3 + comp] >> 3;
+    nch[comp] = (long long)((nbs[comp] + EMIT_CH - 1) / EMIT_CH);
+  }
+  for (long long i = slot; i < nch[0] + nch[1] + nch[2]; i += a.emit_slots) {
+    const int comp = i < nch[0] ? 0 : (i < nch[0] + nch[1] ? 1 : 2);
+    const long long c = i - (comp == 0 ? 0 : (comp == 1 ? nch[0] : nch[0] + nch[1]));
+    const unsigned long long nbytes = nbs[comp];
+    const uint32_t *raw = scan_raw(a, f, comp);
+    const uint32_t h = a.bit_base[f * 4 + comp];
+    const unsigned long long b0 = (unsigned long long)c * EMIT_CH + threadIdx.x * (EMIT_CH / 256);
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < EMIT_CH / 1024; k++) {
+      const unsigned long long mb = b0 + 4 * k;
+      if (mb < nbytes) cnt += ff_bytes(shifted_word(raw, mb >> 2, h), (int)min(nbytes - mb, 4ull));
+    }
+    const int tot = block_sum256(cnt, red);
+    if (threadIdx.x == 0) a.ffc[(long long)(f * 3 + comp) * emit_chunks(a.g) + c] = (uint32_t)tot;
+  }
+}
+
+// the stuffed interiors at the offsets k_band_stuff_scan gave (dst: the
+// band's buffer, cap bytes: a chunk that would end past it is not written,
+// and the counts say so to the caller via the total)
+__global__ __launch_bounds__(256) void k_band_write(EntArgs a, uint8_t *dst, unsigned long long cap) {
+  __shared__ uint8_t s_out[2 * EMIT_CH];
+  __shared__ int red[4];
+  const int slot = blockIdx.x % a.emit_slots, f = blockIdx.x / a.emit_slots;
+  const long long nchmax = emit_chunks(a.g);
+  long long nch[3];
+#pragma unroll
+  for (int comp = 0; comp < 3; comp++) nch[comp] = (long long)(((a.scan_bits[f * 3 + comp] >> 3) + EMIT_CH - 1) / EMIT_CH);
+  for (long long i = slot; i < nch[0] + nch[1] + nch[2]; i += a.emit_slots) {
+    const int comp = i < nch[0] ? 0 : (i < nch[0] + nch[1] ? 1 : 2);
+    const long long c = i - (comp == 0 ? 0 : (comp == 1 ? nch[0] : nch[0] + nch[1]));
+    const unsigned long long nbytes = a.scan_bits[f * 3 + comp] >> 3;
+    const uint32_t *raw = scan_raw(a, f, comp);
+    const uint32_t h = a.bit_base[f * 4 + comp];
+    const long long ci = (long long)(f * 3 + comp) * nchmax + c;
+    const int tot = (int)a.ffc[ci];
+    const unsigned long long o0 = a.choff[ci];
+    const unsigned long long clen = min((unsigned long long)EMIT_CH, nbytes - (unsigned long long)c * EMIT_CH) + tot;
+    if (o0 + clen <= cap)  // (workgroup-uniform)
+      stuff_chunk([&](unsigned long long w) { return shifted_word(raw, w, h); }, [](unsigned long long) {}, nbytes,
+                  (unsigned long long)c * EMIT_CH, o0, tot, dst, s_out, red);
+    if (threadIdx.x == 0) a.ffc[ci] = 0;  // left zeroed for the next count
+  }
+}
+
+// the band's scan words zeroed again (k_pack_lb's band form ORs onto zero):
+// the words of its bits only
+__global__ void k_band_zero(EntArgs a, const unsigned long long *rec) {
+  const int i = blockIdx.y;  // f * 3 + comp
+  const int f = i / 3, comp = i - 3 * f;
+  uint32_t *raw = (uint32_t *)scan_raw(a, f, comp);
+  const unsigned long long nw = (rec[(long long)i * BREC + 1] + 31) >> 5;
+  for (unsigned long long w = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; w < nw;
+       w += (unsigned long long)gridDim.x * blockDim.x)
+    raw[w] = 0u;
+}
+
+// root: frame f from every band's records allrec[world][n][3][BREC] and
+// stuffed interiors src[world][stride]: headers, per scan the SOS, the seam
+// bytes between the bands (the pending bits of the bands before, completed
+// by the next band's head: encoder.c:385-415, stuffed when 0xFF), the pad
+// (:425-432) and EOI; the interiors' copies go to the piece table
+// pieces[f][world][3] = {src offset, dst offset, bytes} for k_copy_bytes.
+// One workgroup per frame.
+__global__ __launch_bounds__(256) void k_band_join(EntArgs a, const unsigned long long *allrec, int world,
+                                                   unsigned long long stride, unsigned long long *pieces) {
+  const int f = blockIdx.x, tid = threadIdx.x;
+  const int n = a.nframes;
+  uint8_t *out = a.out + (long long)f * a.g.out_cap;
+  __shared__ int s_n[4];
+  __shared__ int s_bad;
+  if (tid == 0) {
+    // the frame fits its output (headers, markers and pads within 1024 B)
+    unsigned long long need = 1024;
+    for (int r = 0; r < world; r++)
+      for (int c = 0; c < 3; c++) need += 2 * allrec[(((long long)r * n + f) * 3 + c) * BREC] + 4;
+    s_bad = a.err[f] || need > (unsigned long long)a.g.out_cap;
+    for (int r = 0; r < world && !s_bad; r++) {  // every band's interiors inside its stride
+      unsigned long long end = 0;
+      for (int i = 0; i < 3 * n; i++) end += allrec[((long long)r * n * 3 + i) * BREC];
+      s_bad = end > stride;
+    }
+  }
+  __syncthreads();
+  if (s_bad) {
+    if (tid == 0) {
+      a.out_len[f] = 0;
+      a.err[f] = a.err[f] ? a.err[f] : 3;
+      for (int r = 0; r < world; r++)
+        for (int c = 0; c < 3; c++) pieces[(((long long)f * world + r) * 3 + c) * 3 + 2] = 0;
+    }
+    return;
+  }
+  const int hlen = emit_headers(a, f, out, s_n);
+  if (tid != 0) return;
+  unsigned long long pos = (unsigned long long)hlen;
+  for (int c = 0; c < 3; c++) {
+    const uint8_t sos[10] = {0xFF, 0xDA, 0x00, 0x08, 0x01, (uint8_t)(c + 1), (uint8_t)(c ? 0x11 : 0x00), 0x00, 0x3F, 0x00};
+    for (int i = 0; i < 10; i++) out[pos + i] = sos[i];
+    pos += 10;
+    uint32_t pend = 0, np = 0;  // bits of the byte being filled (np < 8)
+    unsigned long long total_bits = 0;
+    for (int r = 0; r < world; r++) {
+      const unsigned long long *rc = allrec + (((long long)r * n + f) * 3 + c) * BREC;
+      // this band's interiors start in its buffer after those of the earlier scans
+      unsigned long long so = 0;
+      for (int i = 0; i < f * 3 + c; i++) so += allrec[((long long)r * n * 3 + i) * BREC];
+      const uint32_t h = (uint32_t)(rc[2] & 255), hv = (uint32_t)(rc[2] >> 8);
+      const uint32_t t = (uint32_t)(rc[3] & 255), tv = (uint32_t)(rc[3] >> 8);
+      total_bits += rc[1];
+      pend = (pend << h) | hv;
+      np += h;
+      if (np == 8) {  // a seam byte completed
+        out[pos++] = (uint8_t)pend;
+        if ((pend & 255) == 0xFF) out[pos++] = 0x00;
+        pend = np = 0;
+      }
+      unsigned long long *pc = pieces + (((long long)f * world + r) * 3 + c) * 3;
+      pc[0] = (unsigned long long)r * stride + so;
+      pc[1] = (unsigned long long)f * a.g.out_cap + pos;
+      pc[2] = rc[0];
+      pos += rc[0];
+      // the tail (t > 0 only after the head reached a byte boundary: pend
+      // is empty then) starts the next byte
+      pend = (pend << t) | tv;
+      np += t;
+    }
+    a.scan_bits[f * 3 + c] = total_bits;
+    // fill_last_byte (:425-432): the free low bits set, never stuffed; a
+    // whole 0xFF when the scan ended on a byte boundary
+    out[pos++] = np ? (uint8_t)((pend << (8 - np)) | ((1u << (8 - np)) - 1u)) : (uint8_t)0xFF;
+  }
+  out[pos] = 0xFF;
+  out[pos + 1] = 0xD9;
+  a.out_len[f] = pos + 2;
+}
+
+// byte copies of the piece table {src offset, dst offset, bytes} (blockIdx.y
+// = piece; destination words whole, sources re-aligned with v_alignbyte)
+__global__ __launch_bounds__(256) void k_copy_bytes(uint8_t *dst, const uint8_t *src, const unsigned long long *pieces) {
+  const unsigned long long *pc = pieces + 3 * (long long)blockIdx.y;
+  const unsigned long long so = pc[0], dof = pc[1], n = pc[2];
+  if (!n) return;
+  const unsigned long long G = (unsigned long long)gridDim.x * blockDim.x;
+  const unsigned long long t0 = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+  // head bytes up to the destination's word boundary, then whole words
+  const unsigned long long head = min(n, (4 - (dof & 3)) & 3);
+  if (t0 < head) dst[dof + t0] = src[so + t0];
+  const unsigned long long nw = (n - head) >> 2, s1 = so + head;
+  const uint32_t *sw = (const uint32_t *)(src + (s1 & ~3ull));
+  const uint32_t sh = (uint32_t)(s1 & 3);
+  uint32_t *dw = (uint32_t *)(dst + dof + head);
+  for (unsigned long long j = t0; j < nw; j += G) {
+    const uint32_t lo = sw[j];
+    dw[j] = sh ? __builtin_amdgcn_alignbyte(sw[j + 1], lo, sh) : lo;
+  }
+  const unsigned long long tl = n - head - 4 * nw;
+  if (t0 < tl) dst[dof + head + 4 * nw + t0] = src[so + head + 4 * nw + t0];
 }
 
 // ---- region batches: each region (x, y, w, h) of one frame into its slot ---
@@ -3852,6 +4131,26 @@ hipError_t launch_emit(const EntArgs &a0, hipStream_t s) {
     hipLaunchKernelGGL(k_emit_count, dim3(a.nframes * a.emit_slots), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_emit_scan, dim3(a.nframes), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_emit_write, dim3(a.nframes * a.emit_slots), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_band_stuff(const EntArgs &a0, const unsigned long long *allbits, int world, int rank,
+                             unsigned long long *rec, unsigned long long *total, uint8_t *dst, unsigned long long cap,
+                             hipStream_t s) {
+  EntArgs a = a0;
+  if (a.emit_slots < 1) a.emit_slots = EMIT_SLOTS;
+  const int ns = 3 * a.nframes;
+  hipLaunchKernelGGL(k_band_stuff_prep, dim3((ns + 63) / 64), dim3(64), 0, s, a, allbits, world, rank, rec);
+  hipLaunchKernelGGL(k_band_count_ff, dim3(a.nframes * a.emit_slots), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_band_stuff_scan, dim3(1), dim3(256), 0, s, a, rec, total);
+  hipLaunchKernelGGL(k_band_write, dim3(a.nframes * a.emit_slots), dim3(256), 0, s, a, dst, cap);
+  hipLaunchKernelGGL(k_band_zero, dim3(64, ns), dim3(256), 0, s, a, rec);
+  return hipGetLastError();
+}
+hipError_t launch_band_join(const EntArgs &a, const unsigned long long *allrec, int world, unsigned long long stride,
+                            unsigned long long *pieces, const uint8_t *src, hipStream_t s) {
+  hipLaunchKernelGGL(k_band_join, dim3(a.nframes), dim3(256), 0, s, a, allrec, world, stride, pieces);
+  hipLaunchKernelGGL(k_copy_bytes, dim3(64, a.nframes * world * 3), dim3(256), 0, s, a.out, src,
+                     (const unsigned long long *)pieces);
   return hipGetLastError();
 }
 hipError_t launch_gather_regions(uint8_t *dst, long long slot_bytes, int pitch, const uint8_t *src,

@@ -299,7 +299,7 @@ class StagedExchange(DeviceExchange):
         return None
 
 
-def encode_banded_dev(band, n: int, xch, frame_batch=None, events=None):
+def encode_banded_dev(band, n: int, xch, frame_batch=None, events=None, emit: str = "root"):
     """encode_banded with the device-resident protocol: the last DCs (int16
     [n, 4], gathered as int32 pairs), the histograms (summed in place), the
     bit counts (gathered) and the packed words (gathered to the root) never
@@ -310,7 +310,20 @@ def encode_banded_dev(band, n: int, xch, frame_batch=None, events=None):
     The root's frame_batch (an assembler) builds its tables on its own stream
     while the bands pack, then assembles.  `events`: optional list that
     receives (name, torch.cuda.Event) pairs recorded on the band stream after
-    each phase.  Returns nothing; read the frames from frame_batch.output()."""
+    each phase.  Returns nothing; read the frames from frame_batch.output().
+
+    emit="bands" distributes the JFIF byte emission: once the bit counts are
+    gathered every band knows where its scans start, stuffs the bytes of the
+    final scans that lie wholly inside it (mij_band_stuff_async) and sends
+    those, with a record of its few edge bits per scan, to the root, which
+    writes the headers, the seam bytes between bands, the pads and EOI and
+    copies the stuffed bytes into place (mij_assemble_stuffed_async) -- the
+    root's share of the byte work no longer grows with the frame.  The price is
+    a second host read (the stuffed sizes, to size the gather exactly).
+    emit="root": the bands' packed words go to the root, which shifts them
+    into place and emits the whole frame (mij_assemble_async)."""
+    if emit not in ("root", "bands"):
+        raise ValueError(f"emit must be 'root' or 'bands', not {emit!r}")
     torch = xch.torch
     rank, world = xch.rank, xch.world
     dev = xch.device
@@ -361,16 +374,43 @@ def encode_banded_dev(band, n: int, xch, frame_batch=None, events=None):
         allbits = xch.all_gather(bits).contiguous()               # [world, 3n + 1]
         mark("pack")
         ready.synchronize()
-        stride = max(1, int(h_bounds.max()))
-        buf = torch.empty(stride, dtype=torch.int32, device=dev)
-        band.band_words_async(n, buf.data_ptr(), stride)
-        gathered = xch.gather(buf)
-        mark("words")
-        if a is None:
-            return
+        if emit == "bands":
+            # the stuffed bytes of a band <= 2x its whole bytes <= 8 x its word bound
+            cap = 8 * max(1, int(h_bounds.max()))
+            sbuf = torch.empty(cap + 48, dtype=torch.uint8, device=dev)
+            rec = torch.empty(n * 3 * 4, dtype=torch.int64, device=dev)
+            tot = torch.empty(1, dtype=torch.int64, device=dev)
+            band.band_stuff_async(n, allbits.data_ptr(), world, rank, rec.data_ptr(), tot.data_ptr(),
+                                  sbuf.data_ptr(), cap)
+            allrec = xch.all_gather(rec).contiguous()             # [world, n*3*4]
+            tots = xch.all_gather(tot)                           # [world, 1]
+            h_tot = xch.host_buffer(world)
+            d.wait_stream(s)
+            with torch.cuda.stream(d):
+                h_tot.copy_(tots.view(-1), non_blocking=True)
+                ready2 = torch.cuda.Event()
+                ready2.record(d)
+            ready2.synchronize()
+            # exact gather size (+16: the root's word copies read one word past)
+            stride = (int(h_tot.max()) + 31) & ~15
+            gathered = xch.gather(sbuf[:stride])
+            mark("stuff")
+            if a is None:
+                return
+        else:
+            stride = max(1, int(h_bounds.max()))
+            buf = torch.empty(stride, dtype=torch.int32, device=dev)
+            band.band_words_async(n, buf.data_ptr(), stride)
+            gathered = xch.gather(buf)
+            mark("words")
+            if a is None:
+                return
     a.wait_stream(s)
     with torch.cuda.stream(a):
-        frame_batch.assemble_async(n, allbits.data_ptr(), world, gathered.data_ptr(), stride)
+        if emit == "bands":
+            frame_batch.assemble_stuffed_async(n, allrec.data_ptr(), world, gathered.data_ptr(), stride)
+        else:
+            frame_batch.assemble_async(n, allbits.data_ptr(), world, gathered.data_ptr(), stride)
     # the tensors read by the assembly are freed on the band stream: keep that
     # stream behind the assembly
     s.wait_stream(a)

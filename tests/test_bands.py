@@ -323,7 +323,7 @@ def _dev_bands(port, q):
     n, H, W = frames.shape[:3]
     res = {}
 
-    def protocol(world, shrink=0):
+    def protocol(world, shrink=0, emit="root"):
         bands = []
         for r in range(world):
             r0, rows = sharding.band_rows(H, world, r)
@@ -352,14 +352,31 @@ def _dev_bands(port, q):
         # the bounds hold (at most 3 words per frame above the words)
         for d, t in zip(bound, bits):
             assert 0 <= int(d) - int(t[3 * n]) <= 3 * n
-        stride = int(torch.cat(bound).max()) - shrink
-        gathered = torch.zeros((world, stride), dtype=torch.int32, device=dev)
-        torch.cuda.synchronize()
-        for r, b in enumerate(bands):
-            b.band_words_async(n, gathered[r].data_ptr(), stride)
-            b.sync()
-        full.assemble_async(n, allbits.data_ptr(), world, gathered.data_ptr(), stride)
-        full.sync()
+        if emit == "bands":  # distributed emission: each band stuffs its interiors
+            cap = 8 * int(torch.cat(bound).max())
+            bufs = [torch.zeros(cap + 48, dtype=torch.uint8, device=dev) for _ in bands]
+            recs = [torch.empty(n * 3 * 4, dtype=torch.int64, device=dev) for _ in bands]
+            tots = [torch.empty(1, dtype=torch.int64, device=dev) for _ in bands]
+            torch.cuda.synchronize()
+            for r, b in enumerate(bands):
+                b.band_stuff_async(n, allbits.data_ptr(), world, r, recs[r].data_ptr(), tots[r].data_ptr(),
+                                   bufs[r].data_ptr(), cap)
+                b.sync()
+            stride = (int(torch.cat(tots).max()) + 31) & ~15
+            gathered = torch.stack([x[:stride] for x in bufs]).contiguous()
+            allrec = torch.stack(recs).contiguous()
+            # every band's words are consumed: zero again for the next pack
+            full.assemble_stuffed_async(n, allrec.data_ptr(), world, gathered.data_ptr(), stride)
+            full.sync()
+        else:
+            stride = int(torch.cat(bound).max()) - shrink
+            gathered = torch.zeros((world, stride), dtype=torch.int32, device=dev)
+            torch.cuda.synchronize()
+            for r, b in enumerate(bands):
+                b.band_words_async(n, gathered[r].data_ptr(), stride)
+                b.sync()
+            full.assemble_async(n, allbits.data_ptr(), world, gathered.data_ptr(), stride)
+            full.sync()
         out = []
         for f in range(n):
             try:
@@ -376,6 +393,10 @@ def _dev_bands(port, q):
 
     for world in (1, 2, 3, 4):
         res[world], res[(world, "after")] = protocol(world)
+    # distributed emission, up to one MCU row per band (20 bands of 16 rows:
+    # seam bytes between most bands, bands of a few bits per chroma scan)
+    for world in (1, 2, 3, 4, 7, 20):
+        res[(world, "bands")], res[(world, "bands_after")] = protocol(world, emit="bands")
     # a word buffer shorter than a band's words: every frame fails, nothing
     # is written past the buffer
     res["short"], _ = protocol(2, shrink=4000)
@@ -422,6 +443,10 @@ def test_device_resident_band_protocol():
         # a band batch left by the protocol encodes its own rows correctly
         r0, rows = sharding.band_rows(320, world, world - 1)
         assert res[(world, "after")] == O.cref_encode(np.ascontiguousarray(frames[0][r0:r0 + rows]))
+    for world in (1, 2, 3, 4, 7, 20):
+        assert res[(world, "bands")] == want, f"{world} bands, distributed emission"
+        r0, rows = sharding.band_rows(320, world, world - 1)
+        assert res[(world, "bands_after")] == O.cref_encode(np.ascontiguousarray(frames[0][r0:r0 + rows]))
     assert all(isinstance(o, str) for o in res["short"]), res["short"]
     assert res["nccl"] == [want, want]
     assert res["phases"] == ["start", "analyze", "histograms", "pack", "words", "assemble"]
@@ -435,7 +460,7 @@ def test_device_resident_band_protocol():
 # the gathered [world, stride] words) runs exactly as there
 # ---------------------------------------------------------------------------
 
-def _staged_rank(rank, world, port, q, spec):
+def _staged_rank(rank, world, port, q, spec, emit="root"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import hashlib
     import torch
@@ -459,7 +484,7 @@ def _staged_rank(rank, world, port, q, spec):
         xch = sharding.StagedExchange(dist, "cuda:0")
         outs = []
         for _ in range(2):  # twice: the second step reuses every buffer
-            sharding.encode_banded_dev(band, n, xch, full)
+            sharding.encode_banded_dev(band, n, xch, full, emit=emit)
             band.sync()
             if full is not None:
                 full.sync()
@@ -475,12 +500,12 @@ def _staged_rank(rank, world, port, q, spec):
         dist.destroy_process_group()
 
 
-def _run_staged(world, spec):
+def _run_staged(world, spec, emit="root"):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_staged_rank, args=(r, world, port, q, spec)) for r in range(world)]
+    procs = [ctx.Process(target=_staged_rank, args=(r, world, port, q, spec, emit)) for r in range(world)]
     for p in procs:
         p.start()
     outs = q.get(timeout=300)
@@ -490,8 +515,9 @@ def _run_staged(world, spec):
     return outs
 
 
+@pytest.mark.parametrize("emit", ["root", "bands"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_device_protocol_multi_rank_staged(world):
+def test_device_protocol_multi_rank_staged(world, emit):
     """encode_banded_dev over 2 and 3 ranks (processes on one GPU, gloo
     collectives staged through host memory): each band's first DC predicted
     from the previous rank's last DC, histograms summed, every band packed
@@ -500,15 +526,17 @@ def test_device_protocol_multi_rank_staged(world):
     import oracle as O
     import recipes
     W, H = 480, 320
-    outs = _run_staged(world, (W, H, "small"))
+    outs = _run_staged(world, (W, H, "small"), emit)
     want = [O.cref_encode(recipes.config3_frame(7, H, W)), O.cref_encode(recipes.noise(H, W, 12)),
             O.cref_encode(recipes.config3_frame(8, H, W))]
     assert outs == [want, want]
 
 
-def test_device_protocol_two_ranks_full_size(manifest):
+@pytest.mark.parametrize("emit", ["root", "bands"])
+def test_device_protocol_two_ranks_full_size(manifest, emit):
     """The same at config 4's size: 7680x4320 frame 0 in two bands, against
-    the reference build's sha256 (tests/golden/manifest.json)."""
+    the reference build's sha256 (tests/golden/manifest.json), with the
+    root's emission and with the distributed one."""
     want = manifest["config4_frame0"]
-    outs = _run_staged(2, (7680, 4320, "full"))
+    outs = _run_staged(2, (7680, 4320, "full"), emit)
     assert outs == [[(want["jpg_len"], want["jpg_sha256"])]] * 2
