@@ -567,6 +567,10 @@ __device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int
 // Bit length = code length + (symbol & 15) + ZRLs * ZRL code length for
 // every token kind (DC: symbol = class <= 11; EOB: symbol 0x00).
 constexpr uint32_t TOK_AC = 1u << 10;
+// the padding token after a segment's last one (AC symbol 0xFF, which no
+// token carries: magnitudes stop at class 11): k_pack_lb's code table holds
+// 0 for it -- no bits, no ZRLs
+constexpr uint32_t LB_NOTOK = TOK_AC | 0xFFu;
 // AC-token loop over both 32-bit mask halves at once (A/B knob; measured:
 // token K1 3.39 -> 3.49 ms, the selects cost more than the saved iterations)
 #ifndef MIJ_K1_ACMERGE
@@ -675,7 +679,13 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
   const int prev = (int)row_shr0<1>((uint32_t)dc0);
   wave_lds_sync();
   if (g == 0) {
-    if (pos == (chroma ? 7 : 15)) *segcnt = incl;
+    if (pos == (chroma ? 7 : 15)) {
+      *segcnt = incl;
+      // the segment's token count padded to a multiple of 4 with LB_NOTOK
+      // (k_pack_lb decodes 4 tokens per lane: a lane's slots are then all
+      // tokens or all padding, and no token needs a mask)
+      for (uint32_t i = incl; i & 3u; i++) tok_at(segtok, segoff + i) = LB_NOTOK;
+    }
     if (valid) {
       if (dc_diffed || pos != 0 || first_pred) {
         const int diff = dc_diffed ? dc0 : dc0 - (pos != 0 ? prev : pred0);  // :168-177
@@ -2614,13 +2624,29 @@ constexpr int LB_STEPS = MIJ_LB_STEPS, LB_STEPS_C = MIJ_LB_STEPS_C;
 static_assert(LB_STEPS_C <= LB_STEPS && 64 * LB_STEPS <= SEG_TOK, "k_pack_lb: register steps inside a slot");
 static_assert(PACK_SEGS % 64 == 0 && LB_THREADS <= 1024, "k_pack_lb: 4 segments per 16-lane row");
 
-// bits of a token (encoder.c:434-460, ZRLs :490-494); tab = [DC | AC][256]
-// len << 16 | code of this scan's tables
+// k_pack_lb's code table: per [DC | AC][symbol] the Huffman code already
+// shifted left by the symbol's magnitude bit count (cls = symbol & 15,
+// encoder.c:434-460) in bits 0-26 and the total length code length + cls in
+// bits 27-31 (<= 16 + 11 = 27 bits: magnitudes stop at class 11 after
+// encoder.c:109's clip), so a token's code is one table read and one OR;
+// symbols without a code read 0.  A token slot past the end of its segment
+// is LB_NOTOK (K1 pads every segment to a multiple of 4 tokens with it),
+// whose entry is 0: no bits, no ZRLs, nothing to mask in its decode.
+constexpr uint32_t LB_CODE = (1u << 27) - 1u;
+__device__ __forceinline__ uint32_t lb_tab_entry(uint32_t e, uint32_t sym) {
+  const uint32_t cls = sym & 15u;
+  return e ? ((e & 0xFFFFu) << cls) | (((e >> 16) + cls) << 27) : 0u;
+}
+// bits of a token (encoder.c:434-460, ZRLs :490-494 apart): code (with the
+// magnitude bits) into `code`, its length returned
 __device__ __forceinline__ uint32_t lb_tok_code(const uint32_t *tab, uint32_t t, uint32_t &code) {
-  const uint32_t sym = t & 255u, cls = sym & 15u;
-  const uint32_t e = tab[((t >> 2) & 256u) | sym];  // TOK_AC (bit 10) selects the AC table
-  code = ((e & 0xFFFFu) << cls) | (t >> 16);
-  return (e >> 16) + cls;
+  const uint32_t e = tab[((t >> 2) & 256u) | (t & 255u)];  // TOK_AC (bit 10) selects the AC table
+  code = (e & LB_CODE) | (t >> 16);
+  return e >> 27;
+}
+// its length alone
+__device__ __forceinline__ uint32_t lb_tok_len(const uint32_t *tab, uint32_t t) {
+  return tab[((t >> 2) & 256u) | (t & 255u)] >> 27;
 }
 
 // OR `len` (1..64) bits, left-aligned in v, into the big-endian word buffer at
@@ -2730,16 +2756,14 @@ __global__ __launch_bounds__(LB_THREADS, lb_occ<PW>()) void k_pack_lb(EntArgs a)
   const long long fs0 = (long long)f * G.nseg + sbase + s0;  // the group's first segment
   int nt[LB_SEGS_PER_ROW];
   uint32_t Lz = 0, zcode = 0;
-  // a step's 4 tokens (those below lim = tokens left - 4 * sub): bits, ZRLs included
+  // a step's 4 tokens (lim = tokens left - 4 * sub): bits, ZRLs included.
+  // K1 padded the segment to a multiple of 4 tokens with LB_NOTOK (0 bits),
+  // so a lane's 4 slots are all tokens (lim > 0) or all past the end
   auto step_bits = [&](const u4v &t, int lim) -> uint32_t {
     uint32_t b = 0;
 #pragma unroll
-    for (int e = 0; e < 4; e++) {
-      uint32_t code;
-      const uint32_t L = lb_tok_code(tab, t[e], code);
-      b += e < lim ? L + ((t[e] >> 8) & 3u) * Lz : 0u;
-    }
-    return b;
+    for (int e = 0; e < 4; e++) b += lb_tok_len(tab, t[e]) + ((t[e] >> 8) & 3u) * Lz;
+    return lim > 0 ? b : 0u;
   };
   // steps past the registers (segments of more than 64 * LB_STEPS tokens)
   auto load_step = [&](int k, int i0) -> u4v {
@@ -2755,14 +2779,13 @@ __global__ __launch_bounds__(LB_THREADS, lb_occ<PW>()) void k_pack_lb(EntArgs a)
 #pragma unroll
     for (int e = 0; e < 4; e++) {
       uint32_t code;
-      uint32_t L = lb_tok_code(tab, t[e], code);
-      uint32_t nzr = (t[e] >> 8) & 3u;
-      if (e >= lim) L = nzr = code = 0u;
+      const uint32_t L = lb_tok_code(tab, t[e], code);
+      const uint32_t nzr = (t[e] >> 8) & 3u;
       for (uint32_t z = nzr; z; z--) acc = (acc << Lz) | zcode;
       acc = (acc << L) | code;
       nb += L + nzr * Lz;
     }
-    return nb;
+    return lim > 0 ? nb : 0u;  // (the string of a lane past the end is never placed)
   };
   unsigned long long pacc[LB_SEGS_PER_ROW][LB_STEPS];
   uint32_t pnb[LB_SEGS_PER_ROW][LB_STEPS], bk[LB_SEGS_PER_ROW];
@@ -2784,13 +2807,14 @@ __global__ __launch_bounds__(LB_THREADS, lb_occ<PW>()) void k_pack_lb(EntArgs a)
                                  : u4v{0u, 0u, 0u, 0u};
     t0w[k] = in && sub == 0 ? a.tok0[fs0 + sl] : 0u;  // token 0 (dense array)
   }
-  for (int i = tid; i < 512; i += LB_THREADS) tab[i] = a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + i];
-  __syncthreads();
-  {
-    const uint32_t zac = tab[256 + 0xF0];
+  for (int i = tid; i < 512; i += LB_THREADS)
+    tab[i] = lb_tab_entry(a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + i], (uint32_t)i & 255u);
+  {  // the ZRL code (AC symbol 0xF0: cls 0, so the entry is code / length)
+    const uint32_t zac = a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + 256 + 0xF0];
     Lz = zac >> 16;
     zcode = zac & 0xFFFFu;
   }
+  __syncthreads();
   // ---- 1. bits of each segment.  The register steps are merged here, once
   // (phase 3 only places them); steps past them are read twice ---------------
 #pragma unroll
@@ -2940,7 +2964,7 @@ __global__ __launch_bounds__(LB_THREADS, lb_occ<PW>()) void k_pack_lb(EntArgs a)
       for (int e = 0; e < 4; e++) {
         L[e] = lb_tok_code(tab, t[e], code[e]);
         nzr[e] = (t[e] >> 8) & 3u;
-        if (e >= lim) L[e] = nzr[e] = code[e] = 0u;
+        if (lim <= 0) L[e] = nzr[e] = code[e] = 0u;  // (a lane past the end places nothing)
         nb += L[e] + nzr[e] * Lz;
       }
       return nb;
