@@ -242,9 +242,9 @@ class DeviceExchange:
     def host_buffer(self, n: int):
         """a pinned host int64 buffer of n values, reused (a step reads it
         before the next step writes it)"""
-        hb = getattr(self, "_host", None)
+        hb = getattr(self, "_hbuf", None)
         if hb is None or hb.numel() < n:
-            hb = self._host = self.torch.empty(n, dtype=self.torch.int64, pin_memory=True)
+            hb = self._hbuf = self.torch.empty(n, dtype=self.torch.int64, pin_memory=True)
         return hb[:n]
 
     def gather(self, buf):
@@ -274,23 +274,23 @@ class StagedExchange(DeviceExchange):
         if dist is None:
             raise ValueError("StagedExchange needs a process group")
 
-    def _host(self, t):
+    def _to_host(self, t):
         return t.contiguous().cpu()  # blocking copy: waits for the current stream
 
     def all_gather(self, t):
-        h = self._host(t)
+        h = self._to_host(t)
         out = self.torch.empty((self.world,) + tuple(h.shape), dtype=h.dtype)
         self.dist.all_gather(list(out.unbind(0)), h)
         return out.to(t.device)
 
     def all_reduce_sum(self, t):
-        h = self._host(t)
+        h = self._to_host(t)
         self.dist.all_reduce(h, op=self.dist.ReduceOp.SUM)
         t.copy_(h)
         return t
 
     def gather(self, buf):
-        h = self._host(buf)
+        h = self._to_host(buf)
         if self.rank == 0:
             out = self.torch.empty((self.world, h.numel()), dtype=h.dtype)
             self.dist.gather(h, gather_list=list(out.unbind(0)), dst=0)

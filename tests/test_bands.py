@@ -468,7 +468,8 @@ def _staged_rank(rank, world, port, q, spec, emit="root"):
     torch.cuda.set_device(0)  # torch's HIP runtime before the library's
     import mijpeg
     import recipes
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import datetime
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=90))
     try:
         W, H, kind = spec
         if kind == "small":
@@ -508,9 +509,23 @@ def _run_staged(world, spec, emit="root"):
     procs = [ctx.Process(target=_staged_rank, args=(r, world, port, q, spec, emit)) for r in range(world)]
     for p in procs:
         p.start()
-    outs = q.get(timeout=300)
+    # poll: a rank that fails leaves the others blocked in a collective, so
+    # stop at the first non-zero exit instead of waiting out the queue
+    import queue
+    import time
+    t_end = time.time() + 150
+    outs = None
+    while outs is None:
+        try:
+            outs = q.get(timeout=2)
+        except queue.Empty:
+            bad = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if bad or time.time() > t_end:
+                for p in procs:
+                    p.kill()
+                raise AssertionError(f"staged ranks failed (exit codes {[p.exitcode for p in procs]})")
     for p in procs:
-        p.join(timeout=120)
+        p.join(timeout=60)
         assert p.exitcode == 0
     return outs
 
