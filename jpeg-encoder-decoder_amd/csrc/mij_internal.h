@@ -136,6 +136,15 @@ __host__ __device__ inline FGeom frame_geom(const Geom &G, const int2 *fd, int f
 // Device-resident constant tables for one quality setting.
 struct Tables {
   int4 mfma_a[12 * 64];   // A fragments: 4 M-tiles x 3 digits x 64 lanes
+  // the same in band order (M-tile m = zigzag 16m..16m+15): the fused token
+  // K1 (lane group g then holds zigzag 16m + 4g .. +3 of every M-tile m)
+  int4 mfma_a_band[12 * 64];
+  // band order: an M-tile whose |N| < zlim[c][m] in every lane is all zeros
+  // (a power of two below 2^21 q (1 - 2e-6) - 6000 for the band's smallest q;
+  // 0: the band is not tested -- its zeros are too rare to pay for the test)
+  // packed for K1's SGPRs: bits 5 (4c + m) .. +4 hold log2 zlim[c][m] (0: untested)
+  unsigned long long zlog;
+  int zlim[2][4];
   float qfac[2][64];      // zigzag order: 1 / (2^21 * q)
   int qint[2][64];        // zigzag order: integer quantizer
   int dqt[2][64];         // zigzag order: DQT bytes

@@ -598,8 +598,10 @@ constexpr uint32_t LB_NOTOK = TOK_AC | 0xFFu;
 #endif
 
 // One N-tile of coefficients -> compacted token stream of its segment(s).
-// o[k] = zigzag coefficient 16g+k of block bcol (DC raw in o[0] of g == 0,
-// or the DC difference when dc_diffed).  Every lane of the wave calls this.
+// o[k] = zigzag coefficient 16g+k of block bcol, or with BAND zigzag
+// 16(k>>2) + 4g + (k&3) (the DC raw in o[0] of g == 0 either way, or the DC
+// difference when dc_diffed); zm: the bands (BAND) the wave found all zero.
+// Every lane of the wave calls this.
 // Tokens of a block, in bitstream order (encoder.c:462-502): its DC
 // difference (:434-446), the AC run/size symbols (:448-460, ZRLs folded in,
 // :490-494), then EOB unless coefficient 63 is nonzero (:479-484).  The DC of
@@ -620,46 +622,87 @@ __device__ __forceinline__ uint32_t &tok_at(uint32_t *base, uint32_t i) {
   return base[i];
 #endif
 }
-__device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g, int bcol,
+template <bool BAND>
+__device__ __forceinline__ void emit_tokens(const int (&o)[16], uint32_t zm, int lane, int g, int bcol,
                                             bool valid, bool chroma, bool dc_diffed,
                                             bool first_pred, int pred0,
                                             uint32_t *segtok, uint32_t segoff, uint32_t *tok0, uint32_t *segcnt, uint32_t *hDC,
                                             uint32_t *hAC, int16_t (*st)[16], int kflags = 0) {
-  u4v c0, c1;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {  // one v_perm per pair
-    c0[k] = pack_i16x2(o[2 * k], o[2 * k + 1]);
-    c1[k] = pack_i16x2(o[8 + 2 * k], o[9 + 2 * k]);
-  }
   // staged block-major (block b's 64 coefficients in zigzag order at st +
   // 64 b), its 16-byte chunks XOR-swizzled by b & 7 (coefficient z at
-  // 64 b + (z ^ 8 (b & 7))): the 8 lanes of a ds_write_b128 group store to 8
+  // 64 b + (z ^ 8 (b & 7))): the 8 lanes of a ds_write group store to 8
   // different bank quads instead of one (blocks are 128 B = 32 banks apart:
   // 8-way conflicts), and the AC loop's reads of one z spread over the banks
   const int zsw = 8 * (bcol & 7);
   int16_t *stb = &st[0][0] + 64 * bcol;
-  *(u4v *)(stb + ((16 * g) ^ zsw)) = c0;
-  *(u4v *)(stb + ((16 * g + 8) ^ zsw)) = c1;
   // nonzero mask: min(half, 1) per packed int16 pair puts coefficient 2k's
   // flag at bit 2k and 2k+1's at bit 16+2k
   // (v_pk_min_u16 in asm: the compiler rewrites min(h, 1) into compares and
   // selects, three times the instructions)
-  uint32_t pm = 0;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const uint32_t w = k < 4 ? c0[k] : c1[k - 4];
+  auto pkmin1 = [](uint32_t w) {
     uint32_t h;
     asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(h) : "v"(w));
-    pm |= h << (2 * k);
+    return h;
+  };
+  uint32_t Mlo, Mhi;  // the block's 64-bit nonzero mask (zigzag bit z)
+  if constexpr (BAND) {
+    // lane group g holds zigzag 16m + 4g .. +3 of band m (o[4m .. 4m+3]);
+    // the bands the wave found all zero (zm) are neither staged nor masked
+    uint32_t pm = 0;
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      if (zm >> m & 1u) continue;
+      const uint32_t w0 = pack_i16x2(o[4 * m], o[4 * m + 1]), w1 = pack_i16x2(o[4 * m + 2], o[4 * m + 3]);
+      uint2 piece;
+      piece.x = w0;
+      piece.y = w1;
+      *(uint2 *)(stb + ((16 * m + 4 * g) ^ zsw)) = piece;
+      pm |= pkmin1(w0) << (4 * m) | pkmin1(w1) << (4 * m + 2);
+    }
+    uint32_t m16 = (pm & 0x5555u) | ((pm >> 15) & 0xAAAAu);
+    if (g == 0) m16 &= ~1u;  // the DC is not part of the AC run structure
+    // bands 0|1 form the low word (zigzag 4g + r and 16 + 4g + r), 2|3 the high
+    const uint32_t lo_c = ((m16 & 0xFu) | ((m16 & 0xF0u) << 12)) << (4 * g);
+    const uint32_t hi_c = (((m16 >> 8) & 0xFu) | ((m16 & 0xF000u) << 4)) << (4 * g);
+    if ((zm & 0xCu) == 0xCu) {  // bands 2 and 3 all zero: OR the low words of the 4 groups
+      const auto r16 = __builtin_amdgcn_permlane16_swap(lo_c, lo_c, false, false);
+      const uint32_t h = r16[0] | r16[1];
+      const auto r32 = __builtin_amdgcn_permlane32_swap(h, h, false, false);
+      Mlo = r32[0] | r32[1];
+      Mhi = 0;
+    } else {
+      // rows 0-1 gather the low words of groups g and g + 2, rows 2-3 the
+      // high words; one row swap completes each, one half swap spreads both
+      const auto x = __builtin_amdgcn_permlane32_swap(lo_c, hi_c, false, false);
+      uint32_t h = x[0] | x[1];
+      const auto r16 = __builtin_amdgcn_permlane16_swap(h, h, false, false);
+      h = r16[0] | r16[1];
+      const auto r32 = __builtin_amdgcn_permlane32_swap(h, h, false, false);
+      Mlo = r32[0];
+      Mhi = r32[1];
+    }
+  } else {
+    u4v c0, c1;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {  // one v_perm per pair
+      c0[k] = pack_i16x2(o[2 * k], o[2 * k + 1]);
+      c1[k] = pack_i16x2(o[8 + 2 * k], o[9 + 2 * k]);
+    }
+    *(u4v *)(stb + ((16 * g) ^ zsw)) = c0;
+    *(u4v *)(stb + ((16 * g + 8) ^ zsw)) = c1;
+    uint32_t pm = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) pm |= pkmin1(k < 4 ? c0[k] : c1[k - 4]) << (2 * k);
+    uint32_t m16 = (pm & 0x5555u) | ((pm >> 15) & 0xAAAAu);
+    if (g == 0) m16 &= ~1u;  // the DC is not part of the AC run structure
+    // the block's 64-bit mask: rows 0|1 form the low word, rows 2|3 the high
+    uint32_t h = m16 << (16 * (g & 1));
+    const auto r16 = __builtin_amdgcn_permlane16_swap(h, h, false, false);
+    h = r16[0] | r16[1];
+    const auto r32 = __builtin_amdgcn_permlane32_swap(h, h, false, false);
+    Mlo = r32[0];
+    Mhi = r32[1];
   }
-  uint32_t m16 = (pm & 0x5555u) | ((pm >> 15) & 0xAAAAu);
-  if (g == 0) m16 &= ~1u;  // the DC is not part of the AC run structure
-  // the block's 64-bit mask: rows 0|1 form the low word, rows 2|3 the high
-  uint32_t h = m16 << (16 * (g & 1));
-  const auto r16 = __builtin_amdgcn_permlane16_swap(h, h, false, false);
-  h = r16[0] | r16[1];
-  const auto r32 = __builtin_amdgcn_permlane32_swap(h, h, false, false);
-  const uint32_t Mlo = r32[0], Mhi = r32[1];
   const int eob = !(Mhi >> 31);
   const int n = valid ? 1 + __popc(Mlo) + __popc(Mhi) + eob : 0;
   // token offsets of the blocks inside their segment (chroma rows hold two
@@ -849,6 +892,15 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   // audit (tests only): per block the 64 keep/replay decisions of the fast
   // path, exported so they can be compared with tests/tau_check.c's model
   constexpr bool AUDIT = MODE & K1M_AUDIT;
+  // band order (fused token variants from pixels): M-tile m of the DCT is
+  // zigzag 16m..16m+15, so lane group g holds zigzag 16m + 4g .. +3 of every
+  // band m; a band whose |N| stay below its limit in every lane of the wave
+  // is all zeros, and its quantisation, staging and mask work are skipped
+  // (Tables::mfma_a_band / zlog).  Other variants: lane group g holds zigzag
+  // 16g..16g+15 (their coefficient stores write whole block lines).
+  constexpr bool BAND = PIX && TOK && !(MODE & K1M_COEF_OUT);
+  // zigzag index of coefficient k (0..15) of lane group gg
+  auto zof = [](int gg, int k) { return BAND ? 16 * (k >> 2) + 4 * gg + (k & 3) : 16 * gg + k; };
   const int2 *const fdims = REG ? a.fdims : nullptr;
   __shared__ __attribute__((aligned(16))) uint8_t s_raw[PIX ? NW : 1][TILE_RAW];
   __shared__ __attribute__((aligned(16))) uint8_t s_tile[PIX ? NW : 1][LDS_WAVE];
@@ -896,7 +948,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   if (threadIdx.x < 2) s_inv8q[threadIdx.x] = 1.0f / (float)(8 * T->qint[threadIdx.x][0]);
   if (threadIdx.x < 2 * DCTIE_WORDS) (&s_dctie[0][0])[threadIdx.x] = (&T->dctie[0][0])[threadIdx.x];
   if (PIX) {
-    for (int i = threadIdx.x; i < 12 * 64; i += NT) s_A[i] = T->mfma_a[i];
+    for (int i = threadIdx.x; i < 12 * 64; i += NT) s_A[i] = (BAND ? T->mfma_a_band : T->mfma_a)[i];
     if (LUT_LDS)
       for (int i = threadIdx.x; i < 3 * LUT_WORDS; i += NT) s_lut[i] = (&T->lut[0][0])[i];
   }
@@ -913,6 +965,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   const int g = lane >> 4, bcol = lane & 15;
   const int c4 = lane & 31, pr = lane >> 5;
   const int q_dc[2] = {T->qint[0][0], T->qint[1][0]};
+  const unsigned long long zlog = BAND ? T->zlog : 0ull;  // wave-uniform: SGPRs
   const Geom &G = a.g;
   const int bw = G.w >> 3, mw = G.w >> 4;
   const int ntiles = a.nframes * G.tiles_per_frame;
@@ -1092,7 +1145,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
         return mx < mwf;
       };
       auto block_of = [&](const int nt, int &blk) -> bool { return block_at(nt, bcol, blk); };
-      auto finish = [&](const int nt, int (&o)[16]) {
+      auto finish = [&](const int nt, int (&o)[16], uint32_t zm) {
         const int comp = nt == 2 ? 1 : 0;
         int blk;
         const bool valid = block_of(nt, blk);
@@ -1176,7 +1229,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
             pred0 = blk == cstart ? (a.dc_pred ? (int)a.dc_pred[p.f * 4 + (comp == 0 ? 0 : (bcol >= 8 ? 2 : 1))] : 0)
                                   : (int)a.dc[(long long)p.f * G.nblk + blk - 1];
           }
-          emit_tokens(o, lane, g, bcol, valid, comp == 1, !PIX && a.dc_diffed, first_pred, pred0,
+          emit_tokens<BAND>(o, zm, lane, g, bcol, valid, comp == 1, !PIX && a.dc_diffed, first_pred, pred0,
                       a.tok + (long long)p.f * G.nseg * SEG_TOK, (uint32_t)seg * SEG_TOK, a.tok0 + fs,
                       a.seg_ntok + fs, s_hdc[TOK ? slot : 0][comp][bcol & (HREP - 1)],
                       s_hac[TOK ? slot : 0][comp][bcol & (HREP - 1)],
@@ -1210,13 +1263,35 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
           // and trunc(t + tau) differ iff some coefficient's +-tau interval
           // straddles a truncation boundary (each hi >= its lo)
           int slo = 0, shi = 0;
+          uint32_t zm = 0;  // band order: the N-tile's all-zero bands (wave-uniform)
           if (kflags & K1F_NO_QUANT) {
 #pragma unroll
             for (int k = 0; k < 16; k++) o[k] = acc[k >> 2][k & 3];
           } else
 #pragma unroll
           for (int m = 0; m < 4; m++) {
-            const float4 fac = *(const float4 *)&s_fac[comp][16 * g + 4 * m];
+            if constexpr (BAND) {
+              // |N| < L in every lane: the reference's |F/q| < 1 for all of
+              // the band (Tables::zlim; the DC at g == 0 is not part of it)
+              // (an opaque copy: the limits are re-derived per use on the
+              // scalar unit instead of eight of them held in SGPRs)
+              unsigned long long zl = zlog;
+              asm volatile("" : "+s"(zl));
+              const uint32_t lg = (uint32_t)(zl >> (5 * (4 * comp + m))) & 31u;
+              if (lg) {
+                const uint32_t L = 1u << lg;
+                const uint32_t x = ((uint32_t)((m == 0 && g == 0) ? 0 : acc[m][0]) + L) |
+                                   ((uint32_t)acc[m][1] + L) | ((uint32_t)acc[m][2] + L) |
+                                   ((uint32_t)acc[m][3] + L);
+                if (!__ballot(x >= 2u * L)) {
+                  zm |= 1u << m;
+#pragma unroll
+                  for (int r = 0; r < 4; r++) o[4 * m + r] = 0;
+                  continue;
+                }
+              }
+            }
+            const float4 fac = *(const float4 *)&s_fac[comp][BAND ? 16 * m + 4 * g : 16 * g + 4 * m];
             const f2v lc2 = {lc, lc};
 #pragma unroll
             for (int h = 0; h < 2; h++) {
@@ -1245,7 +1320,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
               for (int r = 0; r < 4; r++) {
                 const int k = 4 * m + r;
                 const float nf = (float)acc[m][r];
-                const float fa = s_fac[comp][16 * g + k];
+                const float fa = s_fac[comp][zof(g, k)];
                 const float tv = fmaf(fa, lc, 1.0e-6f);
                 mm |= (uint32_t)((int)fmaf(nf, fa, -tv) != (int)fmaf(nf, fa, tv)) << k;
               }
@@ -1315,7 +1390,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
                   const int j = r + (lane >> 3), x = lane & 7;
                   const int e = lst[j < nch ? j : 0];
                   const int ol = e >> 4, k = e & 15;
-                  const int z = 16 * (ol >> 4) + k;
+                  const int z = zof(ol >> 4, k);
                   const int rz = s_zz[z], v = rz >> 3, u = rz & 7;
                   const uint8_t *Pb = L + (nt * 16 + (ol & 15)) * LDS_BLK;
                   double in = 0.0;
@@ -1353,7 +1428,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
               while (mm) {
                 const int k = __ffs(mm) - 1;
                 mm &= mm - 1u;
-                const int z = 16 * g + k;
+                const int z = zof(g, k);
                 const int v = ac_exact(Pb, z, s_qint[comp][z], s_cos, s_zz);
 #pragma unroll
                 for (int j = 0; j < 16; j++) o[j] = j == k ? v : o[j];
@@ -1364,14 +1439,14 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
           // store (their VMEM count per tile varies)
           if (nt == MIJ_K1_DMAWAIT_NT && !DEFER && !(kflags & K1F_NO_DMAWAIT)) dma_wait();
           K1_PHASE(3);
-          finish(nt, o);
+          finish(nt, o, zm);
           K1_PHASE(4);
         }
       } else if (!PIX) {
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
           int o[16];
-          finish(nt, o);
+          finish(nt, o, 0u);
         }
       }
       if (PIX) wave_lds_sync();
@@ -3111,6 +3186,281 @@ __global__ __launch_bounds__(LB_THREADS, lb_occ<PW>()) void k_pack_lb(EntArgs a)
 #undef LB_STAMP
 }
 
+// ===========================================================================
+// k_pack_flat: k_pack_lb's job with the group's tokens as one flat stream.
+// A pack group's bitstream is its segments' token strings back to back, and
+// K1 pads every segment to a multiple of 4 tokens (LB_NOTOK, no bits), so the
+// group is a list of 4-token chunks, each inside one segment slot and 16-byte
+// aligned.  Every thread takes one chunk per round (256 chunks, 1024 tokens a
+// round; the segment of a chunk by binary search of the chunk counts' prefix),
+// merges its 4 tokens into one bit string, and a workgroup scan of the string
+// lengths places them in the LDS window relative to the group's first bit --
+// every token is read and decoded once, and no lane idles on a short segment
+// (k_pack_lb gives 16 lanes to a segment: a chroma segment of ~16 tokens kept
+// 12 of them idle, and a luma segment's tokens past the first 64 were read
+// and decoded twice).  The next round's chunk is loaded while a round is
+// placed.  Then the group's aggregate goes out, the decoupled look-back finds
+// its start bit and the window is stored shifted into place, as in k_pack_lb.
+// A group whose bits outgrow the window (near worst-case entropy) takes its
+// start bit and sweeps its chunks again once per window, at absolute offsets.
+// ===========================================================================
+constexpr int PF_THREADS = 256, PF_WAVES = PF_THREADS / 64;
+// (MIJ_PACK_FLAT=0: k_pack_lb instead, for A/B)
+#ifndef MIJ_PACK_FLAT
+#define MIJ_PACK_FLAT 1
+#endif
+#ifndef MIJ_PF_OCC
+#define MIJ_PF_OCC 8
+#endif
+#ifndef MIJ_PF_OCC_WIDE
+#define MIJ_PF_OCC_WIDE 6
+#endif
+template <int PW>
+constexpr int pf_occ() { return PW > PACK_WORDS ? MIJ_PF_OCC_WIDE : MIJ_PF_OCC; }
+static_assert(PACK_SEGS == 64, "k_pack_flat: one wave scans the group's segments");
+template <int PW, bool FF>
+__global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs a) {
+  __shared__ uint32_t buf[PW];
+  __shared__ uint32_t tab[2 * 256];
+  __shared__ uint32_t s_cp[PACK_SEGS + 1];  // exclusive prefix of the segments' chunks; [64]: all
+  __shared__ uint32_t s_ws[2][PF_WAVES];     // a round's bits per wave (two rounds in turn)
+  __shared__ unsigned long long s_prefix;
+  __shared__ int s_ticket;
+  __shared__ uint32_t s_over;
+  constexpr int FFN = PW / EMIT_CW + 2;
+  __shared__ uint32_t s_ff[FFN];
+  __shared__ uint32_t s_ffnb;
+  const Geom &G = a.g;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (FF && tid < FFN) s_ff[tid] = 0;
+  if (tid == 0) s_over = 0;
+  const int gy = (G.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (G.nsc + PACK_SEGS - 1) / PACK_SEGS;
+  const int gpf = gy + 2 * gc;
+  // the scan from the workgroup's index, the group inside it from the scan's
+  // ticket (groups claimed in scan order, as k_pack_lb)
+  const int f = blockIdx.x / gpf, bq = blockIdx.x - f * gpf;
+  const int comp = bq < gy ? 0 : (bq < gy + gc ? 1 : 2);
+  const int sbase = comp == 0 ? 0 : (comp == 1 ? G.nsy : G.nsy + G.nsc), ns = comp == 0 ? G.nsy : G.nsc;
+  const int gscan0 = f * gpf + (comp == 0 ? 0 : gy + (comp == 2 ? gc : 0));
+  const int nq = comp == 0 ? gy : gc;
+  if (tid == 0) s_ticket = (int)atomicAdd(&a.pack_ticket[f * 3 + comp], 1u);
+  const int chroma = comp != 0;
+  for (int i = tid; i < 512; i += PF_THREADS)
+    tab[i] = lb_tab_entry(a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + i], (uint32_t)i & 255u);
+  for (int i = tid; i < PW; i += PF_THREADS) buf[i] = 0;
+  uint32_t Lz, zcode;
+  {  // the ZRL code (AC symbol 0xF0: cls 0, so the entry is code / length)
+    const uint32_t zac = a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + 256 + 0xF0];
+    Lz = zac >> 16;
+    zcode = zac & 0xFFFFu;
+  }
+  __syncthreads();
+  const int q = s_ticket;
+  const int gid = gscan0 + q;
+  const int s0 = q * PACK_SEGS, nsg = min(ns, s0 + PACK_SEGS) - s0;
+  const long long fs0 = (long long)f * G.nseg + sbase + s0;  // the group's first segment
+  if (wave == 0) {  // chunks per segment (K1 padded each to a multiple of 4 tokens)
+    const uint32_t nt = lane < nsg ? min(a.seg_ntok[fs0 + lane], (uint32_t)SEG_TOK) : 0u;
+    const uint32_t ch = (nt + 3u) >> 2;
+    const uint32_t incl = wave_scan64(ch);
+    s_cp[lane] = lane < nsg ? incl - ch : 0xFFFFFFFFu;  // (no chunk maps past the group)
+    if (lane == 63) s_cp[PACK_SEGS] = incl;
+  }
+  __syncthreads();
+  const uint32_t C = s_cp[PACK_SEGS];
+  const uint32_t *tokg = a.tok + fs0 * SEG_TOK;
+  // chunk c's 4 tokens (c < C): its segment s is the last with s_cp[s] <= c
+  auto chunk_load = [&](uint32_t c, u4v &t) {
+    t = u4v{0u, 0u, 0u, 0u};
+    if (c >= C) return;
+    int s = 0;
+#pragma unroll
+    for (int step = 32; step; step >>= 1)
+      if (s_cp[s + step] <= c) s += step;
+    const uint32_t o = 4u * (c - s_cp[s]);
+    t = *(const u4v *)(tokg + (long long)s * SEG_TOK + o);
+    if (o == 0) t[0] = a.tok0[fs0 + s];  // token 0 of a segment (dense array)
+  };
+  // a chunk's bits: per token the code (magnitude bits included) and its
+  // ZRLs (encoder.c:490-494); merged into one left-growing string when they
+  // fit 64 bits
+  auto decode = [&](const u4v &t, uint32_t (&L)[4], uint32_t (&code)[4], uint32_t (&nzr)[4]) -> uint32_t {
+    uint32_t nb = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      L[e] = lb_tok_code(tab, t[e], code[e]);
+      nzr[e] = (t[e] >> 8) & 3u;
+      nb += L[e] + nzr[e] * Lz;
+    }
+    return nb;
+  };
+  // one sweep over the group's chunks: positions relative to the group's
+  // first bit (+ boff); whole: every bit into the window (a chunk past it
+  // sets the overflow flag), else only the bits inside [lo_bit, hi_bit)
+  auto sweep = [&](bool whole, uint32_t boff, uint32_t lo_bit, uint32_t hi_bit) -> uint32_t {
+    const uint32_t lim = (PW - 1) * 32;  // one spare word for the shifted store
+    uint32_t run = boff;
+    bool over = false;
+    u4v tn;
+    chunk_load((uint32_t)tid, tn);
+    for (uint32_t c0 = 0, r = 0; c0 < C; c0 += PF_THREADS, r++) {
+      const u4v t = tn;
+      const bool have = c0 + tid < C;
+      if (c0 + PF_THREADS < C) chunk_load(c0 + PF_THREADS + tid, tn);  // next round in flight
+      uint32_t L[4], code[4], nzr[4];
+      uint32_t nb = decode(t, L, code, nzr);
+      if (!have) nb = 0;
+      const uint32_t x = wave_scan64(nb);
+      if (lane == 63) s_ws[r & 1][wave] = x;
+      __syncthreads();
+      uint32_t before = 0, tot = 0;
+#pragma unroll
+      for (int w = 0; w < PF_WAVES; w++) {
+        const uint32_t v = s_ws[r & 1][w];
+        tot += v;
+        before += w < wave ? v : 0u;
+      }
+      const uint32_t pos = run + before + x - nb;
+      run += tot;
+      if (!nb) continue;
+      if (whole && pos + nb > lim) {
+        over = true;
+      } else if (nb <= 64) {
+        unsigned long long acc = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          for (uint32_t z = nzr[e]; z; z--) acc = (acc << Lz) | zcode;
+          acc = (acc << L[e]) | code[e];
+        }
+        if (whole) put_bits64(buf, pos, acc << (64 - nb), nb);
+        else put_bits64_win(buf, pos, acc << (64 - nb), nb, lo_bit, hi_bit);
+      } else {  // more than 64 bits: token by token
+        uint32_t p = pos;
+        for (int e = 0; e < 4; e++) {
+          for (uint32_t z = nzr[e]; z; z--) {
+            if (whole) put_bits(buf, p, zcode, (int)Lz);
+            else if (p < hi_bit && p + Lz > lo_bit) put_bits_window(buf, p, lo_bit, hi_bit, zcode, (int)Lz);
+            p += Lz;
+          }
+          if (L[e]) {
+            if (whole) put_bits(buf, p, code[e], (int)L[e]);
+            else if (p < hi_bit && p + L[e] > lo_bit) put_bits_window(buf, p, lo_bit, hi_bit, code[e], (int)L[e]);
+          }
+          p += L[e];
+        }
+      }
+    }
+    if (whole && __ballot(over) && lane == 0) s_over = 1;
+    return run - boff;
+  };
+  const uint32_t gbits = sweep(true, 0u, 0u, 0u);
+  // the group's aggregate out, then its start bit by decoupled look-back
+  // over the groups before it (wave 0; publishes the inclusive prefix)
+  if (tid == 0 && q > 0)
+    __hip_atomic_store(&a.pack_state[gid], LB_AGG | gbits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (wave == 0) {
+    const unsigned long long base = a.bit_base ? a.bit_base[f * 4 + comp] : 0u;
+    unsigned long long *stt = a.pack_state;
+    unsigned long long prefix = base;
+    if (q > 0) {
+      prefix = 0;
+      long long j = gid - 1;
+      while (true) {
+        const long long jj = j - lane;
+        unsigned long long sv = jj >= gscan0 ? __hip_atomic_load(&stt[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                             : (LB_INC | base);
+        const unsigned long long m2 = __ballot((sv >> 62) == 2), m0 = __ballot((sv >> 62) == 0);
+        const unsigned long long upto = m2 ? (m2 & (~m2 + 1)) : 0ull;  // lowest inclusive lane
+        if (m0 & (upto ? upto - 1 : ~0ull)) {  // a group before it has not published yet
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        const int kk = upto ? __ffsll((long long)m2) - 1 : 63;
+        unsigned long long add = lane <= kk ? (sv & LB_VAL) : 0ull;
+        for (int off = 32; off; off >>= 1) add += __shfl_xor(add, off);
+        prefix += add;
+        if (upto) break;
+        j -= 64;
+      }
+    }
+    if (lane == 0) {
+      __hip_atomic_store(&stt[gid], LB_INC | (prefix + gbits), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (q == nq - 1) a.scan_bits[f * 3 + comp] = prefix + gbits;
+      s_prefix = prefix;
+      if (FF) s_ffnb = q == nq - 1 ? (uint32_t)((prefix + gbits) >> 3) : ~0u;
+    }
+  }
+  __syncthreads();
+  uint32_t *raw_scan = a.raw + (long long)f * G.raw_fs +
+                       (comp == 0 ? 0 : G.raw_words[0] + (comp == 2 ? G.raw_words[1] : 0));
+  const unsigned long long prefix = s_prefix;
+  // the group's words in the scan: [first, first + n)
+  uint32_t n = (uint32_t)(((prefix & 31) + gbits + 31) >> 5);
+  if ((prefix >> 5) + n + 1 > (unsigned long long)G.raw_words[comp]) {  // cannot happen for valid tokens;
+    if (tid == 0) a.err[f] = 2;                                          // never write out of bounds
+    n = 0;
+  }
+  const unsigned long long gw = prefix >> 5;
+  uint32_t *raw = raw_scan + gw;
+  auto ff_add = [&](uint32_t v, uint32_t W, uint32_t c0) {
+    const int c = ff_word(v, W, s_ffnb);
+    if (c) atomicAdd(&s_ff[W / EMIT_CW - c0], (uint32_t)c);
+  };
+  auto ff_flush = [&](uint32_t w_first) {
+    __syncthreads();
+    if (FF && tid < FFN && s_ff[tid]) {  // the window's chunk counts out, zeroed for the next
+      atomicAdd(&a.ffc[(long long)(f * 3 + comp) * emit_chunks(G) + w_first / EMIT_CW + tid], s_ff[tid]);
+      s_ff[tid] = 0;
+    }
+  };
+  if (!s_over) {
+    // the window shifted into place: the edge words may be shared with the
+    // neighbouring groups -- OR (onto zero), or in seam mode (EntArgs::seam)
+    // the first word to the side
+    const uint32_t sh = (uint32_t)(prefix & 31);
+    const uint32_t c0 = (uint32_t)gw / EMIT_CW;
+    for (uint32_t i = tid; i < n; i += PF_THREADS) {
+      const uint32_t v = __builtin_amdgcn_alignbit(i ? buf[i - 1] : 0u, buf[i], sh);
+      if (FF || a.seam) {
+        if (i == 0 && sh) {
+          a.seam[gid] = v;
+        } else {
+          raw[i] = v;
+          if (FF) ff_add(v, (uint32_t)gw + i, c0);
+        }
+      } else if (i == 0 || i == n - 1) atomicOr(&raw[i], v);
+      else raw[i] = v;
+    }
+    ff_flush((uint32_t)gw);
+    return;
+  }
+  // wider than the window: window by window at offsets from the group's
+  // first word (boff = its first bit inside that word)
+  const uint32_t boff = (uint32_t)(prefix & 31);
+  for (uint32_t w0 = 0; w0 < n; w0 += PW) {
+    const uint32_t wn = min((uint32_t)PW, n - w0);
+    __syncthreads();
+    for (uint32_t i = tid; i < wn; i += PF_THREADS) buf[i] = 0;
+    __syncthreads();
+    sweep(false, boff, w0 * 32, (w0 + wn) * 32);
+    __syncthreads();
+    const uint32_t c0 = ((uint32_t)gw + w0) / EMIT_CW;
+    for (uint32_t i = tid; i < wn; i += PF_THREADS) {
+      const uint32_t wi = w0 + i;
+      if (FF || a.seam) {
+        if (wi == 0 && boff) {
+          a.seam[gid] = buf[i];
+        } else {
+          raw[wi] = buf[i];
+          if (FF) ff_add(buf[i], (uint32_t)gw + wi, c0);
+        }
+      } else if (wi == 0 || wi == n - 1) atomicOr(&raw[wi], buf[i]);
+      else raw[wi] = buf[i];
+    }
+    ff_flush((uint32_t)gw + w0);
+  }
+}
+
 // k_seam_fix (seam mode, EntArgs::seam): k_pack_lb stored every scan word
 // whole, each by the one group that reaches its end, and left a group's first
 // word, when the group before it ends inside that word, in seam[]; this ORs
@@ -4136,6 +4486,13 @@ hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s, bool state_zeroed) {
     if (e != hipSuccess) return e;
   }
   const bool ff = a.ff_pack && a.seam;
+#if MIJ_PACK_FLAT
+  if (a.pack_wide && ff) hipLaunchKernelGGL((k_pack_flat<MIJ_PACK_WIDE_WORDS, true>), dim3((unsigned)groups), dim3(PF_THREADS), 0, s, a);
+  else if (a.pack_wide) hipLaunchKernelGGL((k_pack_flat<MIJ_PACK_WIDE_WORDS, false>), dim3((unsigned)groups), dim3(PF_THREADS), 0, s, a);
+  else if (ff) hipLaunchKernelGGL((k_pack_flat<PACK_WORDS, true>), dim3((unsigned)groups), dim3(PF_THREADS), 0, s, a);
+  else hipLaunchKernelGGL((k_pack_flat<PACK_WORDS, false>), dim3((unsigned)groups), dim3(PF_THREADS), 0, s, a);
+  return hipGetLastError();
+#endif
   if (a.pack_wide && ff) hipLaunchKernelGGL((k_pack_lb<MIJ_PACK_WIDE_WORDS, true>), dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
   else if (a.pack_wide) hipLaunchKernelGGL((k_pack_lb<MIJ_PACK_WIDE_WORDS, false>), dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
   else if (ff) hipLaunchKernelGGL((k_pack_lb<PACK_WORDS, true>), dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
