@@ -284,7 +284,7 @@ def run_regions(args, world, rank, local, dist):
     verified = 0
     if args.verify:
         import oracle as O
-        for i in range(min(len(regions), 4 * args.verify)):
+        for i in range(len(regions) if args.verify < 0 else min(len(regions), 4 * args.verify)):
             if batch.output(i) != O.cref_encode(frame, args.quality, regions[i]):
                 raise SystemExit(f"bench regions: region {i} differs from the oracle")
             verified += 1
@@ -398,7 +398,7 @@ def run_detect(args, world, rank, local, dist):
     verified = 0
     if args.verify and want[0]:
         n, areas = want
-        for i in range(min(n, 4 * args.verify)):
+        for i in range(n if args.verify < 0 else min(n, 4 * args.verify)):
             if batch.output(i) != O.cref_encode(frames[last], args.quality, areas[i]):
                 raise SystemExit(f"bench detect: area {i} differs from the oracle")
             verified += 1
@@ -490,7 +490,7 @@ def run_decode(args, world, rank, local, dist):
         dist.barrier()
     el, px_all = sharding.reduce_timing(el, W * H * F * args.steps, dist, dist_device(dist, local))
     verified = 0
-    for i in range(min(F, args.verify)):
+    for i in range(F if args.verify < 0 else min(F, args.verify)):
         for g, w in zip(dec.coefs(i), enc.coefs(i, diffed=True)):
             if not (g == w).all():
                 raise SystemExit(f"bench decode: frame {i} coefficients differ from the encoder's")

@@ -232,15 +232,11 @@ static void fill_tables(int quality, Tables *t) {
   }
   // A fragments of v_mfma_i32_16x16x64_i8: lane l holds row (l & 15) and the
   // 16 k-values 16*(l>>4) .. +15.  Row r of M-tile m is zigzag coefficient
-  // z = 16*(r>>2) + 4m + (r&3) (lane group g of the output then holds zigzag
-  // 16g .. 16g+15), or z = 16m + r in band order (mfma_a_band: an M-tile is
-  // one frequency band, whose zeros a wave can skip); k = pixel index y*8+x
-  // of the block.
-  for (int band = 0; band < 2; band++)
+  // z = 16*(r>>2) + 4m + (r&3); k = pixel index y*8+x of the block.
   for (int m = 0; m < 4; m++)
     for (int lane = 0; lane < 64; lane++) {
       const int row = lane & 15, kg = lane >> 4;
-      const int z = band ? 16 * m + row : 16 * (row >> 2) + 4 * m + (row & 3);
+      const int z = 16 * (row >> 2) + 4 * m + (row & 3);
       const int rz = k_zz[z], v = rz >> 3, u = rz & 7;
       int8_t dig[3][16];
       for (int j = 0; j < 16; j++) {
@@ -264,23 +260,21 @@ static void fill_tables(int quality, Tables *t) {
         dig[1][j] = (int8_t)d1;
         dig[2][j] = (int8_t)d0;
       }
-      for (int d = 0; d < 3; d++)
-        memcpy(&(band ? t->mfma_a_band : t->mfma_a)[(m * 3 + d) * 64 + lane], dig[d], 16);
+      for (int d = 0; d < 3; d++) memcpy(&t->mfma_a[(m * 3 + d) * 64 + lane], dig[d], 16);
     }
-  // zero-band limits (K1 band order): the reference's |F/q| < 1
-  // wherever |N| + 4096 (the integer DCT's error bound, L1/2) stays below
-  // 2^21 q (1 - 1e-6); tested only where the band's zeros are common enough
-  // to pay for the test (luma bands from q >= 30, chroma from q >= 9)
-  for (int c = 0; c < 2; c++)
-    for (int m = 0; m < 4; m++) {
-      int qmin = 256;
-      for (int z = m ? 16 * m : 1; z < 16 * m + 16; z++) qmin = q[c][k_zz[z]] < qmin ? q[c][k_zz[z]] : qmin;
-      const double lim = 2097152.0 * qmin * (1.0 - 2e-6) - 6000.0;
-      long long L = 1;
-      while (2 * L <= (long long)lim) L *= 2;
-      t->zlim[c][m] = qmin >= (c ? 9 : 30) ? (int)L : 0;
-      if (t->zlim[c][m]) t->zlog |= (unsigned long long)__builtin_ctzll(L) << (5 * (4 * c + m));
+  // K1's chroma all-AC-zero test (Tables::czl): the reference's |F/q| < 1
+  // wherever |N| + 4096 (the integer DCT's error bound, L1 / 2 <= 4096)
+  // stays below 2^21 q (1 - 1e-6); the test runs where all-zero chroma
+  // N-tiles are common (smallest chroma AC quantiser >= 9: Q <= 75)
+  {
+    int qmin = 256;
+    for (int z = 0; z < 64; z++) {
+      const int qz = q[1][k_zz[z]];
+      t->czl[z] = z ? (int)(2097152.0 * qz * (1.0 - 2e-6) - 6000.0) : (1 << 30);
+      if (z) qmin = qz < qmin ? qz : qmin;
     }
+    t->cz_on = qmin >= 9;
+  }
 }
 
 // ---------------------------------------------------------------------------

@@ -136,21 +136,18 @@ __host__ __device__ inline FGeom frame_geom(const Geom &G, const int2 *fd, int f
 // Device-resident constant tables for one quality setting.
 struct Tables {
   int4 mfma_a[12 * 64];   // A fragments: 4 M-tiles x 3 digits x 64 lanes
-  // the same in band order (M-tile m = zigzag 16m..16m+15): the fused token
-  // K1 (lane group g then holds zigzag 16m + 4g .. +3 of every M-tile m)
-  int4 mfma_a_band[12 * 64];
-  // band order: an M-tile whose |N| < zlim[c][m] in every lane is all zeros
-  // (a power of two below 2^21 q (1 - 2e-6) - 6000 for the band's smallest q;
-  // 0: the band is not tested -- its zeros are too rare to pay for the test)
-  // packed for K1's SGPRs: bits 5 (4c + m) .. +4 hold log2 zlim[c][m] (0: untested)
-  unsigned long long zlog;
-  int zlim[2][4];
   float qfac[2][64];      // zigzag order: 1 / (2^21 * q)
   int qint[2][64];        // zigzag order: integer quantizer
   int dqt[2][64];         // zigzag order: DQT bytes
   double cosd[64];        // encoder.c:8-16 constants
   uint32_t lut[3][1024];  // colour-exception bitmaps (Y by R,G/2; Cb by G,B/2; Cr by G,R/2)
   uint32_t dctie[2][DCTIE_WORDS];  // bit K: the reference's DC at |S| = 8qK is K - 1
+  // K1's chroma all-AC-zero test: per zigzag z the limit L_z = 2^21 q_z
+  // (1 - 2e-6) - 6000 under which |N| means the reference's |F/q| < 1 (z = 0,
+  // the DC, never fails: 2^30); cz_on = 0 where all-zero chroma N-tiles are
+  // too rare to pay for the test (Q > 75)
+  int czl[64];
+  int cz_on;
 };
 
 struct K1Args {

@@ -598,10 +598,8 @@ constexpr uint32_t LB_NOTOK = TOK_AC | 0xFFu;
 #endif
 
 // One N-tile of coefficients -> compacted token stream of its segment(s).
-// o[k] = zigzag coefficient 16g+k of block bcol, or with BAND zigzag
-// 16(k>>2) + 4g + (k&3) (the DC raw in o[0] of g == 0 either way, or the DC
-// difference when dc_diffed); zm: the bands (BAND) the wave found all zero.
-// Every lane of the wave calls this.
+// o[k] = zigzag coefficient 16g+k of block bcol (DC raw in o[0] of g == 0,
+// or the DC difference when dc_diffed).  Every lane of the wave calls this.
 // Tokens of a block, in bitstream order (encoder.c:462-502): its DC
 // difference (:434-446), the AC run/size symbols (:448-460, ZRLs folded in,
 // :490-494), then EOB unless coefficient 63 is nonzero (:479-484).  The DC of
@@ -622,86 +620,52 @@ __device__ __forceinline__ uint32_t &tok_at(uint32_t *base, uint32_t i) {
   return base[i];
 #endif
 }
-template <bool BAND>
-__device__ __forceinline__ void emit_tokens(const int (&o)[16], uint32_t zm, int lane, int g, int bcol,
+__device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g, int bcol,
                                             bool valid, bool chroma, bool dc_diffed,
                                             bool first_pred, int pred0,
                                             uint32_t *segtok, uint32_t segoff, uint32_t *tok0, uint32_t *segcnt, uint32_t *hDC,
-                                            uint32_t *hAC, int16_t (*st)[16], int kflags = 0) {
+                                            uint32_t *hAC, int16_t (*st)[16], int kflags = 0, bool acz = false) {
+  // acz (a compile-time constant where it is set): every AC coefficient of
+  // the N-tile is zero -- no staging, no masks, no AC tokens; each block is
+  // its DC token and EOB
+  uint32_t Mlo = 0, Mhi = 0;
+  const int zsw = 8 * (bcol & 7);
+  if (!acz) {
+  u4v c0, c1;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {  // one v_perm per pair
+    c0[k] = pack_i16x2(o[2 * k], o[2 * k + 1]);
+    c1[k] = pack_i16x2(o[8 + 2 * k], o[9 + 2 * k]);
+  }
   // staged block-major (block b's 64 coefficients in zigzag order at st +
   // 64 b), its 16-byte chunks XOR-swizzled by b & 7 (coefficient z at
-  // 64 b + (z ^ 8 (b & 7))): the 8 lanes of a ds_write group store to 8
+  // 64 b + (z ^ 8 (b & 7))): the 8 lanes of a ds_write_b128 group store to 8
   // different bank quads instead of one (blocks are 128 B = 32 banks apart:
   // 8-way conflicts), and the AC loop's reads of one z spread over the banks
-  const int zsw = 8 * (bcol & 7);
   int16_t *stb = &st[0][0] + 64 * bcol;
+  *(u4v *)(stb + ((16 * g) ^ zsw)) = c0;
+  *(u4v *)(stb + ((16 * g + 8) ^ zsw)) = c1;
   // nonzero mask: min(half, 1) per packed int16 pair puts coefficient 2k's
   // flag at bit 2k and 2k+1's at bit 16+2k
   // (v_pk_min_u16 in asm: the compiler rewrites min(h, 1) into compares and
   // selects, three times the instructions)
-  auto pkmin1 = [](uint32_t w) {
+  uint32_t pm = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint32_t w = k < 4 ? c0[k] : c1[k - 4];
     uint32_t h;
     asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(h) : "v"(w));
-    return h;
-  };
-  uint32_t Mlo, Mhi;  // the block's 64-bit nonzero mask (zigzag bit z)
-  if constexpr (BAND) {
-    // lane group g holds zigzag 16m + 4g .. +3 of band m (o[4m .. 4m+3]);
-    // the bands the wave found all zero (zm) are neither staged nor masked
-    uint32_t pm = 0;
-#pragma unroll
-    for (int m = 0; m < 4; m++) {
-      if (zm >> m & 1u) continue;
-      const uint32_t w0 = pack_i16x2(o[4 * m], o[4 * m + 1]), w1 = pack_i16x2(o[4 * m + 2], o[4 * m + 3]);
-      uint2 piece;
-      piece.x = w0;
-      piece.y = w1;
-      *(uint2 *)(stb + ((16 * m + 4 * g) ^ zsw)) = piece;
-      pm |= pkmin1(w0) << (4 * m) | pkmin1(w1) << (4 * m + 2);
-    }
-    uint32_t m16 = (pm & 0x5555u) | ((pm >> 15) & 0xAAAAu);
-    if (g == 0) m16 &= ~1u;  // the DC is not part of the AC run structure
-    // bands 0|1 form the low word (zigzag 4g + r and 16 + 4g + r), 2|3 the high
-    const uint32_t lo_c = ((m16 & 0xFu) | ((m16 & 0xF0u) << 12)) << (4 * g);
-    const uint32_t hi_c = (((m16 >> 8) & 0xFu) | ((m16 & 0xF000u) << 4)) << (4 * g);
-    if ((zm & 0xCu) == 0xCu) {  // bands 2 and 3 all zero: OR the low words of the 4 groups
-      const auto r16 = __builtin_amdgcn_permlane16_swap(lo_c, lo_c, false, false);
-      const uint32_t h = r16[0] | r16[1];
-      const auto r32 = __builtin_amdgcn_permlane32_swap(h, h, false, false);
-      Mlo = r32[0] | r32[1];
-      Mhi = 0;
-    } else {
-      // rows 0-1 gather the low words of groups g and g + 2, rows 2-3 the
-      // high words; one row swap completes each, one half swap spreads both
-      const auto x = __builtin_amdgcn_permlane32_swap(lo_c, hi_c, false, false);
-      uint32_t h = x[0] | x[1];
-      const auto r16 = __builtin_amdgcn_permlane16_swap(h, h, false, false);
-      h = r16[0] | r16[1];
-      const auto r32 = __builtin_amdgcn_permlane32_swap(h, h, false, false);
-      Mlo = r32[0];
-      Mhi = r32[1];
-    }
-  } else {
-    u4v c0, c1;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {  // one v_perm per pair
-      c0[k] = pack_i16x2(o[2 * k], o[2 * k + 1]);
-      c1[k] = pack_i16x2(o[8 + 2 * k], o[9 + 2 * k]);
-    }
-    *(u4v *)(stb + ((16 * g) ^ zsw)) = c0;
-    *(u4v *)(stb + ((16 * g + 8) ^ zsw)) = c1;
-    uint32_t pm = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) pm |= pkmin1(k < 4 ? c0[k] : c1[k - 4]) << (2 * k);
-    uint32_t m16 = (pm & 0x5555u) | ((pm >> 15) & 0xAAAAu);
-    if (g == 0) m16 &= ~1u;  // the DC is not part of the AC run structure
-    // the block's 64-bit mask: rows 0|1 form the low word, rows 2|3 the high
-    uint32_t h = m16 << (16 * (g & 1));
-    const auto r16 = __builtin_amdgcn_permlane16_swap(h, h, false, false);
-    h = r16[0] | r16[1];
-    const auto r32 = __builtin_amdgcn_permlane32_swap(h, h, false, false);
-    Mlo = r32[0];
-    Mhi = r32[1];
+    pm |= h << (2 * k);
+  }
+  uint32_t m16 = (pm & 0x5555u) | ((pm >> 15) & 0xAAAAu);
+  if (g == 0) m16 &= ~1u;  // the DC is not part of the AC run structure
+  // the block's 64-bit mask: rows 0|1 form the low word, rows 2|3 the high
+  uint32_t h = m16 << (16 * (g & 1));
+  const auto r16 = __builtin_amdgcn_permlane16_swap(h, h, false, false);
+  h = r16[0] | r16[1];
+  const auto r32 = __builtin_amdgcn_permlane32_swap(h, h, false, false);
+  Mlo = r32[0];
+  Mhi = r32[1];
   }
   const int eob = !(Mhi >> 31);
   const int n = valid ? 1 + __popc(Mlo) + __popc(Mhi) + eob : 0;
@@ -757,7 +721,7 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], uint32_t zm, int
   // base + 1 + the block's set bits below z, its run the distance to the
   // highest of them (the DC at z = 0 when there is none).  Token word:
   // (run << 4 | cls) is sym | ZRLs << 8 (run <= 62).
-  if (valid && !(kflags & K1F_NO_ACLOOP)) {
+  if (!acz && valid && !(kflags & K1F_NO_ACLOOP)) {
     const int16_t *sl = &st[0][0] + 64 * bcol;
     auto token = [&](int z, int rank, int zp) {
       const int cz = sl[z ^ zsw];
@@ -873,6 +837,10 @@ constexpr int k1_waves() {
   return k1_base(MODE) == K1M_TOK_OUT ? MIJ_K1_TOK_WAVES : (k1_wide<MODE>() ? 12 : 4);
 }
 
+// chroma all-AC-zero fast path of the token K1 (A/B knob)
+#ifndef MIJ_K1_CZ
+#define MIJ_K1_CZ 1
+#endif
 #ifndef MIJ_K1_COOP_REPLAY
 #define MIJ_K1_COOP_REPLAY 1
 #endif
@@ -892,15 +860,6 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   // audit (tests only): per block the 64 keep/replay decisions of the fast
   // path, exported so they can be compared with tests/tau_check.c's model
   constexpr bool AUDIT = MODE & K1M_AUDIT;
-  // band order (fused token variants from pixels): M-tile m of the DCT is
-  // zigzag 16m..16m+15, so lane group g holds zigzag 16m + 4g .. +3 of every
-  // band m; a band whose |N| stay below its limit in every lane of the wave
-  // is all zeros, and its quantisation, staging and mask work are skipped
-  // (Tables::mfma_a_band / zlog).  Other variants: lane group g holds zigzag
-  // 16g..16g+15 (their coefficient stores write whole block lines).
-  constexpr bool BAND = PIX && TOK && !(MODE & K1M_COEF_OUT);
-  // zigzag index of coefficient k (0..15) of lane group gg
-  auto zof = [](int gg, int k) { return BAND ? 16 * (k >> 2) + 4 * gg + (k & 3) : 16 * gg + k; };
   const int2 *const fdims = REG ? a.fdims : nullptr;
   __shared__ __attribute__((aligned(16))) uint8_t s_raw[PIX ? NW : 1][TILE_RAW];
   __shared__ __attribute__((aligned(16))) uint8_t s_tile[PIX ? NW : 1][LDS_WAVE];
@@ -916,6 +875,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   __shared__ double s_cos[64];
   __shared__ uint8_t s_zz[64];
   __shared__ int s_qint[2][64];
+  __shared__ __attribute__((aligned(16))) int s_czl[PIX ? 64 : 1];  // chroma all-AC-zero limits
   __shared__ __attribute__((aligned(16))) int16_t s_st[TOK ? NW : 1][64][16];  // token staging
   // per-frame histograms of this workgroup: [frame slot][luma, chroma][copy][symbol];
   // the tokenize pass keeps HREP copies (by block) to spread same-symbol atomics
@@ -946,9 +906,10 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   }
   if (threadIdx.x < 128) s_qint[threadIdx.x >> 6][threadIdx.x & 63] = T->qint[threadIdx.x >> 6][threadIdx.x & 63];
   if (threadIdx.x < 2) s_inv8q[threadIdx.x] = 1.0f / (float)(8 * T->qint[threadIdx.x][0]);
+  if (PIX && threadIdx.x < 64) s_czl[threadIdx.x] = T->czl[threadIdx.x];
   if (threadIdx.x < 2 * DCTIE_WORDS) (&s_dctie[0][0])[threadIdx.x] = (&T->dctie[0][0])[threadIdx.x];
   if (PIX) {
-    for (int i = threadIdx.x; i < 12 * 64; i += NT) s_A[i] = (BAND ? T->mfma_a_band : T->mfma_a)[i];
+    for (int i = threadIdx.x; i < 12 * 64; i += NT) s_A[i] = T->mfma_a[i];
     if (LUT_LDS)
       for (int i = threadIdx.x; i < 3 * LUT_WORDS; i += NT) s_lut[i] = (&T->lut[0][0])[i];
   }
@@ -965,7 +926,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   const int g = lane >> 4, bcol = lane & 15;
   const int c4 = lane & 31, pr = lane >> 5;
   const int q_dc[2] = {T->qint[0][0], T->qint[1][0]};
-  const unsigned long long zlog = BAND ? T->zlog : 0ull;  // wave-uniform: SGPRs
+  const bool cz_on = PIX && !AUDIT && MIJ_K1_CZ && T->cz_on;  // wave-uniform
   const Geom &G = a.g;
   const int bw = G.w >> 3, mw = G.w >> 4;
   const int ntiles = a.nframes * G.tiles_per_frame;
@@ -1145,7 +1106,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
         return mx < mwf;
       };
       auto block_of = [&](const int nt, int &blk) -> bool { return block_at(nt, bcol, blk); };
-      auto finish = [&](const int nt, int (&o)[16], uint32_t zm) {
+      auto finish = [&](const int nt, int (&o)[16], bool acz) {
         const int comp = nt == 2 ? 1 : 0;
         int blk;
         const bool valid = block_of(nt, blk);
@@ -1229,11 +1190,11 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
             pred0 = blk == cstart ? (a.dc_pred ? (int)a.dc_pred[p.f * 4 + (comp == 0 ? 0 : (bcol >= 8 ? 2 : 1))] : 0)
                                   : (int)a.dc[(long long)p.f * G.nblk + blk - 1];
           }
-          emit_tokens<BAND>(o, zm, lane, g, bcol, valid, comp == 1, !PIX && a.dc_diffed, first_pred, pred0,
+          emit_tokens(o, lane, g, bcol, valid, comp == 1, !PIX && a.dc_diffed, first_pred, pred0,
                       a.tok + (long long)p.f * G.nseg * SEG_TOK, (uint32_t)seg * SEG_TOK, a.tok0 + fs,
                       a.seg_ntok + fs, s_hdc[TOK ? slot : 0][comp][bcol & (HREP - 1)],
                       s_hac[TOK ? slot : 0][comp][bcol & (HREP - 1)],
-                      s_st[TOK ? wave : 0], kflags);
+                      s_st[TOK ? wave : 0], kflags, acz);
         }
       };
       if (PIX && do_dct) {
@@ -1259,39 +1220,57 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
           v4i(&acc)[4] = accs[cur];
           const float lc = lcs[cur];
           int o[16];
+          // Chroma N-tile: when |N| < L_z (Tables::czl) for every AC
+          // coefficient of every lane, all of them quantise to 0 (the
+          // reference's |F/q| < 1: DESIGN.md §5.2) -- common at Q <= 75, where
+          // the chroma quantisers are large.  Then the N-tile is its DC
+          // coefficients alone: no quantisation or replay, and in the token
+          // variants no staging or AC tokens (the coefficient variants store
+          // the zeros).  (Not in the audit variant, whose decisions the tests
+          // compare with tests/tau_check.c's model coefficient by coefficient.)
+          if constexpr (!AUDIT) {
+            if (nt == 2 && cz_on) {
+              // |N| < L_z for coefficient z: N + L and N - L both in range,
+              // i.e. (N - L) negative and (N + L) not; the sign bit of the
+              // AND of (N - L) & ~(N + L) over the lane's 16 is set iff all are
+              const int4 *czl = (const int4 *)&s_czl[16 * g];
+              uint32_t all = ~0u;
+#pragma unroll
+              for (int m = 0; m < 4; m++) {
+                const int4 Lq = czl[m];
+                const int Lv[4] = {Lq.x, Lq.y, Lq.z, Lq.w};
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                  const uint32_t lo = (uint32_t)acc[m][r] - (uint32_t)Lv[r], hi = (uint32_t)acc[m][r] + (uint32_t)Lv[r];
+                  all &= lo & ~hi;
+                }
+              }
+              if (!__ballot((int)all >= 0)) {
+#pragma unroll
+                for (int k = 0; k < 16; k++) o[k] = 0;
+                bool tie;
+                const int dcv = dc_fast(acc[0][0], 8 * q_dc[comp], s_inv8q[comp], tie);
+                if (g == 0) o[0] = dcv;
+                if (__ballot(tie && g == 0))
+                  if (g == 0 && tie) o[0] = dc_tie(dcv, s_dctie[comp]);
+                K1_PHASE(3);
+                finish(nt, o, true);
+                K1_PHASE(4);
+                continue;
+              }
+            }
+          }
           // trunc(t - tau) is the output; the lane's sums of trunc(t - tau)
           // and trunc(t + tau) differ iff some coefficient's +-tau interval
           // straddles a truncation boundary (each hi >= its lo)
           int slo = 0, shi = 0;
-          uint32_t zm = 0;  // band order: the N-tile's all-zero bands (wave-uniform)
           if (kflags & K1F_NO_QUANT) {
 #pragma unroll
             for (int k = 0; k < 16; k++) o[k] = acc[k >> 2][k & 3];
           } else
 #pragma unroll
           for (int m = 0; m < 4; m++) {
-            if constexpr (BAND) {
-              // |N| < L in every lane: the reference's |F/q| < 1 for all of
-              // the band (Tables::zlim; the DC at g == 0 is not part of it)
-              // (an opaque copy: the limits are re-derived per use on the
-              // scalar unit instead of eight of them held in SGPRs)
-              unsigned long long zl = zlog;
-              asm volatile("" : "+s"(zl));
-              const uint32_t lg = (uint32_t)(zl >> (5 * (4 * comp + m))) & 31u;
-              if (lg) {
-                const uint32_t L = 1u << lg;
-                const uint32_t x = ((uint32_t)((m == 0 && g == 0) ? 0 : acc[m][0]) + L) |
-                                   ((uint32_t)acc[m][1] + L) | ((uint32_t)acc[m][2] + L) |
-                                   ((uint32_t)acc[m][3] + L);
-                if (!__ballot(x >= 2u * L)) {
-                  zm |= 1u << m;
-#pragma unroll
-                  for (int r = 0; r < 4; r++) o[4 * m + r] = 0;
-                  continue;
-                }
-              }
-            }
-            const float4 fac = *(const float4 *)&s_fac[comp][BAND ? 16 * m + 4 * g : 16 * g + 4 * m];
+            const float4 fac = *(const float4 *)&s_fac[comp][16 * g + 4 * m];
             const f2v lc2 = {lc, lc};
 #pragma unroll
             for (int h = 0; h < 2; h++) {
@@ -1320,7 +1299,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
               for (int r = 0; r < 4; r++) {
                 const int k = 4 * m + r;
                 const float nf = (float)acc[m][r];
-                const float fa = s_fac[comp][zof(g, k)];
+                const float fa = s_fac[comp][16 * g + k];
                 const float tv = fmaf(fa, lc, 1.0e-6f);
                 mm |= (uint32_t)((int)fmaf(nf, fa, -tv) != (int)fmaf(nf, fa, tv)) << k;
               }
@@ -1390,7 +1369,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
                   const int j = r + (lane >> 3), x = lane & 7;
                   const int e = lst[j < nch ? j : 0];
                   const int ol = e >> 4, k = e & 15;
-                  const int z = zof(ol >> 4, k);
+                  const int z = 16 * (ol >> 4) + k;
                   const int rz = s_zz[z], v = rz >> 3, u = rz & 7;
                   const uint8_t *Pb = L + (nt * 16 + (ol & 15)) * LDS_BLK;
                   double in = 0.0;
@@ -1428,7 +1407,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
               while (mm) {
                 const int k = __ffs(mm) - 1;
                 mm &= mm - 1u;
-                const int z = zof(g, k);
+                const int z = 16 * g + k;
                 const int v = ac_exact(Pb, z, s_qint[comp][z], s_cos, s_zz);
 #pragma unroll
                 for (int j = 0; j < 16; j++) o[j] = j == k ? v : o[j];
@@ -1439,14 +1418,14 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
           // store (their VMEM count per tile varies)
           if (nt == MIJ_K1_DMAWAIT_NT && !DEFER && !(kflags & K1F_NO_DMAWAIT)) dma_wait();
           K1_PHASE(3);
-          finish(nt, o, zm);
+          finish(nt, o, false);
           K1_PHASE(4);
         }
       } else if (!PIX) {
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
           int o[16];
-          finish(nt, o, 0u);
+          finish(nt, o, false);
         }
       }
       if (PIX) wave_lds_sync();
@@ -3209,8 +3188,15 @@ constexpr int PF_THREADS = 256, PF_WAVES = PF_THREADS / 64;
 #ifndef MIJ_PACK_FLAT
 #define MIJ_PACK_FLAT 1
 #endif
+#ifndef MIJ_PF_K
+#define MIJ_PF_K 2
+#endif
 #ifndef MIJ_PF_OCC
 #define MIJ_PF_OCC 8
+#endif
+constexpr int PF_K = MIJ_PF_K;  // chunks per thread per round
+#ifndef MIJ_PF_PREFETCH
+#define MIJ_PF_PREFETCH 1
 #endif
 #ifndef MIJ_PF_OCC_WIDE
 #define MIJ_PF_OCC_WIDE 6
@@ -3223,7 +3209,7 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   __shared__ uint32_t buf[PW];
   __shared__ uint32_t tab[2 * 256];
   __shared__ uint32_t s_cp[PACK_SEGS + 1];  // exclusive prefix of the segments' chunks; [64]: all
-  __shared__ uint32_t s_ws[2][PF_WAVES];     // a round's bits per wave (two rounds in turn)
+  __shared__ uint32_t s_ws[2][PF_K][PF_WAVES];  // a round's bits per chunk set and wave (two rounds in turn)
   __shared__ unsigned long long s_prefix;
   __shared__ int s_ticket;
   __shared__ uint32_t s_over;
@@ -3296,68 +3282,100 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   };
   // one sweep over the group's chunks: positions relative to the group's
   // first bit (+ boff); whole: every bit into the window (a chunk past it
-  // sets the overflow flag), else only the bits inside [lo_bit, hi_bit)
-  auto sweep = [&](bool whole, uint32_t boff, uint32_t lo_bit, uint32_t hi_bit) -> uint32_t {
+  // sets the overflow flag), else only the bits inside [lo_bit, hi_bit).
+  // A round takes PF_K chunks per thread (chunk c0 + 256 k + tid), all
+  // loaded at once, and needs one barrier; with `publish` the group's
+  // aggregate goes out as soon as the last round's scan has it, before that
+  // round is placed.
+  auto sweep = [&](bool whole, uint32_t boff, uint32_t lo_bit, uint32_t hi_bit, bool publish) -> uint32_t {
     const uint32_t lim = (PW - 1) * 32;  // one spare word for the shifted store
     uint32_t run = boff;
     bool over = false;
-    u4v tn;
-    chunk_load((uint32_t)tid, tn);
-    for (uint32_t c0 = 0, r = 0; c0 < C; c0 += PF_THREADS, r++) {
-      const u4v t = tn;
-      const bool have = c0 + tid < C;
-      if (c0 + PF_THREADS < C) chunk_load(c0 + PF_THREADS + tid, tn);  // next round in flight
-      uint32_t L[4], code[4], nzr[4];
-      uint32_t nb = decode(t, L, code, nzr);
-      if (!have) nb = 0;
-      const uint32_t x = wave_scan64(nb);
-      if (lane == 63) s_ws[r & 1][wave] = x;
-      __syncthreads();
-      uint32_t before = 0, tot = 0;
+    u4v tn[PF_K];  // the next round's chunks, loaded while a round is placed
 #pragma unroll
-      for (int w = 0; w < PF_WAVES; w++) {
-        const uint32_t v = s_ws[r & 1][w];
-        tot += v;
-        before += w < wave ? v : 0u;
+    for (int k = 0; k < PF_K; k++) chunk_load(k * PF_THREADS + tid, tn[k]);
+    for (uint32_t c0 = 0, r = 0; c0 < C; c0 += PF_K * PF_THREADS, r++) {
+      u4v t[PF_K];
+#pragma unroll
+      for (int k = 0; k < PF_K; k++) t[k] = tn[k];
+      if (MIJ_PF_PREFETCH && c0 + PF_K * PF_THREADS < C) {
+#pragma unroll
+        for (int k = 0; k < PF_K; k++) chunk_load(c0 + (PF_K + k) * PF_THREADS + tid, tn[k]);
+      } else if (!MIJ_PF_PREFETCH && c0 > 0) {
+#pragma unroll
+        for (int k = 0; k < PF_K; k++) chunk_load(c0 + k * PF_THREADS + tid, t[k]);
       }
-      const uint32_t pos = run + before + x - nb;
-      run += tot;
-      if (!nb) continue;
-      if (whole && pos + nb > lim) {
-        over = true;
-      } else if (nb <= 64) {
-        unsigned long long acc = 0;
+      uint32_t nb[PF_K], x[PF_K];
+      unsigned long long acc[PF_K];
+#pragma unroll
+      for (int k = 0; k < PF_K; k++) {
+        uint32_t L[4], code[4], nzr[4];
+        nb[k] = decode(t[k], L, code, nzr);  // (a chunk past the group: zero tokens, no bits)
+        if (c0 + k * PF_THREADS + tid >= C) nb[k] = 0;
+        acc[k] = 0;
 #pragma unroll
         for (int e = 0; e < 4; e++) {
-          for (uint32_t z = nzr[e]; z; z--) acc = (acc << Lz) | zcode;
-          acc = (acc << L[e]) | code[e];
+          for (uint32_t z = nzr[e]; z; z--) acc[k] = (acc[k] << Lz) | zcode;
+          acc[k] = (acc[k] << L[e]) | code[e];
         }
-        if (whole) put_bits64(buf, pos, acc << (64 - nb), nb);
-        else put_bits64_win(buf, pos, acc << (64 - nb), nb, lo_bit, hi_bit);
-      } else {  // more than 64 bits: token by token
-        uint32_t p = pos;
-        for (int e = 0; e < 4; e++) {
-          for (uint32_t z = nzr[e]; z; z--) {
-            if (whole) put_bits(buf, p, zcode, (int)Lz);
-            else if (p < hi_bit && p + Lz > lo_bit) put_bits_window(buf, p, lo_bit, hi_bit, zcode, (int)Lz);
-            p += Lz;
+        x[k] = wave_scan64(nb[k]);
+        if (lane == 63) s_ws[r & 1][k][wave] = x[k];
+      }
+      __syncthreads();
+      uint32_t pos[PF_K];
+#pragma unroll
+      for (int k = 0; k < PF_K; k++) {
+        uint32_t before = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < PF_WAVES; w++) {
+          const uint32_t v = s_ws[r & 1][k][w];
+          tot += v;
+          before += w < wave ? v : 0u;
+        }
+        pos[k] = run + before + x[k] - nb[k];
+        run += tot;
+      }
+      if (publish && c0 + PF_K * PF_THREADS >= C && tid == 0 && q > 0)
+        __hip_atomic_store(&a.pack_state[gid], LB_AGG | (run - boff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int k = 0; k < PF_K; k++) {
+        const uint32_t n = nb[k], p0 = pos[k];
+        if (!n) continue;
+        if (whole && p0 + n > lim) {
+          over = true;
+        } else if (n <= 64) {
+          if (whole) put_bits64(buf, p0, acc[k] << (64 - n), n);
+          else put_bits64_win(buf, p0, acc[k] << (64 - n), n, lo_bit, hi_bit);
+        } else {  // more than 64 bits (rare): the chunk again, token by token
+          u4v tt;
+          chunk_load(c0 + k * PF_THREADS + tid, tt);
+          uint32_t L[4], code[4], nzr[4];
+          decode(tt, L, code, nzr);
+          uint32_t p = p0;
+          for (int e = 0; e < 4; e++) {
+            for (uint32_t z = nzr[e]; z; z--) {
+              if (whole) put_bits(buf, p, zcode, (int)Lz);
+              else if (p < hi_bit && p + Lz > lo_bit) put_bits_window(buf, p, lo_bit, hi_bit, zcode, (int)Lz);
+              p += Lz;
+            }
+            if (L[e]) {
+              if (whole) put_bits(buf, p, code[e], (int)L[e]);
+              else if (p < hi_bit && p + L[e] > lo_bit) put_bits_window(buf, p, lo_bit, hi_bit, code[e], (int)L[e]);
+            }
+            p += L[e];
           }
-          if (L[e]) {
-            if (whole) put_bits(buf, p, code[e], (int)L[e]);
-            else if (p < hi_bit && p + L[e] > lo_bit) put_bits_window(buf, p, lo_bit, hi_bit, code[e], (int)L[e]);
-          }
-          p += L[e];
         }
       }
     }
     if (whole && __ballot(over) && lane == 0) s_over = 1;
     return run - boff;
   };
-  const uint32_t gbits = sweep(true, 0u, 0u, 0u);
-  // the group's aggregate out, then its start bit by decoupled look-back
-  // over the groups before it (wave 0; publishes the inclusive prefix)
-  if (tid == 0 && q > 0)
-    __hip_atomic_store(&a.pack_state[gid], LB_AGG | gbits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // (the group's aggregate goes out inside the sweep; an empty group's here)
+  const uint32_t gbits = sweep(true, 0u, 0u, 0u, true);
+  if (C == 0 && tid == 0 && q > 0)
+    __hip_atomic_store(&a.pack_state[gid], LB_AGG | 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // its start bit by decoupled look-back over the groups before it (wave 0;
+  // publishes the inclusive prefix)
   if (wave == 0) {
     const unsigned long long base = a.bit_base ? a.bit_base[f * 4 + comp] : 0u;
     unsigned long long *stt = a.pack_state;
@@ -3442,7 +3460,7 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
     __syncthreads();
     for (uint32_t i = tid; i < wn; i += PF_THREADS) buf[i] = 0;
     __syncthreads();
-    sweep(false, boff, w0 * 32, (w0 + wn) * 32);
+    sweep(false, boff, w0 * 32, (w0 + wn) * 32, false);
     __syncthreads();
     const uint32_t c0 = ((uint32_t)gw + w0) / EMIT_CW;
     for (uint32_t i = tid; i < wn; i += PF_THREADS) {
