@@ -571,11 +571,6 @@ constexpr uint32_t TOK_AC = 1u << 10;
 // token carries: magnitudes stop at class 11): k_pack_lb's code table holds
 // 0 for it -- no bits, no ZRLs
 constexpr uint32_t LB_NOTOK = TOK_AC | 0xFFu;
-// AC-token loop over both 32-bit mask halves at once (A/B knob; measured:
-// token K1 3.39 -> 3.49 ms, the selects cost more than the saved iterations)
-#ifndef MIJ_K1_ACMERGE
-#define MIJ_K1_ACMERGE 0
-#endif
 // software pipelining of K1's N-tiles, token variants (see the N-tile loop;
 // measured: token K1 3.504 -> 3.441 and 3.514 -> 3.459 ms, two A/B rounds on
 // one box; the coefficient variant spills at 168 VGPRs with it, 3.12 -> 3.18)
@@ -587,12 +582,6 @@ constexpr uint32_t LB_NOTOK = TOK_AC | 0xFFu;
 #endif
 // N-tile of the token K1 before whose stores the next tile's DMA is awaited
 // (A/B: 0, 1 and 2 measured equal, 3.36-3.39 ms)
-#ifndef MIJ_K1_TOKFMT
-#define MIJ_K1_TOKFMT 1
-#endif
-#ifndef MIJ_K1_SFFBH
-#define MIJ_K1_SFFBH 1
-#endif
 #ifndef MIJ_K1_DMAWAIT_NT
 #define MIJ_K1_DMAWAIT_NT 0
 #endif
@@ -723,93 +712,58 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
   // (run << 4 | cls) is sym | ZRLs << 8 (run <= 62).
   if (!acz && valid && !(kflags & K1F_NO_ACLOOP)) {
     const int16_t *sl = &st[0][0] + 64 * bcol;
+    // token of AC coefficient z; rank: the set bits of the block's mask below
+    // z with the DC position counted (the token's index is base + rank); zp:
+    // 63 - the previous set bit (0 for the first: the DC position)
     auto token = [&](int z, int rank, int zp) {
       const int cz = sl[z ^ zsw];
-      const int run = z - zp - 1;
       // m = cz, or ~|cz| when negative (its low cls bits are the magnitude
       // bits, encoder.c:456-458); its leading sign bits (v_ffbh_i32) are
-      // clz(|cz|), so cls = 32 - ffbh_i32(m) (cz != 0: m is neither 0 nor -1)
+      // clz(|cz|), so cls = 32 - ffbh_i32(m) (cz != 0: m is neither 0 nor -1;
+      // no builtin: __builtin_clrsb lowers to four instructions)
       const int m = cz + (cz >> 31);
-#if MIJ_K1_SFFBH
-      uint32_t lead;  // (no builtin; __builtin_clrsb lowers to four instructions)
+      uint32_t lead;
       asm("v_ffbh_i32 %0, %1" : "=v"(lead) : "v"(m));
       const uint32_t cls = 32u - lead;
-#else
-      const uint32_t cls = 32u - (uint32_t)__builtin_clz((uint32_t)max(cz, -cz));
-#endif
       const uint32_t mag = __builtin_amdgcn_ubfe((uint32_t)m, 0u, cls);
-#if MIJ_K1_TOKFMT
-      // run + 64 shifted by 4 is TOK_AC | run << 4 (run <= 62): one shift-or
-      // for the symbol word, one for the token (zp here: 63 - the previous
-      // set bit, so run + 64 = z + zp is one add)
+      // run + 64 = z + zp (one add) shifted by 4 is TOK_AC | run << 4 (run <=
+      // 62): the symbol word in one v_lshl_add (cls < 16), the token in one
+      // v_lshl_or
       const uint32_t runp = (uint32_t)(z + zp);
-      const uint32_t t = (runp << 4) | cls;
-      if (!(kflags & K1F_NO_TOKSTORE)) tok_at(segtok, segoff + (uint32_t)(base + 1 + rank)) = t | (mag << 16);
+      const uint32_t t = (runp << 4) + cls;
+      if (!(kflags & K1F_NO_TOKSTORE)) tok_at(segtok, segoff + (uint32_t)(base + rank)) = t | (mag << 16);
       if (!(kflags & K1F_NO_HIST)) {
         atomicAdd(&hAC[t & 255u], 1u);
         if (runp >= 80u) atomicAdd(&hAC[0xF0], (runp - 64u) >> 4);
       }
-#else
-      const uint32_t t = ((uint32_t)run << 4) | cls | TOK_AC;
-      if (!(kflags & K1F_NO_TOKSTORE)) tok_at(segtok, segoff + (uint32_t)(base + 1 + rank)) = t | (mag << 16);
-      if (!(kflags & K1F_NO_HIST)) {
-        atomicAdd(&hAC[t & 255u], 1u);
-        if (run >= 16) atomicAdd(&hAC[0xF0], (unsigned)(run >> 4));
-      }
-#endif
     };
     const uint32_t cm = 0x11111111u << g;
     const int rank_lo = __popc(Mlo), zp_lo = 31 - __clz((int)(Mlo | 1u));
-#if MIJ_K1_ACMERGE
-    // one loop over both halves: the wave runs max(lo + hi) iterations
-    // instead of max(lo) + max(hi), at a few selects per iteration
-    uint32_t mlo = Mlo & cm, mhi = Mhi & cm;
-    while (mlo | mhi) {
-      const bool lo = mlo != 0;
-      const uint32_t m = lo ? mlo : mhi, M = lo ? Mlo : Mhi;
-      const int zz = __builtin_ctz(m);
-      const uint32_t bef = M & ((1u << zz) - 1u);
-      const int h = lo ? 0 : 32;
-      token(h + zz, (lo ? 0 : rank_lo) + __popc(bef), bef ? h + 31 - __clz((int)bef) : (lo ? 0 : zp_lo));
-      if (lo) mlo &= mlo - 1u;
-      else mhi &= mhi - 1u;
-    }
-#else
-#if MIJ_K1_TOKFMT
-#define MIJ_BELOW(M, z) __builtin_amdgcn_ubfe((M), 0u, (uint32_t)(z))  // bits of M below z: one v_bfe
-#else
-#define MIJ_BELOW(M, z) ((M) & ((1u << (z)) - 1u))
-#endif
-#if MIJ_K1_TOKFMT
-    // (token's zp argument: 63 - the previous set bit)
+    // (Measured and dropped: one loop over both 32-bit halves, the wave
+    // running max(lo + hi) iterations instead of max(lo) + max(hi) at a few
+    // selects per iteration: 3.39 -> 3.49 ms.)
+    // The DC position (bit 0) counted as set below every AC token of the low
+    // half: the set bits below z then always include one (the run's start is
+    // their highest, 0 for the first token) and their count is the token's
+    // index past the block's DC token
+    const uint32_t M1 = Mlo | 1u;
     for (uint32_t m = Mlo & cm; m; m &= m - 1u) {
       const int z = __builtin_ctz(m);
-      const uint32_t bef = MIJ_BELOW(Mlo, z);
-      token(z, __popc(bef), 32 + __clz((int)(bef | 1u)));
+      const uint32_t bef = __builtin_amdgcn_ubfe(M1, 0u, (uint32_t)z);  // bits below z: one v_bfe
+      uint32_t lz;  // (bef != 0: no zero check)
+      asm("v_ffbh_u32 %0, %1" : "=v"(lz) : "v"(bef));
+      token(z, __popc(bef), 32 + (int)lz);
     }
+    const int rank_lo1 = rank_lo + 1;
     for (uint32_t m = Mhi & cm; m; m &= m - 1u) {
       const int zz = __builtin_ctz(m);
-      const uint32_t bef = MIJ_BELOW(Mhi, zz);
+      const uint32_t bef = __builtin_amdgcn_ubfe(Mhi, 0u, (uint32_t)zz);
       // v_ffbh_u32 of 0 is ~0u: the min picks 63 - zp_lo exactly when no
       // bit of the high half lies below zz (no compare and select)
       uint32_t lz;
       asm("v_ffbh_u32 %0, %1" : "=v"(lz) : "v"(bef));
-      token(32 + zz, rank_lo + __popc(bef), (int)min(lz, (uint32_t)(63 - zp_lo)));
+      token(32 + zz, rank_lo1 + __popc(bef), (int)min(lz, (uint32_t)(63 - zp_lo)));
     }
-#else
-    for (uint32_t m = Mlo & cm; m; m &= m - 1u) {
-      const int z = __builtin_ctz(m);
-      const uint32_t bef = MIJ_BELOW(Mlo, z);
-      token(z, __popc(bef), 31 - __clz((int)(bef | 1u)));
-    }
-    for (uint32_t m = Mhi & cm; m; m &= m - 1u) {
-      const int zz = __builtin_ctz(m);
-      const uint32_t bef = MIJ_BELOW(Mhi, zz);
-      token(32 + zz, rank_lo + __popc(bef), bef ? 63 - __clz((int)bef) : zp_lo);
-    }
-#endif
-#undef MIJ_BELOW
-#endif
   }
   wave_lds_sync();
 }
