@@ -582,6 +582,11 @@ constexpr uint32_t LB_NOTOK = TOK_AC | 0xFFu;
 #endif
 // N-tile of the token K1 before whose stores the next tile's DMA is awaited
 // (A/B: 0, 1 and 2 measured equal, 3.36-3.39 ms)
+// AC tokens by rank (lane g: ranks g, g + 4, ...) instead of by zigzag
+// residue (z == g mod 4) (A/B knob)
+#ifndef MIJ_K1_RANKSPLIT
+#define MIJ_K1_RANKSPLIT 0
+#endif
 #ifndef MIJ_K1_DMAWAIT_NT
 #define MIJ_K1_DMAWAIT_NT 0
 #endif
@@ -747,7 +752,18 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
     // their highest, 0 for the first token) and their count is the token's
     // index past the block's DC token
     const uint32_t M1 = Mlo | 1u;
+#if MIJ_K1_RANKSPLIT
+    // lane g takes the block's set bits of rank g, g + 4, ... (the four
+    // lanes of a block share its tokens evenly, where z == g (mod 4) gave
+    // one of them most of a textured block's low frequencies)
+    auto drop = [](uint32_t m, int n) {
+      for (int i = 0; i < n; i++) m &= m - 1u;
+      return m;
+    };
+    for (uint32_t m = drop(Mlo, g); m; m = drop(m, 4)) {
+#else
     for (uint32_t m = Mlo & cm; m; m &= m - 1u) {
+#endif
       const int z = __builtin_ctz(m);
       const uint32_t bef = __builtin_amdgcn_ubfe(M1, 0u, (uint32_t)z);  // bits below z: one v_bfe
       uint32_t lz;  // (bef != 0: no zero check)
@@ -755,7 +771,12 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
       token(z, __popc(bef), 32 + (int)lz);
     }
     const int rank_lo1 = rank_lo + 1;
+#if MIJ_K1_RANKSPLIT
+    // (the high half continues the rank sequence where the low half ended)
+    for (uint32_t m = drop(Mhi, (g - rank_lo) & 3); m; m = drop(m, 4)) {
+#else
     for (uint32_t m = Mhi & cm; m; m &= m - 1u) {
+#endif
       const int zz = __builtin_ctz(m);
       const uint32_t bef = __builtin_amdgcn_ubfe(Mhi, 0u, (uint32_t)zz);
       // v_ffbh_u32 of 0 is ~0u: the min picks 63 - zp_lo exactly when no
@@ -3660,7 +3681,7 @@ __device__ __forceinline__ void stuff_chunk(const WordFn &word, const AfterFn &a
   // the 0xFF bytes before it (wave totals through LDS, a wave scan per round).
   const unsigned long long wb0 = cb + (unsigned long long)wave * (4 * WPW);
   uint32_t wds[WPW / 64];
-  int lims[WPW / 64];
+  int lims[WPW / 64], cfs[WPW / 64];
   int wcnt = 0;
 #pragma unroll
   for (int k = 0; k < WPW / 64; k++) {
@@ -3669,7 +3690,10 @@ __device__ __forceinline__ void stuff_chunk(const WordFn &word, const AfterFn &a
     wds[k] = lims[k] ? word(mb >> 2) : 0u;
   }
 #pragma unroll
-  for (int k = 0; k < WPW / 64; k++) wcnt += lims[k] ? ff_bytes(wds[k], lims[k]) : 0;
+  for (int k = 0; k < WPW / 64; k++) {  // (kept: the layout pass below needs them again)
+    cfs[k] = lims[k] ? ff_bytes(wds[k], lims[k]) : 0;
+    wcnt += cfs[k];
+  }
 #pragma unroll
   for (int k = 0; k < WPW / 64; k++)
     if (lims[k]) after_load((wb0 + 4ull * (64 * k + lane)) >> 2);
@@ -3682,7 +3706,7 @@ __device__ __forceinline__ void stuff_chunk(const WordFn &word, const AfterFn &a
   for (int k = 0; k < WPW / 64; k++) {
     const int lim = lims[k];
     const uint32_t wd = wds[k];
-    const int cf = lim ? ff_bytes(wd, lim) : 0;
+    const int cf = cfs[k];
     const int incl = (int)wave_scan64((uint32_t)(lim + cf));
     int op = carry + incl - (lim + cf);
     carry += __shfl(incl, 63);
