@@ -812,6 +812,10 @@ constexpr int k1_waves() {
   return k1_base(MODE) == K1M_TOK_OUT ? MIJ_K1_TOK_WAVES : (k1_wide<MODE>() ? 12 : 4);
 }
 
+// the MFMA digit chain's shifts as 64-bit pair shifts (A/B knob)
+#ifndef MIJ_K1_SHL64
+#define MIJ_K1_SHL64 0
+#endif
 // chroma all-AC-zero fast path of the token K1 (A/B knob)
 #ifndef MIJ_K1_CZ
 #define MIJ_K1_CZ 1
@@ -1046,10 +1050,39 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
             }
 #endif
             const v4i Fv = {F.x, F.y, F.z, F.w};
+#if MIJ_K1_SHL64
+            // The digit shifts two accumulators at a time (v_lshlrev_b64 of
+            // the pairs r = 0|1 and 2|3): the low element of a pair carries a
+            // bias of 2^17 from the first digit on, which keeps it inside
+            // [0, 2^25) before each shift (the partial sums stay within
+            // +-2^17 and +-16,711,680), so no bit crosses
+            // into its partner; N = the low element ^ 2^31 at the end.
+            v4i c;
+            if (d == 0) {
+              c = v4i{1 << 17, 0, 1 << 17, 0};
+            } else {
+#pragma unroll
+              for (int h = 0; h < 2; h++) {
+                unsigned long long pr = (unsigned long long)(uint32_t)acc[m][2 * h] |
+                                        ((unsigned long long)(uint32_t)acc[m][2 * h + 1] << 32);
+                asm("v_lshlrev_b64 %0, 7, %1" : "=v"(pr) : "v"(pr));
+                c[2 * h] = (int)(uint32_t)pr;
+                c[2 * h + 1] = (int)(uint32_t)(pr >> 32);
+              }
+            }
+#else
             const v4i c = d == 0 ? v4i{0, 0, 0, 0} : acc[m] << 7;
+#endif
             acc[m] = (kflags & K1F_NO_MFMA) ? c + Fv + Bf
                                             : __builtin_amdgcn_mfma_i32_16x16x64_i8(Fv, Bf, c, 0, 0, 0);
           }
+#if MIJ_K1_SHL64
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+          acc[m][0] ^= (int)0x80000000u;
+          acc[m][2] ^= (int)0x80000000u;
+        }
+#endif
       };
 
       // coefficient input: this tile's planes were loaded one tile ahead;
