@@ -816,6 +816,10 @@ constexpr int k1_waves() {
 #ifndef MIJ_K1_SHL64
 #define MIJ_K1_SHL64 0
 #endif
+// the chroma all-AC-zero test on the top two MFMA digits (A/B knob)
+#ifndef MIJ_K1_CZ2
+#define MIJ_K1_CZ2 0
+#endif
 // chroma all-AC-zero fast path of the token K1 (A/B knob)
 #ifndef MIJ_K1_CZ
 #define MIJ_K1_CZ 1
@@ -885,10 +889,21 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   }
   if (threadIdx.x < 128) s_qint[threadIdx.x >> 6][threadIdx.x & 63] = T->qint[threadIdx.x >> 6][threadIdx.x & 63];
   if (threadIdx.x < 2) s_inv8q[threadIdx.x] = 1.0f / (float)(8 * T->qint[threadIdx.x][0]);
-  if (PIX && threadIdx.x < 64) s_czl[threadIdx.x] = T->czl[threadIdx.x];
+  // (MIJ_K1_CZ2: the limits of the top two digits, (N - D2) / 128 with
+  // |D2| <= 128 * 64 * 64 = 2^19: |N| < L whenever |(N - D2) / 128| < (L - 2^19) / 128)
+  if (PIX && threadIdx.x < 64)
+    s_czl[threadIdx.x] = !MIJ_K1_CZ2 ? T->czl[threadIdx.x]
+                                     : (threadIdx.x ? (T->czl[threadIdx.x] - (1 << 19)) >> 7 : 1 << 23);
   if (threadIdx.x < 2 * DCTIE_WORDS) (&s_dctie[0][0])[threadIdx.x] = (&T->dctie[0][0])[threadIdx.x];
   if (PIX) {
-    for (int i = threadIdx.x; i < 12 * 64; i += NT) s_A[i] = T->mfma_a[i];
+    for (int i = threadIdx.x; i < 12 * 64; i += NT) {
+      int4 v = T->mfma_a[i];
+      // MIJ_K1_CZ2: the DC row (row 0 of M-tile 0, lanes 0, 16, 32, 48) sums
+      // the pixels in the top digit instead of the last (dc_sum)
+      if (MIJ_K1_CZ2 && i < 3 * 64 && (i & 15) == 0 && (i >> 6) != 1)
+        v = (i >> 6) == 0 ? int4{0x01010101, 0x01010101, 0x01010101, 0x01010101} : int4{0, 0, 0, 0};
+      s_A[i] = v;
+    }
     if (LUT_LDS)
       for (int i = threadIdx.x; i < 3 * LUT_WORDS; i += NT) s_lut[i] = (&T->lut[0][0])[i];
   }
@@ -1024,65 +1039,84 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
       // on its predecessor's result; the N-tile's quantisation and stores
       // follow before the next N-tile's MFMAs (16 accumulator VGPRs live).
       const bool do_dct = !(kflags & K1F_NO_DCT);
-      auto dct_ntile = [&](const int nt, v4i (&acc)[4], float &lc) {
-        v4i Bf = *(const v4i *)(L + (nt * 16 + bcol) * LDS_BLK + 16 * g);
-        // L1 = sum |pixel - 128| of the block bounds the integer DCT's
-        // rounding error: |N - 2^19 sum K X| <= sum |W - 2^19 K| |X| <= L1 / 2
-        uint32_t l1 = 0;
+      // digit d of the chain for the four M-tiles (B operand Bf)
+      auto dct_digit = [&](const int d, v4i (&acc)[4], const v4i Bf) {
 #pragma unroll
-        for (int k = 0; k < 4; k++) l1 = __builtin_amdgcn_sad_u8((uint32_t)Bf[k], 0x80808080u, l1);
-        const auto r16 = __builtin_amdgcn_permlane16_swap(l1, l1, false, false);
-        l1 = r16[0] + r16[1];
-        const auto r32 = __builtin_amdgcn_permlane32_swap(l1, l1, false, false);
-        // 1.25 * (L1/2 + 64) for the integer DCT and float(N), + 0.095 L1 for
-        // the fp32 roundings of t -+ tau (<= 1.8e-7 |N| with |N| <= 2^19 L1)
-        lc = fmaf((float)(r32[0] + r32[1]), 0.72f, 80.0f);
-        Bf ^= (int)0x80808080;  // pixel - 128 as int8
-#pragma unroll
-        for (int d = 0; d < 3; d++)
-#pragma unroll
-          for (int m = 0; m < 4; m++) {
-            const int4 F = s_A[(3 * m + d) * 64 + lane];
+        for (int m = 0; m < 4; m++) {
+          const int4 F = s_A[(3 * m + d) * 64 + lane];
 #ifdef MIJ_K1_DIAG
-            if (kflags & K1F_EXTRA_LDS) {  // diagnostics: a second, unused read of the fragment
-              v4i dummy;
-              asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(dummy) : "v"((uint32_t)(uintptr_t)(lds_void_t *)&s_A[(3 * m + d) * 64 + lane]) : "memory");
-            }
-#endif
-            const v4i Fv = {F.x, F.y, F.z, F.w};
-#if MIJ_K1_SHL64
-            // The digit shifts two accumulators at a time (v_lshlrev_b64 of
-            // the pairs r = 0|1 and 2|3): the low element of a pair carries a
-            // bias of 2^17 from the first digit on, which keeps it inside
-            // [0, 2^25) before each shift (the partial sums stay within
-            // +-2^17 and +-16,711,680), so no bit crosses
-            // into its partner; N = the low element ^ 2^31 at the end.
-            v4i c;
-            if (d == 0) {
-              c = v4i{1 << 17, 0, 1 << 17, 0};
-            } else {
-#pragma unroll
-              for (int h = 0; h < 2; h++) {
-                unsigned long long pr = (unsigned long long)(uint32_t)acc[m][2 * h] |
-                                        ((unsigned long long)(uint32_t)acc[m][2 * h + 1] << 32);
-                asm("v_lshlrev_b64 %0, 7, %1" : "=v"(pr) : "v"(pr));
-                c[2 * h] = (int)(uint32_t)pr;
-                c[2 * h + 1] = (int)(uint32_t)(pr >> 32);
-              }
-            }
-#else
-            const v4i c = d == 0 ? v4i{0, 0, 0, 0} : acc[m] << 7;
-#endif
-            acc[m] = (kflags & K1F_NO_MFMA) ? c + Fv + Bf
-                                            : __builtin_amdgcn_mfma_i32_16x16x64_i8(Fv, Bf, c, 0, 0, 0);
+          if (kflags & K1F_EXTRA_LDS) {  // diagnostics: a second, unused read of the fragment
+            v4i dummy;
+            asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(dummy) : "v"((uint32_t)(uintptr_t)(lds_void_t *)&s_A[(3 * m + d) * 64 + lane]) : "memory");
           }
+#endif
+          const v4i Fv = {F.x, F.y, F.z, F.w};
 #if MIJ_K1_SHL64
+          // The digit shifts two accumulators at a time (v_lshlrev_b64 of
+          // the pairs r = 0|1 and 2|3): the low element of a pair carries a
+          // bias of 2^17 from the first digit on, which keeps it inside
+          // [0, 2^25) before each shift (the partial sums stay within
+          // +-2^17 and +-16,711,680), so no bit crosses
+          // into its partner; N = the low element ^ 2^31 at the end.
+          v4i c;
+          if (d == 0) {
+            c = v4i{1 << 17, 0, 1 << 17, 0};
+          } else {
+            // (the accumulator as two 64-bit values: the compiler's own
+            // v_lshlrev_b64 on the register pairs, with its MFMA-read wait
+            // states; inline asm here read stale results)
+            typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+            c = __builtin_bit_cast(v4i, __builtin_bit_cast(u64x2, acc[m]) << 7);
+          }
+#else
+          const v4i c = d == 0 ? v4i{0, 0, 0, 0} : acc[m] << 7;
+#endif
+          acc[m] = (kflags & K1F_NO_MFMA) ? c + Fv + Bf
+                                          : __builtin_amdgcn_mfma_i32_16x16x64_i8(Fv, Bf, c, 0, 0, 0);
+        }
+#if MIJ_K1_SHL64
+        if (d == 2) {
 #pragma unroll
         for (int m = 0; m < 4; m++) {
           acc[m][0] ^= (int)0x80000000u;
           acc[m][2] ^= (int)0x80000000u;
         }
+        }
 #endif
+      };
+      // the first ndig digits of N-tile nt (ndig < 3: the chroma test of
+      // MIJ_K1_CZ2 runs on the top two, the third digit follows if needed)
+      // the error bound of N-tile nt's N (lanes of a block: its L1) from the
+      // raw pixels Bp: L1 = sum |pixel - 128| bounds the integer DCT's
+      // rounding error: |N - 2^19 sum K X| <= sum |W - 2^19 K| |X| <= L1 / 2
+      auto dct_lc = [&](const v4i Bp) -> float {
+        uint32_t l1 = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) l1 = __builtin_amdgcn_sad_u8((uint32_t)Bp[k], 0x80808080u, l1);
+        const auto r16 = __builtin_amdgcn_permlane16_swap(l1, l1, false, false);
+        l1 = r16[0] + r16[1];
+        const auto r32 = __builtin_amdgcn_permlane32_swap(l1, l1, false, false);
+        // 1.25 * (L1/2 + 64) for the integer DCT and float(N), + 0.095 L1 for
+        // the fp32 roundings of t -+ tau (<= 1.8e-7 |N| with |N| <= 2^19 L1)
+        return fmaf((float)(r32[0] + r32[1]), 0.72f, 80.0f);
+      };
+      auto dct_ntile = [&](const int nt, v4i (&acc)[4], float &lc, const int ndig) {
+        const v4i Bp = *(const v4i *)(L + (nt * 16 + bcol) * LDS_BLK + 16 * g);
+        // (two digits: the chroma test needs no bound; the third digit's
+        // path computes it)
+        if (ndig == 3) lc = dct_lc(Bp);
+        const v4i Bf = Bp ^ (int)0x80808080;  // pixel - 128 as int8
+#pragma unroll
+        for (int d = 0; d < 3; d++)
+          if (d < ndig) dct_digit(d, acc, Bf);
+      };
+      // the DC row's pixel sum: in the last digit, or (MIJ_K1_CZ2) in the top
+      // one, i.e. times 2^14 after the third digit and 2^7 after the second
+      // (with MIJ_K1_SHL64 the second digit's low elements carry 2^24)
+      auto dc_sum = [&](const int acc00, const int ndig) -> int {
+        if (!MIJ_K1_CZ2) return acc00;
+        if (ndig == 3) return acc00 >> 14;
+        return (MIJ_K1_SHL64 ? acc00 - (1 << 24) : acc00) >> 7;
       };
 
       // coefficient input: this tile's planes were loaded one tile ahead;
@@ -1212,21 +1246,24 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
         constexpr bool PIPE = MIJ_K1_PIPE && TOK;
         v4i accs[PIPE ? 2 : 1][4];
         float lcs[PIPE ? 2 : 1];  // per block: error bound of N in N units
-        if (PIPE) dct_ntile(0, accs[0], lcs[0]);
+        // (MIJ_K1_CZ2: the chroma N-tile's chain stops after two digits when
+        // the all-AC-zero test runs; the third follows if the test fails)
+        const int nd_c = MIJ_K1_CZ2 && cz_on ? 2 : 3;
+        if (PIPE) dct_ntile(0, accs[0], lcs[0], 3);
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
           const int comp = nt == 2 ? 1 : 0;
           const int cur = PIPE ? (nt & 1) : 0;
           if (!PIPE) {
-            dct_ntile(nt, accs[0], lcs[0]);
+            dct_ntile(nt, accs[0], lcs[0], nt == 2 ? nd_c : 3);
           } else if (nt + 1 < 3) {
 #if MIJ_K1_AREL
             asm volatile("" ::: "memory");  // A fragments re-read from LDS per N-tile
 #endif
-            dct_ntile(nt + 1, accs[PIPE ? (cur ^ 1) : 0], lcs[PIPE ? (cur ^ 1) : 0]);
+            dct_ntile(nt + 1, accs[PIPE ? (cur ^ 1) : 0], lcs[PIPE ? (cur ^ 1) : 0], nt + 1 == 2 ? nd_c : 3);
           }
           v4i(&acc)[4] = accs[cur];
-          const float lc = lcs[cur];
+          float lc = lcs[cur];
           int o[16];
           // Chroma N-tile: when |N| < L_z (Tables::czl) for every AC
           // coefficient of every lane, all of them quantise to 0 (the
@@ -1249,7 +1286,9 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
                 const int Lv[4] = {Lq.x, Lq.y, Lq.z, Lq.w};
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
-                  const uint32_t lo = (uint32_t)acc[m][r] - (uint32_t)Lv[r], hi = (uint32_t)acc[m][r] + (uint32_t)Lv[r];
+                  // (two digits with MIJ_K1_SHL64: the low elements' 2^24 bias off)
+                  const uint32_t v = (uint32_t)acc[m][r] - (MIJ_K1_CZ2 && MIJ_K1_SHL64 && !(r & 1) ? (1u << 24) : 0u);
+                  const uint32_t lo = v - (uint32_t)Lv[r], hi = v + (uint32_t)Lv[r];
                   all &= lo & ~hi;
                 }
               }
@@ -1257,7 +1296,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
 #pragma unroll
                 for (int k = 0; k < 16; k++) o[k] = 0;
                 bool tie;
-                const int dcv = dc_fast(acc[0][0], 8 * q_dc[comp], s_inv8q[comp], tie);
+                const int dcv = dc_fast(dc_sum(acc[0][0], nd_c), 8 * q_dc[comp], s_inv8q[comp], tie);
                 if (g == 0) o[0] = dcv;
                 if (__ballot(tie && g == 0))
                   if (g == 0 && tie) o[0] = dc_tie(dcv, s_dctie[comp]);
@@ -1265,6 +1304,11 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
                 finish(nt, o, true);
                 K1_PHASE(4);
                 continue;
+              }
+              if (MIJ_K1_CZ2) {  // the test failed: the third digit, and the bound
+                const v4i Bp = *(const v4i *)(L + (nt * 16 + bcol) * LDS_BLK + 16 * g);
+                lc = dct_lc(Bp);
+                dct_digit(2, acc, Bp ^ (int)0x80808080);
               }
             }
           }
@@ -1319,7 +1363,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
           }
           {  // z = 0: exact from the pixel sum (fac = 0 above)
             bool tie;
-            const int dcv = dc_fast(acc[0][0], 8 * q_dc[comp], s_inv8q[comp], tie);
+            const int dcv = dc_fast(dc_sum(acc[0][0], 3), 8 * q_dc[comp], s_inv8q[comp], tie);
             if (g == 0) o[0] = dcv;
             if (__ballot(tie && g == 0))
               if (g == 0 && tie) o[0] = dc_tie(dcv, s_dctie[comp]);
