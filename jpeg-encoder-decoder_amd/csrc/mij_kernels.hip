@@ -812,11 +812,16 @@ constexpr int k1_waves() {
   return k1_base(MODE) == K1M_TOK_OUT ? MIJ_K1_TOK_WAVES : (k1_wide<MODE>() ? 12 : 4);
 }
 
-// the MFMA digit chain's shifts as 64-bit pair shifts (A/B knob)
+// the MFMA digit chain's shifts as 64-bit pair shifts (config 3, two A/B
+// rounds on one box: token K1 3.15 -> 3.08 ms at Q=50, 4.74 -> 4.73 at Q=90;
+// v_lshlrev_b64 issues in the 4.5 cycles of a 32-bit left shift,
+// profiles/r04/probe/valu_rate5.txt)
 #ifndef MIJ_K1_SHL64
-#define MIJ_K1_SHL64 0
+#define MIJ_K1_SHL64 1
 #endif
-// the chroma all-AC-zero test on the top two MFMA digits (A/B knob)
+// the chroma all-AC-zero test on the top two MFMA digits (A/B knob; measured
+// 3.15 -> 3.09-3.13 ms alone at Q=50, nothing on top of MIJ_K1_SHL64, and
+// 4.74 -> 4.77 at Q=90, where the test is off)
 #ifndef MIJ_K1_CZ2
 #define MIJ_K1_CZ2 0
 #endif
