@@ -825,6 +825,11 @@ constexpr int k1_waves() {
 #ifndef MIJ_K1_CZ2
 #define MIJ_K1_CZ2 0
 #endif
+// the chroma N-tile's error bound computed only when its all-AC-zero test
+// fails (A/B knob)
+#ifndef MIJ_K1_LCDEFER
+#define MIJ_K1_LCDEFER 0
+#endif
 // chroma all-AC-zero fast path of the token K1 (A/B knob)
 #ifndef MIJ_K1_CZ
 #define MIJ_K1_CZ 1
@@ -1105,11 +1110,11 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
         // the fp32 roundings of t -+ tau (<= 1.8e-7 |N| with |N| <= 2^19 L1)
         return fmaf((float)(r32[0] + r32[1]), 0.72f, 80.0f);
       };
-      auto dct_ntile = [&](const int nt, v4i (&acc)[4], float &lc, const int ndig) {
+      auto dct_ntile = [&](const int nt, v4i (&acc)[4], float &lc, const int ndig, const bool want_lc) {
         const v4i Bp = *(const v4i *)(L + (nt * 16 + bcol) * LDS_BLK + 16 * g);
-        // (two digits: the chroma test needs no bound; the third digit's
-        // path computes it)
-        if (ndig == 3) lc = dct_lc(Bp);
+        // (two digits, or MIJ_K1_LCDEFER: the chroma test needs no bound; its
+        // fail path computes it)
+        if (ndig == 3 && want_lc) lc = dct_lc(Bp);
         const v4i Bf = Bp ^ (int)0x80808080;  // pixel - 128 as int8
 #pragma unroll
         for (int d = 0; d < 3; d++)
@@ -1254,18 +1259,20 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
         // (MIJ_K1_CZ2: the chroma N-tile's chain stops after two digits when
         // the all-AC-zero test runs; the third follows if the test fails)
         const int nd_c = MIJ_K1_CZ2 && cz_on ? 2 : 3;
-        if (PIPE) dct_ntile(0, accs[0], lcs[0], 3);
+        const bool lc_c = !(MIJ_K1_LCDEFER && cz_on);  // the chroma bound up front
+        if (PIPE) dct_ntile(0, accs[0], lcs[0], 3, true);
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
           const int comp = nt == 2 ? 1 : 0;
           const int cur = PIPE ? (nt & 1) : 0;
           if (!PIPE) {
-            dct_ntile(nt, accs[0], lcs[0], nt == 2 ? nd_c : 3);
+            dct_ntile(nt, accs[0], lcs[0], nt == 2 ? nd_c : 3, nt != 2 || lc_c);
           } else if (nt + 1 < 3) {
 #if MIJ_K1_AREL
             asm volatile("" ::: "memory");  // A fragments re-read from LDS per N-tile
 #endif
-            dct_ntile(nt + 1, accs[PIPE ? (cur ^ 1) : 0], lcs[PIPE ? (cur ^ 1) : 0], nt + 1 == 2 ? nd_c : 3);
+            dct_ntile(nt + 1, accs[PIPE ? (cur ^ 1) : 0], lcs[PIPE ? (cur ^ 1) : 0], nt + 1 == 2 ? nd_c : 3,
+                      nt + 1 != 2 || lc_c);
           }
           v4i(&acc)[4] = accs[cur];
           float lc = lcs[cur];
@@ -1310,10 +1317,10 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
                 K1_PHASE(4);
                 continue;
               }
-              if (MIJ_K1_CZ2) {  // the test failed: the third digit, and the bound
+              if (MIJ_K1_CZ2 || MIJ_K1_LCDEFER) {  // the test failed: the bound (and the third digit)
                 const v4i Bp = *(const v4i *)(L + (nt * 16 + bcol) * LDS_BLK + 16 * g);
                 lc = dct_lc(Bp);
-                dct_digit(2, acc, Bp ^ (int)0x80808080);
+                if (MIJ_K1_CZ2) dct_digit(2, acc, Bp ^ (int)0x80808080);
               }
             }
           }
@@ -3251,7 +3258,13 @@ constexpr int PF_THREADS = 256, PF_WAVES = PF_THREADS / 64;
 #ifndef MIJ_PF_OCC
 #define MIJ_PF_OCC 8
 #endif
-constexpr int PF_K = MIJ_PF_K;  // chunks per thread per round
+#ifndef MIJ_PF_K_WIDE
+#define MIJ_PF_K_WIDE MIJ_PF_K
+#endif
+// chunks per thread per round (the wide window's variant runs five
+// workgroups per CU by its LDS, with VGPRs to spare for larger rounds)
+template <int PW>
+constexpr int pf_k() { return PW > PACK_WORDS ? MIJ_PF_K_WIDE : MIJ_PF_K; }
 #ifndef MIJ_PF_PREFETCH
 #define MIJ_PF_PREFETCH 1
 #endif
@@ -3263,6 +3276,7 @@ constexpr int pf_occ() { return PW > PACK_WORDS ? MIJ_PF_OCC_WIDE : MIJ_PF_OCC; 
 static_assert(PACK_SEGS == 64, "k_pack_flat: one wave scans the group's segments");
 template <int PW, bool FF>
 __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs a) {
+  constexpr int PF_K = pf_k<PW>();
   __shared__ uint32_t buf[PW];
   __shared__ uint32_t tab[2 * 256];
   __shared__ uint32_t s_cp[PACK_SEGS + 1];  // exclusive prefix of the segments' chunks; [64]: all
