@@ -582,11 +582,6 @@ constexpr uint32_t LB_NOTOK = TOK_AC | 0xFFu;
 #endif
 // N-tile of the token K1 before whose stores the next tile's DMA is awaited
 // (A/B: 0, 1 and 2 measured equal, 3.36-3.39 ms)
-// AC tokens by rank (lane g: ranks g, g + 4, ...) instead of by zigzag
-// residue (z == g mod 4) (A/B knob)
-#ifndef MIJ_K1_RANKSPLIT
-#define MIJ_K1_RANKSPLIT 0
-#endif
 #ifndef MIJ_K1_DMAWAIT_NT
 #define MIJ_K1_DMAWAIT_NT 0
 #endif
@@ -752,18 +747,7 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
     // their highest, 0 for the first token) and their count is the token's
     // index past the block's DC token
     const uint32_t M1 = Mlo | 1u;
-#if MIJ_K1_RANKSPLIT
-    // lane g takes the block's set bits of rank g, g + 4, ... (the four
-    // lanes of a block share its tokens evenly, where z == g (mod 4) gave
-    // one of them most of a textured block's low frequencies)
-    auto drop = [](uint32_t m, int n) {
-      for (int i = 0; i < n; i++) m &= m - 1u;
-      return m;
-    };
-    for (uint32_t m = drop(Mlo, g); m; m = drop(m, 4)) {
-#else
     for (uint32_t m = Mlo & cm; m; m &= m - 1u) {
-#endif
       const int z = __builtin_ctz(m);
       const uint32_t bef = __builtin_amdgcn_ubfe(M1, 0u, (uint32_t)z);  // bits below z: one v_bfe
       uint32_t lz;  // (bef != 0: no zero check)
@@ -771,12 +755,7 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
       token(z, __popc(bef), 32 + (int)lz);
     }
     const int rank_lo1 = rank_lo + 1;
-#if MIJ_K1_RANKSPLIT
-    // (the high half continues the rank sequence where the low half ended)
-    for (uint32_t m = drop(Mhi, (g - rank_lo) & 3); m; m = drop(m, 4)) {
-#else
     for (uint32_t m = Mhi & cm; m; m &= m - 1u) {
-#endif
       const int zz = __builtin_ctz(m);
       const uint32_t bef = __builtin_amdgcn_ubfe(Mhi, 0u, (uint32_t)zz);
       // v_ffbh_u32 of 0 is ~0u: the min picks 63 - zp_lo exactly when no
@@ -818,17 +797,6 @@ constexpr int k1_waves() {
 // profiles/r04/probe/valu_rate5.txt)
 #ifndef MIJ_K1_SHL64
 #define MIJ_K1_SHL64 1
-#endif
-// the chroma all-AC-zero test on the top two MFMA digits (A/B knob; measured
-// 3.15 -> 3.09-3.13 ms alone at Q=50, nothing on top of MIJ_K1_SHL64, and
-// 4.74 -> 4.77 at Q=90, where the test is off)
-#ifndef MIJ_K1_CZ2
-#define MIJ_K1_CZ2 0
-#endif
-// the chroma N-tile's error bound computed only when its all-AC-zero test
-// fails (A/B knob)
-#ifndef MIJ_K1_LCDEFER
-#define MIJ_K1_LCDEFER 0
 #endif
 // chroma all-AC-zero fast path of the token K1 (A/B knob)
 #ifndef MIJ_K1_CZ
@@ -899,21 +867,10 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   }
   if (threadIdx.x < 128) s_qint[threadIdx.x >> 6][threadIdx.x & 63] = T->qint[threadIdx.x >> 6][threadIdx.x & 63];
   if (threadIdx.x < 2) s_inv8q[threadIdx.x] = 1.0f / (float)(8 * T->qint[threadIdx.x][0]);
-  // (MIJ_K1_CZ2: the limits of the top two digits, (N - D2) / 128 with
-  // |D2| <= 128 * 64 * 64 = 2^19: |N| < L whenever |(N - D2) / 128| < (L - 2^19) / 128)
-  if (PIX && threadIdx.x < 64)
-    s_czl[threadIdx.x] = !MIJ_K1_CZ2 ? T->czl[threadIdx.x]
-                                     : (threadIdx.x ? (T->czl[threadIdx.x] - (1 << 19)) >> 7 : 1 << 23);
+  if (PIX && threadIdx.x < 64) s_czl[threadIdx.x] = T->czl[threadIdx.x];
   if (threadIdx.x < 2 * DCTIE_WORDS) (&s_dctie[0][0])[threadIdx.x] = (&T->dctie[0][0])[threadIdx.x];
   if (PIX) {
-    for (int i = threadIdx.x; i < 12 * 64; i += NT) {
-      int4 v = T->mfma_a[i];
-      // MIJ_K1_CZ2: the DC row (row 0 of M-tile 0, lanes 0, 16, 32, 48) sums
-      // the pixels in the top digit instead of the last (dc_sum)
-      if (MIJ_K1_CZ2 && i < 3 * 64 && (i & 15) == 0 && (i >> 6) != 1)
-        v = (i >> 6) == 0 ? int4{0x01010101, 0x01010101, 0x01010101, 0x01010101} : int4{0, 0, 0, 0};
-      s_A[i] = v;
-    }
+    for (int i = threadIdx.x; i < 12 * 64; i += NT) s_A[i] = T->mfma_a[i];
     if (LUT_LDS)
       for (int i = threadIdx.x; i < 3 * LUT_WORDS; i += NT) s_lut[i] = (&T->lut[0][0])[i];
   }
@@ -1087,19 +1044,19 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
 #if MIJ_K1_SHL64
         if (d == 2) {
 #pragma unroll
-        for (int m = 0; m < 4; m++) {
-          acc[m][0] ^= (int)0x80000000u;
-          acc[m][2] ^= (int)0x80000000u;
-        }
+          for (int m = 0; m < 4; m++) {
+            acc[m][0] ^= (int)0x80000000u;
+            acc[m][2] ^= (int)0x80000000u;
+          }
         }
 #endif
       };
-      // the first ndig digits of N-tile nt (ndig < 3: the chroma test of
-      // MIJ_K1_CZ2 runs on the top two, the third digit follows if needed)
-      // the error bound of N-tile nt's N (lanes of a block: its L1) from the
-      // raw pixels Bp: L1 = sum |pixel - 128| bounds the integer DCT's
-      // rounding error: |N - 2^19 sum K X| <= sum |W - 2^19 K| |X| <= L1 / 2
-      auto dct_lc = [&](const v4i Bp) -> float {
+      // N-tile nt: the error bound of its N (lanes of a block: its L1) and
+      // the three digits
+      auto dct_ntile = [&](const int nt, v4i (&acc)[4], float &lc) {
+        const v4i Bp = *(const v4i *)(L + (nt * 16 + bcol) * LDS_BLK + 16 * g);
+        // L1 = sum |pixel - 128| of the block bounds the integer DCT's
+        // rounding error: |N - 2^19 sum K X| <= sum |W - 2^19 K| |X| <= L1 / 2
         uint32_t l1 = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) l1 = __builtin_amdgcn_sad_u8((uint32_t)Bp[k], 0x80808080u, l1);
@@ -1108,25 +1065,10 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
         const auto r32 = __builtin_amdgcn_permlane32_swap(l1, l1, false, false);
         // 1.25 * (L1/2 + 64) for the integer DCT and float(N), + 0.095 L1 for
         // the fp32 roundings of t -+ tau (<= 1.8e-7 |N| with |N| <= 2^19 L1)
-        return fmaf((float)(r32[0] + r32[1]), 0.72f, 80.0f);
-      };
-      auto dct_ntile = [&](const int nt, v4i (&acc)[4], float &lc, const int ndig, const bool want_lc) {
-        const v4i Bp = *(const v4i *)(L + (nt * 16 + bcol) * LDS_BLK + 16 * g);
-        // (two digits, or MIJ_K1_LCDEFER: the chroma test needs no bound; its
-        // fail path computes it)
-        if (ndig == 3 && want_lc) lc = dct_lc(Bp);
+        lc = fmaf((float)(r32[0] + r32[1]), 0.72f, 80.0f);
         const v4i Bf = Bp ^ (int)0x80808080;  // pixel - 128 as int8
 #pragma unroll
-        for (int d = 0; d < 3; d++)
-          if (d < ndig) dct_digit(d, acc, Bf);
-      };
-      // the DC row's pixel sum: in the last digit, or (MIJ_K1_CZ2) in the top
-      // one, i.e. times 2^14 after the third digit and 2^7 after the second
-      // (with MIJ_K1_SHL64 the second digit's low elements carry 2^24)
-      auto dc_sum = [&](const int acc00, const int ndig) -> int {
-        if (!MIJ_K1_CZ2) return acc00;
-        if (ndig == 3) return acc00 >> 14;
-        return (MIJ_K1_SHL64 ? acc00 - (1 << 24) : acc00) >> 7;
+        for (int d = 0; d < 3; d++) dct_digit(d, acc, Bf);
       };
 
       // coefficient input: this tile's planes were loaded one tile ahead;
@@ -1256,26 +1198,21 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
         constexpr bool PIPE = MIJ_K1_PIPE && TOK;
         v4i accs[PIPE ? 2 : 1][4];
         float lcs[PIPE ? 2 : 1];  // per block: error bound of N in N units
-        // (MIJ_K1_CZ2: the chroma N-tile's chain stops after two digits when
-        // the all-AC-zero test runs; the third follows if the test fails)
-        const int nd_c = MIJ_K1_CZ2 && cz_on ? 2 : 3;
-        const bool lc_c = !(MIJ_K1_LCDEFER && cz_on);  // the chroma bound up front
-        if (PIPE) dct_ntile(0, accs[0], lcs[0], 3, true);
+        if (PIPE) dct_ntile(0, accs[0], lcs[0]);
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
           const int comp = nt == 2 ? 1 : 0;
           const int cur = PIPE ? (nt & 1) : 0;
           if (!PIPE) {
-            dct_ntile(nt, accs[0], lcs[0], nt == 2 ? nd_c : 3, nt != 2 || lc_c);
+            dct_ntile(nt, accs[0], lcs[0]);
           } else if (nt + 1 < 3) {
 #if MIJ_K1_AREL
             asm volatile("" ::: "memory");  // A fragments re-read from LDS per N-tile
 #endif
-            dct_ntile(nt + 1, accs[PIPE ? (cur ^ 1) : 0], lcs[PIPE ? (cur ^ 1) : 0], nt + 1 == 2 ? nd_c : 3,
-                      nt + 1 != 2 || lc_c);
+            dct_ntile(nt + 1, accs[PIPE ? (cur ^ 1) : 0], lcs[PIPE ? (cur ^ 1) : 0]);
           }
           v4i(&acc)[4] = accs[cur];
-          float lc = lcs[cur];
+          const float lc = lcs[cur];
           int o[16];
           // Chroma N-tile: when |N| < L_z (Tables::czl) for every AC
           // coefficient of every lane, all of them quantise to 0 (the
@@ -1298,9 +1235,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
                 const int Lv[4] = {Lq.x, Lq.y, Lq.z, Lq.w};
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
-                  // (two digits with MIJ_K1_SHL64: the low elements' 2^24 bias off)
-                  const uint32_t v = (uint32_t)acc[m][r] - (MIJ_K1_CZ2 && MIJ_K1_SHL64 && !(r & 1) ? (1u << 24) : 0u);
-                  const uint32_t lo = v - (uint32_t)Lv[r], hi = v + (uint32_t)Lv[r];
+                  const uint32_t lo = (uint32_t)acc[m][r] - (uint32_t)Lv[r], hi = (uint32_t)acc[m][r] + (uint32_t)Lv[r];
                   all &= lo & ~hi;
                 }
               }
@@ -1308,7 +1243,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
 #pragma unroll
                 for (int k = 0; k < 16; k++) o[k] = 0;
                 bool tie;
-                const int dcv = dc_fast(dc_sum(acc[0][0], nd_c), 8 * q_dc[comp], s_inv8q[comp], tie);
+                const int dcv = dc_fast(acc[0][0], 8 * q_dc[comp], s_inv8q[comp], tie);
                 if (g == 0) o[0] = dcv;
                 if (__ballot(tie && g == 0))
                   if (g == 0 && tie) o[0] = dc_tie(dcv, s_dctie[comp]);
@@ -1316,11 +1251,6 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
                 finish(nt, o, true);
                 K1_PHASE(4);
                 continue;
-              }
-              if (MIJ_K1_CZ2 || MIJ_K1_LCDEFER) {  // the test failed: the bound (and the third digit)
-                const v4i Bp = *(const v4i *)(L + (nt * 16 + bcol) * LDS_BLK + 16 * g);
-                lc = dct_lc(Bp);
-                if (MIJ_K1_CZ2) dct_digit(2, acc, Bp ^ (int)0x80808080);
               }
             }
           }
@@ -1375,7 +1305,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
           }
           {  // z = 0: exact from the pixel sum (fac = 0 above)
             bool tie;
-            const int dcv = dc_fast(dc_sum(acc[0][0], 3), 8 * q_dc[comp], s_inv8q[comp], tie);
+            const int dcv = dc_fast(acc[0][0], 8 * q_dc[comp], s_inv8q[comp], tie);
             if (g == 0) o[0] = dcv;
             if (__ballot(tie && g == 0))
               if (g == 0 && tie) o[0] = dc_tie(dcv, s_dctie[comp]);
