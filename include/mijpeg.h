@@ -84,7 +84,10 @@ enum {
                            defined behaviour (code length >= 32 etc.) */
     MIJ_EPPM = 6,       /* PPM rejected by the rules of utils/original.c:294-365 */
     MIJ_EIO = 7,        /* file could not be opened, read or written */
-    MIJ_EJPEG = 8       /* decoder: stream outside the supported JFIF subset or corrupt */
+    MIJ_EJPEG = 8,      /* decoder: stream outside the supported JFIF subset or corrupt */
+    MIJ_EHANG = 9       /* a device-side wait (pack look-back, ticket) outlasted its
+                           bound: the frame's device state was corrupted; the
+                           frame fails instead of the launch hanging */
 };
 int mij_last_error(void);
 const char *mij_strerror(int code);
@@ -149,7 +152,14 @@ int mij_batch_set_overlap(mij_batch *b, int nsub);
  *   MIJ_OPT_EMIT_SLOTS    0 (default: chosen from frame count, size and Q);
  *                         > 0: JFIF-assembly workgroups per frame
  *   MIJ_OPT_OVERLAP_PRIO  1 (default): the overlap stream (set_overlap) at
- *                         the highest priority; 0: the lowest */
+ *                         the highest priority; 0: the lowest
+ *   MIJ_OPT_FAULT_TICKET  0 (default).  Fault injection for tests: v > 0
+ *                         makes the next encode's packing start frame 0's
+ *                         luma pack ticket at v, as a stale ticket word would
+ *                         (pack group 0 never runs, the groups after it wait
+ *                         on its look-back word); the frame must fail with
+ *                         MIJ_EHANG within the wait bound instead of hanging
+ *                         the launch.  Consumed by that encode. */
 enum {
   MIJ_OPT_SEAM = 0,
   MIJ_OPT_FF_PACK = 1,
@@ -158,7 +168,8 @@ enum {
   MIJ_OPT_PACK_WIDE = 4,
   MIJ_OPT_EMIT_SLOTS = 5,
   MIJ_OPT_OVERLAP_PRIO = 6,
-  MIJ_OPT_COUNT = 7
+  MIJ_OPT_FAULT_TICKET = 7,
+  MIJ_OPT_COUNT = 8
 };
 int mij_batch_set_option(mij_batch *b, int opt, int value);
 int mij_batch_get_option(mij_batch *b, int opt);

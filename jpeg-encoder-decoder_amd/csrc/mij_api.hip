@@ -29,7 +29,7 @@ hipError_t launch_tables(const EntArgs &a, hipStream_t s);
 hipError_t launch_ehuf_struct(const HuffCode *hc, uint32_t *ehuf, hipStream_t s);
 hipError_t launch_bits(const EntArgs &a, hipStream_t s);
 hipError_t launch_scan(const EntArgs &a, hipStream_t s);
-hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s, bool state_zeroed = false);
+hipError_t launch_pack(const EntArgs &a, hipStream_t s, bool state_zeroed = false);
 hipError_t launch_emit(const EntArgs &a, hipStream_t s);
 hipError_t launch_seam_fix(const EntArgs &a, hipStream_t s);
 hipError_t launch_or_words(uint32_t *dst, const uint32_t *src, long long n, hipStream_t s);
@@ -82,6 +82,16 @@ static int fail(int code, const char *fmt, ...) {
   return code;
 }
 // for the other host translation units (mij_stream.hip)
+int mij_frame_fail(int ferr, const char *what, int frame) {
+  switch (ferr) {
+    case FERR_SPIN:
+      return fail(MIJ_EHANG, "%s %d: a device-side wait outlasted its bound (a pack group's look-back "
+                  "publication lost, or a stale pack ticket)", what, frame);
+    case FERR_OVERFLOW: return fail(MIJ_ENOSPC, "%s %d: bits past the scan buffer", what, frame);
+    case FERR_ASSEMBLY: return fail(MIJ_ENOSPC, "%s %d: a band piece outside its buffer", what, frame);
+  }
+  return fail(MIJ_ETABLE, "%s %d: Huffman table construction failed", what, frame);
+}
 int mij_fail(int code, const char *fmt, ...) {
   va_list ap;
   va_start(ap, fmt);
@@ -127,6 +137,7 @@ extern "C" const char *mij_strerror(int code) {
     case MIJ_EPPM: return "PPM rejected (utils/original.c read_ppm rules)";
     case MIJ_EIO: return "file I/O error";
     case MIJ_EJPEG: return "JPEG stream rejected (not a baseline 4:2:0 three-scan JFIF, or corrupt)";
+    case MIJ_EHANG: return "device-side wait outlasted its bound (corrupted device state)";
   }
   return "unknown error";
 }
@@ -300,8 +311,9 @@ struct mij_batch {
   unsigned *d_replays = nullptr;
   uint32_t *d_ffc = nullptr;      // k_emit_count: 0xFF bytes per scan chunk
   uint32_t *d_choff = nullptr;    // k_emit_scan: output offset per scan chunk
-  uint32_t *d_seam = nullptr;     // k_pack_lb -> k_seam_fix: shared first word per pack group
-  unsigned long long *d_pack_state = nullptr;  // k_pack_lb look-back words, per pack group
+  uint64_t *d_scan_base = nullptr;  // band stuffing: each scan's first byte in the band's buffer
+  uint32_t *d_seam = nullptr;     // k_pack_flat -> k_seam_fix: shared first word per pack group
+  unsigned long long *d_pack_state = nullptr;  // k_pack_flat look-back words, per pack group
   unsigned *d_pack_ticket = nullptr;
   uint16_t *d_fixmask = nullptr;  // K1 fix masks: per N-tile (tile * 3 + nt), zero between launches
   uint16_t *d_audit = nullptr;    // mij_batch_audit: per frame, block, lane group 16 straddle bits
@@ -331,8 +343,8 @@ struct mij_batch {
   std::vector<int2> h_fdims;
   uint8_t *d_frame = nullptr;
   size_t frame_cap = 0;
-  // k_pack_lb needs all-zero scan buffers; k_emit_write leaves them so, the
-  // band paths (k_scan + k_pack_lb, no emit) and the assembler's ORed words
+  // the band packing needs all-zero scan buffers; k_emit_write leaves them so, the
+  // band paths (k_scan + k_pack_flat, no emit) and the assembler's ORed words
   // before mij_assemble_end do not.  raw_dirty = frames 0..raw_dirty-1 may
   // hold words (0: every scan buffer is zero)
   int raw_dirty = 0;
@@ -346,7 +358,7 @@ struct mij_batch {
   hipEvent_t ov_k1[16] = {}, ov_done = nullptr;
   bool timing = false;
   // mij_batch_set_option (include/mijpeg.h): entropy-stage variants
-  int opt[MIJ_OPT_COUNT] = {1, 1, 1, 0, -1, 0, 1};
+  int opt[MIJ_OPT_COUNT] = {1, 1, 1, 0, -1, 0, 1, 0};
   static constexpr int HIST = 64;
   hipEvent_t evh[HIST][MIJ_NSTAGES] = {};  // per-step events while timing is on
   hipEvent_t *ev = evh[0];       // current step's events
@@ -366,7 +378,7 @@ static void batch_free(mij_batch *b) {
   void *ptrs[] = {b->d_tab, b->own_in ? b->d_in : nullptr, b->d_coef, b->d_dc, b->d_hist,
                   b->d_ehuf, b->d_raw, b->d_tok, b->d_tok0, b->d_seg_ntok, b->d_seg_bits, b->d_seg_off,
                   b->d_scan_bits, b->d_out_len, b->d_hc, b->d_out, b->d_err, b->d_replays,
-                  b->d_dcpred, b->d_bitbase, b->d_stage, b->d_fixmask, b->d_audit, b->d_ffc, b->d_choff,
+                  b->d_dcpred, b->d_bitbase, b->d_stage, b->d_fixmask, b->d_audit, b->d_ffc, b->d_choff, b->d_scan_base,
                   b->d_seam, b->d_pack_state, b->d_pack_ticket, b->d_fdims, b->d_frame, b->d_regions, b->d_pieces,
                   b->d_bound_acc};
   for (void *p : ptrs)
@@ -446,6 +458,7 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
   HIP_TRY(dalloc(&b->d_replays, 1));
   HIP_TRY(dalloc(&b->d_ffc, F * 3 * emit_chunks(g)));
   HIP_TRY(dalloc(&b->d_choff, F * 3 * emit_chunks(g)));
+  HIP_TRY(dalloc(&b->d_scan_base, F * 3));
   HIP_TRY(hipMemsetAsync(b->d_ffc, 0, sizeof(uint32_t) * F * 3 * emit_chunks(g), b->stream));  // (ff_pack adds)
   HIP_TRY(hipMemsetAsync(b->d_replays, 0, sizeof(unsigned), b->stream));
   HIP_TRY(dalloc(&b->d_fdims, F));
@@ -591,6 +604,7 @@ static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0, bool band = false
   a.bit_base = band ? b->d_bitbase : nullptr;
   a.ffc = b->d_ffc;
   a.choff = b->d_choff;
+  a.scan_base = b->d_scan_base;
   a.pack_state = b->d_pack_state;
   a.pack_ticket = b->d_pack_ticket;
   a.fdims = b->use_fdims ? b->d_fdims : nullptr;
@@ -629,6 +643,7 @@ static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0, bool band = false
     if (a.bit_base) a.bit_base += F * 4;
     a.ffc += F * 3 * emit_chunks(g);
     a.choff += F * 3 * emit_chunks(g);
+    a.scan_base += F * 3;
     a.pack_state += F * gpf;
     a.pack_ticket += F * 3;
     if (a.fdims) a.fdims += F;
@@ -837,7 +852,7 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   // Seam mode (default; MIJ_OPT_SEAM=0 for the A/B): every scan word is stored
   // whole by one pack group; a group's first word, when shared with the group
   // before it, goes to seam[] and k_seam_fix ORs it in after the packing --
-  // the scan buffers need not start zeroed (no atomics in k_pack_lb), and
+  // the scan buffers need not start zeroed (no atomics in k_pack_flat), and
   // k_emit_write does not zero them after reading.  The other paths (bands,
   // assembly) still OR onto zero: they clear what this leaves (raw_dirty).
   if (b->opt[MIJ_OPT_SEAM] && b->d_seam) {
@@ -850,7 +865,7 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
     HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->raw_dirty * b->g.raw_fs, st));
     b->raw_dirty = 0;
   }
-  // diagnostics (MIJ_PACK_TIME with the diag build): per-group phase times of k_pack_lb
+  // diagnostics (MIJ_PACK_TIME with the diag build): per-group phase times of k_pack_flat
   static const bool ptime = diag_env("MIJ_PACK_TIME", 0) != 0;
   const long long ngroups = (long long)nframes * ((b->g.nsy + PACK_SEGS - 1) / PACK_SEGS +
                                                   2 * ((b->g.nsc + PACK_SEGS - 1) / PACK_SEGS));
@@ -858,7 +873,19 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
     HIP_TRY(hipMalloc(&a.dbg, sizeof(unsigned long long) * 4 * ngroups));
     HIP_TRY(hipMemsetAsync(a.dbg, 0, sizeof(unsigned long long) * 4 * ngroups, st));
   }
-  HIP_TRY(launch_pack_lb(a, st, a.zero_pack != 0));
+  if (b->opt[MIJ_OPT_FAULT_TICKET] && f0 == 0) {
+    // fault injection (tests): frame 0's luma ticket starts past group 0
+    const int v = b->opt[MIJ_OPT_FAULT_TICKET];
+    b->opt[MIJ_OPT_FAULT_TICKET] = 0;
+    if (!a.zero_pack) {
+      HIP_TRY(hipMemsetAsync(a.pack_state, 0, sizeof(unsigned long long) * ngroups, st));
+      HIP_TRY(hipMemsetAsync(a.pack_ticket, 0, sizeof(unsigned) * 3 * nframes, st));
+    }
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)a.pack_ticket, v, 1, st));
+    HIP_TRY(launch_pack(a, st, true));
+  } else {
+    HIP_TRY(launch_pack(a, st, a.zero_pack != 0));
+  }
   if (a.seam) HIP_TRY(launch_seam_fix(a, st));
   if (ptime) {
     std::vector<unsigned long long> h(4 * ngroups);
@@ -1093,9 +1120,10 @@ extern "C" int mij_batch_set_overlap(mij_batch *b, int nsub) {
 extern "C" int mij_batch_set_option(mij_batch *b, int opt, int value) {
   if (pipe_check(b, "set_option")) return g_err;
   if (opt < 0 || opt >= MIJ_OPT_COUNT) return fail(MIJ_EINVAL, "set_option: unknown option %d", opt);
-  const bool binary = opt != MIJ_OPT_PACK_WIDE && opt != MIJ_OPT_EMIT_SLOTS;
+  const bool binary = opt != MIJ_OPT_PACK_WIDE && opt != MIJ_OPT_EMIT_SLOTS && opt != MIJ_OPT_FAULT_TICKET;
   if ((binary && value != 0 && value != 1) || (opt == MIJ_OPT_PACK_WIDE && (value < -1 || value > 1)) ||
-      (opt == MIJ_OPT_EMIT_SLOTS && (value < 0 || value > 4096)))
+      (opt == MIJ_OPT_EMIT_SLOTS && (value < 0 || value > 4096)) ||
+      (opt == MIJ_OPT_FAULT_TICKET && (value < 0 || value > 1 << 20)))
     return fail(MIJ_EINVAL, "set_option: value %d out of range for option %d", value, opt);
   if (opt == MIJ_OPT_OVERLAP_PRIO && b->stream2)
     return fail(MIJ_EINVAL, "set_option: the overlap stream exists already (set the priority before set_overlap)");
@@ -1209,7 +1237,7 @@ extern "C" unsigned long long mij_batch_token_count(mij_batch *b, int nframes) {
 
 extern "C" int mij_batch_geometry(mij_batch *b, long long *out, int n) {
   if (!b || !out) return fail(MIJ_EINVAL, "geometry: bad args");
-  // ... then k_pack_lb's LDS window (words) at this batch's quality
+  // ... then k_pack_flat's LDS window (words) at this batch's quality
   const long long win = ent_args_pack_wide(b) ? PACK_WIDE_WORDS : PACK_WORDS;
   const long long v[] = {b->g.w, b->g.h, b->g.nblk, b->g.nseg, b->g.tiles_per_frame, win};
   const int nv = (int)(sizeof(v) / sizeof(v[0]));
@@ -1244,7 +1272,7 @@ extern "C" int mij_batch_output(mij_batch *b, int frame, uint8_t *dst, size_t ca
   int err = 0;
   HIP_TRY(hipMemcpy(&n, b->d_out_len + frame, sizeof(n), hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(&err, b->d_err + frame, sizeof(err), hipMemcpyDeviceToHost));
-  if (err) return fail(MIJ_ETABLE, "frame %d: Huffman table construction failed", frame);
+  if (err) return mij_frame_fail(err, "frame", frame);
   if (len) *len = (size_t)n;
   if (dst) {
     if (cap < n) return fail(MIJ_ENOSPC, "output: need %llu bytes", (unsigned long long)n);
@@ -1404,7 +1432,7 @@ extern "C" void init_huffman(int16_t *Y, int16_t *Cb, int16_t *Cr, area_t dims,
     fail(MIJ_EHIP, "init_huffman: device copy failed");
     return;
   }
-  if (err) fail(MIJ_ETABLE, "init_huffman: table construction outside defined behaviour");
+  if (err) mij_frame_fail(err, "init_huffman: frame", 0);
   memcpy(&Luma[0], &t[0], sizeof(HuffCode));
   memcpy(&Luma[1], &t[1], sizeof(HuffCode));
   memcpy(&Chroma[0], &t[2], sizeof(HuffCode));
@@ -1502,7 +1530,7 @@ extern "C" int mij_encode_regions(const uint8_t *bgr, int stride_px, int frame_h
   std::vector<int> err(n);
   HIP_TRY(hipMemcpy(err.data(), b->d_err, sizeof(int) * n, hipMemcpyDeviceToHost));
   for (int i = 0; i < n; i++)
-    if (err[i]) return fail(MIJ_ETABLE, "mij_encode_regions: region %d: Huffman table construction failed", i);
+    if (err[i]) return mij_frame_fail(err[i], "mij_encode_regions: region", i);
   size_t off = 0;
   for (int i = 0; i < n; i++) {
     lens[i] = len[i];
@@ -1647,7 +1675,7 @@ extern "C" int mij_band_pack_async(mij_batch *b, int n, uint64_t *d_bits) {
   if (b->raw_dirty) HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->raw_dirty * b->g.raw_fs, b->stream));
   b->raw_dirty = n;
   EntArgs a = ent_args(b, n);
-  HIP_TRY(launch_pack_lb(a, b->stream, true));  // (k_band_bound zeroed its state)
+  HIP_TRY(launch_pack(a, b->stream, true));  // (k_band_bound zeroed its state)
   HIP_TRY(launch_band_count((const unsigned long long *)b->d_scan_bits, n, b->d_pieces,
                             (unsigned long long *)d_bits, b->stream));
   b->band_async_n = n;
@@ -1712,6 +1740,9 @@ extern "C" int mij_band_stuff_async(mij_batch *b, int n, const uint64_t *d_allbi
   a.ff_pack = 0;
   HIP_TRY(launch_band_stuff(a, (const unsigned long long *)d_allbits, world, rank, (unsigned long long *)d_rec,
                             (unsigned long long *)d_total, d_dst, (unsigned long long)cap, b->stream));
+  // the heads' shifts k_band_stuff_prep kept in the bit bases: reset, so no
+  // band call after this one finds them
+  HIP_TRY(hipMemsetAsync(b->d_bitbase, 0, sizeof(uint32_t) * n * 4, b->stream));
   b->band_async_n = 0;  // the scan words are consumed (zeroed)
   if (n >= b->raw_dirty) b->raw_dirty = 0;
   return MIJ_OK;
@@ -1741,7 +1772,7 @@ extern "C" int mij_batch_build_tables(mij_batch *b, int n, const uint32_t *hist)
   HIP_TRY(hipMemcpyAsync(err.data(), b->d_err, sizeof(int) * n, hipMemcpyDeviceToHost, b->stream));
   HIP_TRY(hipStreamSynchronize(b->stream));
   for (int f = 0; f < n; f++)
-    if (err[f]) return fail(MIJ_ETABLE, "frame %d: Huffman table construction failed", f);
+    if (err[f]) return mij_frame_fail(err[f], "frame", f);
   return MIJ_OK;
 }
 
@@ -1759,7 +1790,7 @@ extern "C" int mij_band_tables(mij_batch *b, int n, const uint32_t *hist, unsign
   HIP_TRY(hipMemcpyAsync(err.data(), b->d_err, sizeof(int) * n, hipMemcpyDeviceToHost, b->stream));
   HIP_TRY(hipStreamSynchronize(b->stream));
   for (int f = 0; f < n; f++)
-    if (err[f]) return fail(MIJ_ETABLE, "band frame %d: Huffman table construction failed", f);
+    if (err[f]) return mij_frame_fail(err[f], "band frame", f);
   return MIJ_OK;
 }
 
@@ -1773,11 +1804,11 @@ extern "C" int mij_band_pack(mij_batch *b, int n, const unsigned long long *bit_
   HIP_TRY(hipMemcpyAsync(b->d_bitbase, base.data(), sizeof(uint32_t) * n * 4, hipMemcpyHostToDevice,
                          b->stream));
   EntArgs a = ent_args(b, n, 0, true);
-  // k_pack_lb needs all-zero scan buffers: mij_band_words_all moves the band
+  // the band packing needs all-zero scan buffers: mij_band_words_all moves the band
   // words out and zeroes them; a band packed but never moved leaves them dirty
   if (b->raw_dirty) HIP_TRY(hipMemsetAsync(b->d_raw, 0, sizeof(uint32_t) * b->raw_dirty * b->g.raw_fs, b->stream));
   b->raw_dirty = n;
-  HIP_TRY(launch_pack_lb(a, b->stream));
+  HIP_TRY(launch_pack(a, b->stream));
   std::vector<unsigned long long> tot((size_t)n * 3);
   HIP_TRY(hipMemcpyAsync(tot.data(), b->d_scan_bits, sizeof(uint64_t) * n * 3,
                          hipMemcpyDeviceToHost, b->stream));

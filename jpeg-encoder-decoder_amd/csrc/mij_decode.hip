@@ -62,10 +62,7 @@ struct DecJob {
 // chunk c of a scan covers bits [c*CHUNK, (c+1)*CHUNK): a symbol belongs to
 // the chunk its first bit lies in.  512: measured against 1024 / 2048 / 4096
 // on 256 config-3 streams, 16.3 / 17.7 / 21.1 / 23.9 ms per decode call.
-#ifndef MIJ_DEC_CHUNK
-#define MIJ_DEC_CHUNK 512
-#endif
-constexpr int CHUNK = MIJ_DEC_CHUNK;
+constexpr int CHUNK = 512;
 
 // MSB-first bit window over an unstuffed, 8-byte aligned, zero-padded scan
 struct Bits {

@@ -9,6 +9,9 @@
 // error state of the C ABI (mij_last_error): set and print like the API does
 int mij_fail(int code, const char *fmt, ...);
 void mij_clear_error();
+// a frame's device error code (mij_internal.h FERR_*) as the C ABI's error,
+// naming `what` and the frame
+int mij_frame_fail(int ferr, const char *what, int frame);
 
 // asynchronous transfers on the batch's stream (no synchronisation)
 int mij_batch_upload_async(mij_batch *b, const uint8_t *host, int nframes);

@@ -20,6 +20,15 @@ constexpr int LDS_WAVE = 48 * LDS_BLK;  // 32 Y + 16 chroma blocks per wave
 constexpr int LUT_WORDS = 1024;      // 2^15 bits per colour-exception table
 constexpr int DCTIE_WORDS = 33;      // DC tie bits for K = 0..1055 (|S| <= 8192 -> K <= 1024)
 
+// ---- per-frame device error codes (EntArgs::err) ---------------------------
+constexpr int FERR_TABLE = 1;     // Huffman construction outside the reference's defined behaviour
+constexpr int FERR_OVERFLOW = 2;  // bits past a scan buffer (tokens no K1 wrote): nothing written
+constexpr int FERR_ASSEMBLY = 3;  // band assembly: a piece outside its buffer
+constexpr int FERR_SPIN = 4;      // a device-side wait outlasted SPIN_TICKS, or a stale pack ticket
+// bound of every device-side wait (s_memrealtime ticks, 100 MHz: 100 ms); the
+// waits are microseconds long when the state they wait on is intact
+constexpr unsigned long long SPIN_TICKS = 10000000ull;
+
 // ---- entropy stage: segments ---------------------------------------------
 // A segment is the run of blocks one K1 N-tile covers in a component's scan
 // order: 16 luma blocks of a block row, or 8 Cb / 8 Cr blocks of an MCU row.
@@ -28,26 +37,15 @@ constexpr int DCTIE_WORDS = 33;      // DC tie bits for K = 0..1055 (|S| <= 8192
 constexpr int MAX_BLOCK_TOK = 65;                 // DC + 63 AC + EOB
 constexpr int SEG_TOK = 16 * MAX_BLOCK_TOK;       // 1040 tokens per segment slot
 constexpr int SEG_PER_WG = 64;                    // k_seg_bits segments per workgroup
-#ifndef MIJ_PACK_SEGS
-#define MIJ_PACK_SEGS 64
-#endif
-constexpr int PACK_SEGS = MIJ_PACK_SEGS;          // segments per k_pack workgroup
+constexpr int PACK_SEGS = 64;          // segments per k_pack workgroup
 constexpr int MAX_BLOCK_BITS = 1729;              // 28 DC + 63 * 27 AC bits
 // k_pack assembles a group in LDS windows of PACK_WORDS words; a group wider
 // than one window (only near worst-case entropy) is packed in several passes.
-#ifndef MIJ_PACK_WORDS
-#define MIJ_PACK_WORDS 4096
-#endif
-constexpr int PACK_WORDS = MIJ_PACK_WORDS;
+constexpr int PACK_WORDS = 4096;
 // the window of the high-quality variant (EntArgs::pack_wide, Q >= 85)
-#ifndef MIJ_PACK_WIDE_WORDS
-#define MIJ_PACK_WIDE_WORDS 6144
-#endif
-constexpr int PACK_WIDE_WORDS = MIJ_PACK_WIDE_WORDS;
+constexpr int PACK_WIDE_WORDS = 6144;
 static_assert(PACK_WIDE_WORDS > PACK_WORDS, "the wide pack window must be wider than the default one");
 constexpr int PACK_WIDE_MIN_Q = 85;  // qualities from which the wide window is launched
-// k_pack_lb: tokens per lane loaded in one batch (16 lanes per segment)
-constexpr int PACK_BATCH = 16;
 // JFIF assembly: scans are written in EMIT_CH-byte chunks by EntArgs::
 // emit_slots workgroups per frame, EMIT_SLOTS when unset (round 2's A/B per scan on config 3,
 // emit = count + scan + write: 8 slots 0.260 ms, 16 0.232, 32 0.243,
@@ -55,14 +53,8 @@ constexpr int PACK_BATCH = 16;
 // (seam mode, chunks dealt over the frame's scans, profiles/r03/seam/
 // emit_ab.txt): 8 KB chunks 0.190 ms at Q=50 and 0.549 at Q=90 against
 // 0.210 / 0.639 with 4 KB; 16 KB chunks 0.29 / 0.80.
-#ifndef MIJ_EMIT_CH
-#define MIJ_EMIT_CH 8192
-#endif
-constexpr int EMIT_CH = MIJ_EMIT_CH;
-#ifndef MIJ_EMIT_SLOTS
-#define MIJ_EMIT_SLOTS 192
-#endif
-constexpr int EMIT_SLOTS = MIJ_EMIT_SLOTS;
+constexpr int EMIT_CH = 8192;
+constexpr int EMIT_SLOTS = 192;
 
 // Layout-identical to the reference huff_code (include/structs.h:5-13).
 struct HuffCode {
@@ -212,20 +204,22 @@ struct EntArgs {
   const int16_t *dc_pred;   // DC predictor of each component's first block (null: 0)
   const uint32_t *bit_base; // bit offset of each scan inside its first word (null: 0)
   uint32_t *ffc;            // per frame [3][emit_chunks]: 0xFF bytes per EMIT_CH chunk
-  uint32_t *choff;          // per frame [3][emit_chunks]: output offset of each chunk
-  unsigned long long *pack_state;  // k_pack_lb: per pack group, flag << 62 | bits
-  unsigned int *pack_ticket;       // k_pack_lb: next group to claim, per scan
+  uint32_t *choff;          // per frame [3][emit_chunks]: output offset of each chunk (inside
+                            // its frame; band stuffing: inside its scan, see scan_base)
+  uint64_t *scan_base;      // per frame [3]: band stuffing, a scan's first byte in the band's buffer
+  unsigned long long *pack_state;  // k_pack_flat: per pack group, flag << 62 | bits
+  unsigned int *pack_ticket;       // k_pack_flat: next group to claim, per scan
   unsigned long long *dbg;         // diagnostics only (MIJ_PACK_TIME, diag build)
   const int2 *fdims;               // per-frame image size (region batches), null: the canvas
   uint32_t *seam;                  // per pack group: its first word when shared with the group
                                    // before it (null: edge words OR-ed onto all-zero scan buffers;
                                    // set: k_seam_fix ORs them in, nothing needs zeroed buffers)
   int emit_slots;                  // k_emit_count / k_emit_write workgroups per frame (0: EMIT_SLOTS)
-  int pack_wide;                   // k_pack_lb with a 2 * PACK_WORDS window (high quality)
-  int zero_pack;                   // k_tables_1w also zeroes k_pack_lb's look-back words and tickets
+  int pack_wide;                   // k_pack_flat with a 2 * PACK_WORDS window (high quality)
+  int zero_pack;                   // k_tables_1w also zeroes k_pack_flat's look-back words and tickets
   int seg_dc;                      // k_tables: compute the segment-first DC tokens first (k_seg_dc)
   int tab_dc_only;                 // k_tables_1w: the DC tables only (k_segdc_actab built the AC ones)
-  int ff_pack;                     // seam mode: k_pack_lb / k_seam_fix count the 0xFF bytes of every
+  int ff_pack;                     // seam mode: k_pack_flat / k_seam_fix count the 0xFF bytes of every
                                    // EMIT_CH chunk into ffc as they store (k_emit_count not run;
                                    // k_emit_write leaves the counts zeroed)
 };

@@ -13,7 +13,7 @@
 //   k_ehuf_struct  code tables from caller-owned huff_code structs
 //   k_seg_bits     bits per segment
 //   k_scan         per-scan offsets of each segment
-//   k_pack_lb      segment bits + look-back offsets + bit packing (:434-502)
+//   k_pack_flat    segment bits + look-back offsets + bit packing (:434-502)
 //   k_emit         JFIF assembly + 0xFF stuffing + pad quirks (:383-432,
 //                  :504-644)
 //
@@ -168,37 +168,6 @@ __device__ __forceinline__ int dc_tie(int d, const uint32_t *bits) {
   int k = (d ^ s) - s;
   k -= (int)((bits[k >> 5] >> (k & 31)) & 1u);
   return (k ^ s) - s;
-}
-
-// One AC coefficient replayed exactly as encoder.c:87-109 computes it
-// (column pass summed from 0 in y order, row pass in x order, FP64, no FMA).
-// C = the 64 cosines (LDS), blk = the block's 64 staged pixels (LDS), zz =
-// the zigzag table (LDS: a global load here would wait, vmcnt(0), for every
-// token store and the next tile's DMA still in flight -- it made the replays
-// 10x dearer).  The eight column sums are independent chains, evaluated side
-// by side.
-__device__ __forceinline__ int ac_exact(const uint8_t *blk, int z, int q, const double *C, const uint8_t *zz) {
-  const int rz = zz[z];
-  const int v = rz >> 3, u = rz & 7;
-  double inner[8];
-#pragma unroll
-  for (int x = 0; x < 8; x++) inner[x] = 0.0;
-#pragma unroll 2
-  for (int y = 0; y < 8; y++) {
-    const double cv = C[y * 8 + v];
-    const uint64_t row = *(const uint64_t *)(blk + y * 8);
-#pragma unroll
-    for (int x = 0; x < 8; x++)
-      inner[x] = __dadd_rn(inner[x], __dmul_rn((double)((int)((row >> (8 * x)) & 255) - 128), cv));
-  }
-  double freq = 0.0;
-#pragma unroll
-  for (int x = 0; x < 8; x++) freq = __dadd_rn(freq, __dmul_rn(inner[x], C[x * 8 + u]));
-  if (u == 0) freq = __dmul_rn(freq, SQRT1_2);
-  if (v == 0) freq = __dmul_rn(freq, SQRT1_2);
-  freq = __dmul_rn(freq, 0.25);
-  const int t = (int)__ddiv_rn(freq, (double)q);
-  return t < -2048 ? -2048 : (t > 2047 ? 2047 : t);
 }
 
 // ===========================================================================
@@ -568,23 +537,9 @@ __device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int
 // every token kind (DC: symbol = class <= 11; EOB: symbol 0x00).
 constexpr uint32_t TOK_AC = 1u << 10;
 // the padding token after a segment's last one (AC symbol 0xFF, which no
-// token carries: magnitudes stop at class 11): k_pack_lb's code table holds
+// token carries: magnitudes stop at class 11): the packing's code table holds
 // 0 for it -- no bits, no ZRLs
 constexpr uint32_t LB_NOTOK = TOK_AC | 0xFFu;
-// software pipelining of K1's N-tiles, token variants (see the N-tile loop;
-// measured: token K1 3.504 -> 3.441 and 3.514 -> 3.459 ms, two A/B rounds on
-// one box; the coefficient variant spills at 168 VGPRs with it, 3.12 -> 3.18)
-#ifndef MIJ_K1_PIPE
-#define MIJ_K1_PIPE 1
-#endif
-#ifndef MIJ_K1_AREL
-#define MIJ_K1_AREL 0
-#endif
-// N-tile of the token K1 before whose stores the next tile's DMA is awaited
-// (A/B: 0, 1 and 2 measured equal, 3.36-3.39 ms)
-#ifndef MIJ_K1_DMAWAIT_NT
-#define MIJ_K1_DMAWAIT_NT 0
-#endif
 
 // One N-tile of coefficients -> compacted token stream of its segment(s).
 // o[k] = zigzag coefficient 16g+k of block bcol (DC raw in o[0] of g == 0,
@@ -595,19 +550,12 @@ constexpr uint32_t LB_NOTOK = TOK_AC | 0xFFu;
 // a segment's first block depends on the previous segment: with first_pred
 // the caller supplies that block's predecessor DC (pred0), otherwise (token
 // variant fed from pixels) it is left for k_seg_dc.
-// token i of a frame's streams (MIJ_K1_TOKOFF: a wave-uniform frame base and
-// a 32-bit byte offset, so the store takes the SGPR-base form instead of a
-// 64-bit address add per token; A/B on config 3, 3 rounds: K1 3.280 -> 3.262
-// ms, profiles/r03/probe/k1_tokoff_ab.txt)
-#ifndef MIJ_K1_TOKOFF
-#define MIJ_K1_TOKOFF 1
-#endif
+// token i of a frame's streams: a wave-uniform frame base and a 32-bit byte
+// offset, so the store takes the SGPR-base form instead of a 64-bit address
+// add per token (A/B on config 3, 3 rounds: K1 3.280 -> 3.262 ms,
+// profiles/r03/probe/k1_tokoff_ab.txt)
 __device__ __forceinline__ uint32_t &tok_at(uint32_t *base, uint32_t i) {
-#if MIJ_K1_TOKOFF
   return *(uint32_t *)((char *)base + (i << 2));
-#else
-  return base[i];
-#endif
 }
 __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g, int bcol,
                                             bool valid, bool chroma, bool dc_diffed,
@@ -678,7 +626,7 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
     if (pos == (chroma ? 7 : 15)) {
       *segcnt = incl;
       // the segment's token count padded to a multiple of 4 with LB_NOTOK
-      // (k_pack_lb decodes 4 tokens per lane: a lane's slots are then all
+      // (k_pack_flat decodes 4-token chunks: a lane's slots are then all
       // tokens or all padding, and no token needs a mask)
       for (uint32_t i = incl; i & 3u; i++) tok_at(segtok, segoff + i) = LB_NOTOK;
     }
@@ -783,28 +731,11 @@ constexpr int k1_base(int mode) { return mode & ~(K1M_RGB | K1M_REGIONS | K1M_AU
 // per-wave token staging and run 4-wave workgroups, two per CU.
 template <int MODE>
 constexpr bool k1_wide() { return k1_base(MODE) == K1M_COEF_OUT || k1_base(MODE) == K1M_TOK_OUT; }
-#ifndef MIJ_K1_TOK_WAVES
-#define MIJ_K1_TOK_WAVES 12
-#endif
 template <int MODE>
 constexpr int k1_waves() {
-  return k1_base(MODE) == K1M_TOK_OUT ? MIJ_K1_TOK_WAVES : (k1_wide<MODE>() ? 12 : 4);
+  return k1_wide<MODE>() ? 12 : 4;
 }
 
-// the MFMA digit chain's shifts as 64-bit pair shifts (config 3, two A/B
-// rounds on one box: token K1 3.15 -> 3.08 ms at Q=50, 4.74 -> 4.73 at Q=90;
-// v_lshlrev_b64 issues in the 4.5 cycles of a 32-bit left shift,
-// profiles/r04/probe/valu_rate5.txt)
-#ifndef MIJ_K1_SHL64
-#define MIJ_K1_SHL64 1
-#endif
-// chroma all-AC-zero fast path of the token K1 (A/B knob)
-#ifndef MIJ_K1_CZ
-#define MIJ_K1_CZ 1
-#endif
-#ifndef MIJ_K1_COOP_REPLAY
-#define MIJ_K1_COOP_REPLAY 1
-#endif
 template <int MODE>
 __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) void k_mcu_dct(K1Args a) {
   constexpr bool PIX = !(MODE & K1M_COEF_IN);
@@ -887,7 +818,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   const int g = lane >> 4, bcol = lane & 15;
   const int c4 = lane & 31, pr = lane >> 5;
   const int q_dc[2] = {T->qint[0][0], T->qint[1][0]};
-  const bool cz_on = PIX && !AUDIT && MIJ_K1_CZ && T->cz_on;  // wave-uniform
+  const bool cz_on = PIX && !AUDIT && T->cz_on;  // wave-uniform
   const Geom &G = a.g;
   const int bw = G.w >> 3, mw = G.w >> 4;
   const int ntiles = a.nframes * G.tiles_per_frame;
@@ -1018,7 +949,6 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
           }
 #endif
           const v4i Fv = {F.x, F.y, F.z, F.w};
-#if MIJ_K1_SHL64
           // The digit shifts two accumulators at a time (v_lshlrev_b64 of
           // the pairs r = 0|1 and 2|3): the low element of a pair carries a
           // bias of 2^17 from the first digit on, which keeps it inside
@@ -1035,13 +965,9 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
             typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
             c = __builtin_bit_cast(v4i, __builtin_bit_cast(u64x2, acc[m]) << 7);
           }
-#else
-          const v4i c = d == 0 ? v4i{0, 0, 0, 0} : acc[m] << 7;
-#endif
           acc[m] = (kflags & K1F_NO_MFMA) ? c + Fv + Bf
                                           : __builtin_amdgcn_mfma_i32_16x16x64_i8(Fv, Bf, c, 0, 0, 0);
         }
-#if MIJ_K1_SHL64
         if (d == 2) {
 #pragma unroll
           for (int m = 0; m < 4; m++) {
@@ -1049,7 +975,6 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
             acc[m][2] ^= (int)0x80000000u;
           }
         }
-#endif
       };
       // N-tile nt: the error bound of its N (lanes of a block: its L1) and
       // the three digits
@@ -1192,10 +1117,12 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
         }
       };
       if (PIX && do_dct) {
-        // MIJ_K1_PIPE: N-tile nt + 1's MFMA chain is issued before N-tile nt
-        // is quantised, so the wave's own quantisation covers the chain's
-        // latency (two accumulator sets live)
-        constexpr bool PIPE = MIJ_K1_PIPE && TOK;
+        // token variants: N-tile nt + 1's MFMA chain is issued before N-tile
+        // nt is quantised, so the wave's own quantisation covers the chain's
+        // latency (two accumulator sets live; measured: token K1 3.504 ->
+        // 3.441 and 3.514 -> 3.459 ms, two A/B rounds on one box; the
+        // coefficient variant spills at 168 VGPRs with it, 3.12 -> 3.18)
+        constexpr bool PIPE = TOK;
         v4i accs[PIPE ? 2 : 1][4];
         float lcs[PIPE ? 2 : 1];  // per block: error bound of N in N units
         if (PIPE) dct_ntile(0, accs[0], lcs[0]);
@@ -1206,9 +1133,6 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
           if (!PIPE) {
             dct_ntile(nt, accs[0], lcs[0]);
           } else if (nt + 1 < 3) {
-#if MIJ_K1_AREL
-            asm volatile("" ::: "memory");  // A fragments re-read from LDS per N-tile
-#endif
             dct_ntile(nt + 1, accs[PIPE ? (cur ^ 1) : 0], lcs[PIPE ? (cur ^ 1) : 0]);
           }
           v4i(&acc)[4] = accs[cur];
@@ -1333,13 +1257,13 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
             // recompute them in FP64 exactly as encoder.c:87-109
             uint32_t mm = straddle_mask();
             nrep += (uint32_t)__popc(mm);
-            if constexpr (TOK && MIJ_K1_COOP_REPLAY) {
+            if constexpr (TOK) {
               // The wave's straddles listed (lane << 4 | k, in the wave's
               // token staging, free until this N-tile's tokens) and replayed
               // 8 at a time: lane x of an 8-lane group sums column x of its
               // block (the reference's inner loop, y order), the group's 8
               // column sums meet by shuffles and every lane of it folds them
-              // in x order.  The FP64 operations are ac_exact's, in its order;
+              // in x order.  The FP64 operations are encoder.c:87-109's, in its order
               // a lane with several straddles no longer replays them one
               // after another while the wave waits.
               const int c = __popc(mm);
@@ -1396,21 +1320,12 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
                 }
                 wave_lds_sync();
               }
-            } else {
-              const uint8_t *Pb = L + (nt * 16 + bcol) * LDS_BLK;
-              while (mm) {
-                const int k = __ffs(mm) - 1;
-                mm &= mm - 1u;
-                const int z = 16 * g + k;
-                const int v = ac_exact(Pb, z, s_qint[comp][z], s_cos, s_zz);
-#pragma unroll
-                for (int j = 0; j < 16; j++) o[j] = j == k ? v : o[j];
-              }
             }
           }
           // token variants: the next tile's DMA has landed before the first
-          // store (their VMEM count per tile varies)
-          if (nt == MIJ_K1_DMAWAIT_NT && !DEFER && !(kflags & K1F_NO_DMAWAIT)) dma_wait();
+          // store (their VMEM count per tile varies; waiting before N-tile
+          // 0, 1 or 2 measured equal, 3.36-3.39 ms)
+          if (nt == 0 && !DEFER && !(kflags & K1F_NO_DMAWAIT)) dma_wait();
           K1_PHASE(3);
           finish(nt, o, false);
           K1_PHASE(4);
@@ -1634,38 +1549,7 @@ struct SegDc {
   int comp, dc, pred;
   bool ok;
 };
-#ifndef MIJ_SEGDC_BF
-#define MIJ_SEGDC_BF 0
-#endif
-#ifndef MIJ_SEGDC_U
-#define MIJ_SEGDC_U 32
-#endif
-#if MIJ_SEGDC_BF
-// (branch-free: seg_info's cases as selects and both loads from clamped
-// addresses, so a lane's U segments issue their loads back to back)
-__device__ __forceinline__ SegDc seg_dc_load(const EntArgs &a, const FGeom &fg, int f, int s) {
-  const Geom &G = a.g;
-  SegDc r;
-  const bool y = s < G.nsy;
-  const int c = s - G.nsy;
-  r.comp = y ? 0 : (c >= G.nsc ? 2 : 1);
-  const int local = y ? s : (r.comp == 1 ? c : c - G.nsc);
-  const int cstart = y ? 0 : (r.comp == 1 ? fg.nY : fg.nY + fg.nC);
-  const int row = (int)div_by((uint32_t)max(local, 0), G.tx_m, G.tx_s), tx = local - row * G.tiles_x;
-  const int first = cstart + row * (y ? fg.bw : fg.mw) + tx * (y ? 16 : 8);
-  r.ok = s >= 0 && s < G.nseg && row < (y ? 2 * fg.rows : fg.rows) && tx < fg.tiles_x;
-  const long long fb = (long long)f * G.nblk;
-  const int at = r.ok ? first : 0;
-  const int dc = (int)a.dc[fb + at];
-  const int prev = (int)a.dc[fb + max(at - 1, 0)];
-  // a component's first block is predicted from 0 (encoder.c:168-177), or
-  // from the previous band's last DC when the frame is split into bands
-  const int p0 = a.dc_pred ? (int)a.dc_pred[f * 4 + r.comp] : 0;
-  r.dc = r.ok ? dc : 0;
-  r.pred = !r.ok ? 0 : (first == cstart ? p0 : prev);
-  return r;
-}
-#else
+constexpr int SEGDC_U = 32;  // segments in flight per lane in k_tables' DC waves
 __device__ __forceinline__ SegDc seg_dc_load(const EntArgs &a, const FGeom &fg, int f, int s) {
   SegDc r;
   int first, cstart, local;
@@ -1680,7 +1564,6 @@ __device__ __forceinline__ SegDc seg_dc_load(const EntArgs &a, const FGeom &fg, 
   }
   return r;
 }
-#endif
 // The class counts go to hs[(luma ? 0 : 16) + class][lane & 31]: 32 copies
 // of every counter, so a wave's 64 atomics meet at most in pairs (one
 // counter per class took every lane of a wave with the same class in turn).
@@ -1695,18 +1578,17 @@ __device__ __forceinline__ void seg_dc_store(const EntArgs &a, int f, int s, con
   atomicAdd(&hs[((r.comp ? 16 : 0) + cls) * 32 + (lane & 31)], 1u);
 }
 
-#ifndef MIJ_SEGDC_WG
-#define MIJ_SEGDC_WG 256
-#endif
-// (MIJ_SEGDC_WG 64: one-wave workgroups, which fit beside a running 10-wave
-// K1 -- 256-thread ones wait for it to end; profiles/r03/overlap_trace.txt)
+constexpr int SEGDC_WG = 256;
+// (64-thread workgroups fit beside a running 10-wave K1 -- 256-thread ones
+// wait for it to end; profiles/r03/overlap_trace.txt; the 12-wave K1 leaves
+// room for neither)
 // one workgroup's share (workgroup b of the launch's segment DCs; hs: 32 x
 // 32 words of LDS)
 __device__ __forceinline__ void seg_dc_block(const EntArgs &a, int b, uint32_t *hs) {
-  const int per = (a.g.nseg + MIJ_SEGDC_WG - 1) / MIJ_SEGDC_WG;
+  const int per = (a.g.nseg + SEGDC_WG - 1) / SEGDC_WG;
   const int f = b / per;
-  const int s = (b - f * per) * MIJ_SEGDC_WG + threadIdx.x;
-  for (int i = threadIdx.x; i < 32 * 32; i += MIJ_SEGDC_WG) hs[i] = 0;
+  const int s = (b - f * per) * SEGDC_WG + threadIdx.x;
+  for (int i = threadIdx.x; i < 32 * 32; i += SEGDC_WG) hs[i] = 0;
   __syncthreads();
   if (s < a.g.nseg) seg_dc_store(a, f, s, seg_dc_load(a, frame_geom(a.g, a.fdims, f), f, s), hs, threadIdx.x & 63);
   __syncthreads();
@@ -1718,7 +1600,7 @@ __device__ __forceinline__ void seg_dc_block(const EntArgs &a, int b, uint32_t *
   }
 }
 
-__global__ __launch_bounds__(MIJ_SEGDC_WG) void k_seg_dc(EntArgs a) {
+__global__ __launch_bounds__(SEGDC_WG) void k_seg_dc(EntArgs a) {
   __shared__ uint32_t hs[32 * 32];
   seg_dc_block(a, blockIdx.x, hs);
 }
@@ -1973,10 +1855,7 @@ __device__ __forceinline__ void build_table_wave2(const uint32_t *hist, const ui
   bool wide = false;
 #pragma unroll
   for (int r = 0; r < 4; r++) wide |= f[r] >= (1u << 23);
-#ifndef MIJ_TAB_SORT32
-#define MIJ_TAB_SORT32 1
-#endif
-  if (!MIJ_TAB_SORT32 || __ballot(wide)) {
+  if (__ballot(wide)) {
 #pragma unroll
     for (int r = 0; r < 4; r++)
       k[r] = f[r] ? ((unsigned long long)f[r] << 32) | ((unsigned long long)(256 - (lane + 64 * r)) << 19) | (1ull << 10)
@@ -2282,7 +2161,7 @@ __device__ __forceinline__ void build_table_wave2(const uint32_t *hist, const ui
     }
   }
   if (__ballot(bad)) {
-    if (lane == 0) *err = 1;
+    if (lane == 0) *err = FERR_TABLE;
     return;
   }
   // code_len_freq (all 257 symbols) and counts of 0..255, length L in lane L;
@@ -2330,7 +2209,7 @@ __device__ __forceinline__ void build_table_wave2(const uint32_t *hist, const ui
   const int n = nlc ? nlc - 1 : 0;  // symbols 0..255 with a code
   if (!fail && (__builtin_amdgcn_readlane(cum, 16) != n || n >= 255)) fail = true;
   if (fail) {
-    if (lane == 0) *err = 1;
+    if (lane == 0) *err = FERR_TABLE;
     return;
   }
   // :280-300 canonical first codes, length L in lane L
@@ -2417,7 +2296,7 @@ __global__ __launch_bounds__(256) void k_tables(EntArgs a) {
     const FGeom fg = frame_geom(a.g, a.fdims, f);
     const int half = (a.g.nseg + 1) / 2;
     const int sb = t == 0 ? 0 : half, se = t == 0 ? half : a.g.nseg;
-    constexpr int U = MIJ_SEGDC_U;  // segments in flight per lane
+    constexpr int U = SEGDC_U;  // segments in flight per lane
     for (int s0 = sb + lane; s0 < se; s0 += 64 * U) {
       SegDc r[U];
 #pragma unroll
@@ -2434,8 +2313,15 @@ __global__ __launch_bounds__(256) void k_tables(EntArgs a) {
     // both DC waves' counts are in before either builds its table
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) atomicAdd(&s_done, 1);
-    while (__hip_atomic_load(&s_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 2)
+    // (the other DC wave of this workgroup; bounded like every device wait)
+    const unsigned long long t_wait = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(&s_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 2) {
+      if (__builtin_amdgcn_s_memrealtime() - t_wait > SPIN_TICKS) {
+        if (lane == 0) a.err[f] = FERR_SPIN;
+        break;
+      }
       __builtin_amdgcn_s_sleep(2);
+    }
     // this wave's component: the 32 copies of its 16 counters summed
     if (lane < 16) {
       const int key = (t >> 1) * 16 + lane;
@@ -2460,7 +2346,7 @@ __global__ __launch_bounds__(64) void k_tables_1w(EntArgs a) {
   __shared__ TabScratch2 S;
   const int nt = a.tab_dc_only ? 2 : 4, lane = threadIdx.x;
   const int f = blockIdx.x / nt, idx = blockIdx.x - f * nt, t = a.tab_dc_only ? 2 * idx : idx;
-  if (a.zero_pack) {  // (k_pack_lb runs next: its state, zeroed here instead of two fills)
+  if (a.zero_pack) {  // (k_pack_flat runs next: its state, zeroed here instead of two fills)
     const long long gpf = (a.g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((a.g.nsc + PACK_SEGS - 1) / PACK_SEGS);
     for (long long i = 64 * idx + lane; i < gpf; i += 64 * nt) a.pack_state[f * gpf + i] = 0;
     if (t == 0 && lane < 3) a.pack_ticket[f * 3 + lane] = 0;
@@ -2480,7 +2366,7 @@ __global__ __launch_bounds__(64) void k_tables_1w(EntArgs a) {
 // luma AC table's merge (the long pole of the table stage) runs beside the
 // segment DCs, and k_tables_1w builds only the DC tables after
 // (EntArgs::tab_dc_only).  One wave of an AC workgroup works.
-__global__ __launch_bounds__(MIJ_SEGDC_WG) void k_segdc_actab(EntArgs a) {
+__global__ __launch_bounds__(SEGDC_WG) void k_segdc_actab(EntArgs a) {
   __shared__ TabScratch2 S;
   __shared__ uint32_t hs[32 * 32];
   const int nac = 2 * a.nframes;
@@ -2553,7 +2439,7 @@ __global__ __launch_bounds__(256) void k_seg_bits(EntArgs a) {
 // ===========================================================================
 // k_scan: per scan (frame, component) exclusive scan of segment bits; zeroes
 // the first/last word of every pack group (shared with neighbour groups and
-// OR-combined by k_pack_lb).  One wave per scan.
+// OR-combined by the band packing).  One wave per scan.
 // ===========================================================================
 __global__ void k_scan(EntArgs a) {
   const int sid = blockIdx.x;  // frame * 3 + comp
@@ -2581,7 +2467,7 @@ __global__ void k_scan(EntArgs a) {
       // never write out of bounds)
       const unsigned long long wl = excl >> 5, wh = (excl + v - 1) >> 5;
       if (wh >= (unsigned long long)a.g.raw_words[comp]) {
-        a.err[f] = 2;
+        a.err[f] = FERR_OVERFLOW;
       } else {
         if (i % PACK_SEGS == 0) raw[wl] = 0;
         if (i % PACK_SEGS == PACK_SEGS - 1 || i == ns - 1) raw[wh] = 0;
@@ -2593,7 +2479,8 @@ __global__ void k_scan(EntArgs a) {
 }
 
 // ===========================================================================
-// Bit placement helpers of k_pack_lb's window paths (big-endian bit order).
+// Bit placement helpers of k_pack_flat's token-by-token and window paths
+// (big-endian bit order).
 // ===========================================================================
 __device__ __forceinline__ void put_bits(uint32_t *buf, uint32_t pos, uint32_t val, int len) {
   // len in 1..28, val < 2^len
@@ -2620,59 +2507,12 @@ __device__ __forceinline__ void put_bits_window(uint32_t *buf, uint32_t pos, uin
   }
 }
 
-// ===========================================================================
-// k_pack_lb: segment bits, scan offsets and bit packing in one pass.  Each
-// workgroup takes the next pack group of PACK_SEGS segments of one scan (a
-// ticket keeps groups claimed in scan order), merges each lane's tokens into
-// bit strings and sums its segments' bits, publishes the group's aggregate,
-// packs the group into an LDS window relative to its own first bit (16 lanes
-// -- a DPP row -- per segment place their strings by a row scan of their
-// lengths), and only then finds its start bit by decoupled look-back over the
-// groups before it in the same scan (per group: aggregate, then inclusive
-// prefix, published in one 64-bit word) -- by then those groups have
-// published, so the look-back rarely waits -- and stores the window shifted
-// into place.  Groups wider than one window (near worst-case entropy) take
-// the look-back first and pack window by window at absolute offsets.
-//
-// Seam mode (EntArgs::seam, the frame encodes): a group stores every word it
-// reaches the end of plainly; its first word, when the group before it ends
-// inside that word, goes to seam[] for k_seam_fix -- the scan buffers may
-// hold anything when the kernel starts, and no word is written twice.  (A/B,
-// config 3: 0.72 ms against 0.80 for the OR-onto-zero form, which the band
-// paths keep: there the buffers are all-zero on entry -- k_emit_write zeroes
-// every word it consumes, the host clears them after the band paths -- and a
-// group ORs its first and last word, which it may share with a neighbour.)
-// No ordering between groups beyond the prefix itself.  (Measured: staging a group's tokens in LDS to
-// read them once ran 1.72 ms instead of 1.31 ms per config-3 step -- the
-// 48 KB staging cut residency from 8 to 3 groups per CU, and the kernel is
-// latency-bound; look-back before packing: 0.94-0.97 ms against 0.92 here.)
-// ===========================================================================
+// Pack groups' look-back words (EntArgs::pack_state, one per group of
+// PACK_SEGS segments of one scan): flag << 62 | bits, flag 1 = the group's
+// own bit count (aggregate), 2 = the inclusive prefix of its scan.
 constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1;
-// k_pack_lb: a lane takes 4 consecutive tokens of a segment (one 16-byte
-// load), 16 lanes a segment, 64 tokens per row step; the first LB_STEPS steps
-// of each of a row's PACK_SEGS / 16 segments are merged once in phase 1 and
-// kept in registers, as (64-bit string, length), until phase 3 places them
-// (measured on config 3, where luma segments hold ~138 tokens and chroma ones
-// ~16: LB_STEPS = 3 at occupancy 4 or 5, 0.96 ms, and 2 at 5, 0.92, against
-// 1 at occupancy 6, 0.92; occupancy 6 beats 7 by 0.03 ms)
-constexpr int LB_SEGS_PER_ROW = 4;
-constexpr int LB_ROWS = PACK_SEGS / LB_SEGS_PER_ROW;   // 16-lane rows per workgroup
-constexpr int LB_THREADS = 16 * LB_ROWS;
-constexpr int LB_VPL = PACK_SEGS / 64;                 // look-back scan: segments per lane
-#ifndef MIJ_LB_STEPS
-#define MIJ_LB_STEPS 1
-#endif
-#ifndef MIJ_LB_STEPS_C
-#define MIJ_LB_STEPS_C 1
-#endif
-#ifndef MIJ_LB_OCC
-#define MIJ_LB_OCC 6
-#endif
-constexpr int LB_STEPS = MIJ_LB_STEPS, LB_STEPS_C = MIJ_LB_STEPS_C;
-static_assert(LB_STEPS_C <= LB_STEPS && 64 * LB_STEPS <= SEG_TOK, "k_pack_lb: register steps inside a slot");
-static_assert(PACK_SEGS % 64 == 0 && LB_THREADS <= 1024, "k_pack_lb: 4 segments per 16-lane row");
 
-// k_pack_lb's code table: per [DC | AC][symbol] the Huffman code already
+// The packing's code table: per [DC | AC][symbol] the Huffman code already
 // shifted left by the symbol's magnitude bit count (cls = symbol & 15,
 // encoder.c:434-460) in bits 0-26 and the total length code length + cls in
 // bits 27-31 (<= 16 + 11 = 27 bits: magnitudes stop at class 11 after
@@ -2735,478 +2575,48 @@ __device__ __forceinline__ int ff_word(uint32_t v, uint32_t W, uint32_t nb) {
 }
 constexpr int EMIT_CW = EMIT_CH / 4;  // stream words per emit chunk
 
-// PW: the LDS window in words (PACK_WORDS; high-quality batches, whose groups
-// outgrow it, get the wider PACK_WIDE_WORDS window -- fewer groups per CU,
-// but no group on the window-by-window path; both in mij_internal.h)
-// FF: seam mode with the 0xFF bytes counted as the words are stored
-// (EntArgs::ff_pack; a compile-time variant: at 79 VGPRs the runtime checks
-// of both modes spilled)
-// The wide-window variant (high quality: segments of several hundred tokens)
-// loads MIJ_LB_UNR_WIDE steps past the registers per round (one memory round
-// trip for them instead of one each), with the VGPRs of MIJ_LB_OCC_WIDE groups
-// per CU
-#ifndef MIJ_LB_UNR
-#define MIJ_LB_UNR 1
-#endif
-#ifndef MIJ_LB_UNR_WIDE
-#define MIJ_LB_UNR_WIDE 2
-#endif
-#ifndef MIJ_LB_OCC_WIDE
-#define MIJ_LB_OCC_WIDE 5
-#endif
-template <int PW>
-constexpr int lb_occ() { return PW > PACK_WORDS ? MIJ_LB_OCC_WIDE : MIJ_LB_OCC; }
-template <int PW, bool FF>
-__global__ __launch_bounds__(LB_THREADS, lb_occ<PW>()) void k_pack_lb(EntArgs a) {
-  constexpr int UNR = PW > PACK_WORDS ? MIJ_LB_UNR_WIDE : MIJ_LB_UNR;
-  __shared__ uint32_t buf[PW];
-  __shared__ uint32_t tab[2 * 256];
-  __shared__ uint32_t s_bits[PACK_SEGS], s_off[PACK_SEGS];
-  __shared__ unsigned long long s_prefix;
-  __shared__ uint32_t s_total;
-  __shared__ int s_ticket;
-  constexpr int FFN = PW / EMIT_CW + 2;  // emit chunks one window's words can touch
-  __shared__ uint32_t s_ff[FFN];         // ff_pack: 0xFF bytes per chunk of the window
-  __shared__ uint32_t s_ffnb;            // ff_pack: the scan's whole bytes (its last group), else all
-  const Geom &G = a.g;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (FF && tid < FFN) s_ff[tid] = 0;
-#ifdef MIJ_K1_DIAG
-  unsigned long long tstamp[4];
-#define LB_STAMP(k) tstamp[k] = __builtin_amdgcn_s_memrealtime()
-#else
-#define LB_STAMP(k)
-#endif
-  LB_STAMP(0);
-  const int gy = (G.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (G.nsc + PACK_SEGS - 1) / PACK_SEGS;
-  const int gpf = gy + 2 * gc;
-  // The workgroup's scan follows from its index; its group inside the scan
-  // from the scan's own ticket, so that groups are claimed in scan order (a
-  // group's look-back only waits on groups that have started) without one
-  // counter for the whole launch.  (Measured: one launch-wide ticket 0.92 ms,
-  // per-scan tickets 0.89, dispatch order without a ticket 0.84 -- not safe
-  // by the ISA's guarantees; loading the group dispatch order suggests while
-  // the ticket is in flight: the tickets of a scan arrive out of dispatch
-  // order across the XCDs, so most groups redid their loads, 1.08 ms.)
-  const int f = blockIdx.x / gpf, bq = blockIdx.x - f * gpf;
-  const int comp = bq < gy ? 0 : (bq < gy + gc ? 1 : 2);
-  const int sbase = comp == 0 ? 0 : (comp == 1 ? G.nsy : G.nsy + G.nsc), ns = comp == 0 ? G.nsy : G.nsc;
-  const int gscan0 = f * gpf + (comp == 0 ? 0 : gy + (comp == 2 ? gc : 0));  // the scan's first group
-  const int nq = comp == 0 ? gy : gc;
-  if (tid == 0) s_ticket = (int)atomicAdd(&a.pack_ticket[f * 3 + comp], 1u);
-  __syncthreads();
-  const int q = s_ticket;
-  const int gid = gscan0 + q;
-  const int chroma = comp != 0;
-  const int sub = tid & 15, row = tid >> 4;
-  const int nst = chroma ? LB_STEPS_C : LB_STEPS;  // register steps of this scan
-  const int s0 = q * PACK_SEGS, nsg = min(ns, s0 + PACK_SEGS) - s0;
-  const long long fs0 = (long long)f * G.nseg + sbase + s0;  // the group's first segment
-  int nt[LB_SEGS_PER_ROW];
-  uint32_t Lz = 0, zcode = 0;
-  // a step's 4 tokens (lim = tokens left - 4 * sub): bits, ZRLs included.
-  // K1 padded the segment to a multiple of 4 tokens with LB_NOTOK (0 bits),
-  // so a lane's 4 slots are all tokens (lim > 0) or all past the end
-  auto step_bits = [&](const u4v &t, int lim) -> uint32_t {
-    uint32_t b = 0;
-#pragma unroll
-    for (int e = 0; e < 4; e++) b += lb_tok_len(tab, t[e]) + ((t[e] >> 8) & 3u) * Lz;
-    return lim > 0 ? b : 0u;
-  };
-  // steps past the registers (segments of more than 64 * LB_STEPS tokens)
-  auto load_step = [&](int k, int i0) -> u4v {
-    const uint32_t *tk = a.tok + (fs0 + row + LB_ROWS * k) * SEG_TOK;
-    const int j = i0 + 4 * sub;
-    return j < nt[k] ? *(const u4v *)(tk + j) : u4v{0u, 0u, 0u, 0u};
-  };
-  // a step's 4 tokens merged into one left-growing bit string (ZRLs first,
-  // encoder.c:490-494), and its length; garbage but flagged when > 64 bits
-  auto merge_step = [&](const u4v &t, int lim, unsigned long long &acc) -> uint32_t {
-    uint32_t nb = 0;
-    acc = 0;
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-      uint32_t code;
-      const uint32_t L = lb_tok_code(tab, t[e], code);
-      const uint32_t nzr = (t[e] >> 8) & 3u;
-      for (uint32_t z = nzr; z; z--) acc = (acc << Lz) | zcode;
-      acc = (acc << L) | code;
-      nb += L + nzr * Lz;
-    }
-    return lim > 0 ? nb : 0u;  // (the string of a lane past the end is never placed)
-  };
-  unsigned long long pacc[LB_SEGS_PER_ROW][LB_STEPS];
-  uint32_t pnb[LB_SEGS_PER_ROW][LB_STEPS], bk[LB_SEGS_PER_ROW];
-  // ---- 0. this row's segments: token counts and their first register steps
-  // (LB_STEPS 64-token steps of a luma segment, LB_STEPS_C of a chroma one),
-  // all loads at once: none waits for the counts (a slot holds SEG_TOK
-  // tokens, so reading past a short segment stays inside it; lim masks the
-  // excess) -- one memory round trip before the tables are ready ------------
-  u4v tq[LB_SEGS_PER_ROW][LB_STEPS];
-  uint32_t t0w[LB_SEGS_PER_ROW];
-#pragma unroll
-  for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
-    const int sl = row + LB_ROWS * k;
-    const bool in = sl < nsg;  // row-uniform; no slot past the group's last segment
-    nt[k] = in ? (int)a.seg_ntok[fs0 + sl] : 0;
-#pragma unroll
-    for (int st = 0; st < LB_STEPS; st++)
-      tq[k][st] = in && st < nst ? *(const u4v *)(a.tok + (fs0 + sl) * SEG_TOK + 64 * st + 4 * sub)
-                                 : u4v{0u, 0u, 0u, 0u};
-    t0w[k] = in && sub == 0 ? a.tok0[fs0 + sl] : 0u;  // token 0 (dense array)
-  }
-  for (int i = tid; i < 512; i += LB_THREADS)
-    tab[i] = lb_tab_entry(a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + i], (uint32_t)i & 255u);
-  {  // the ZRL code (AC symbol 0xF0: cls 0, so the entry is code / length)
-    const uint32_t zac = a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + 256 + 0xF0];
-    Lz = zac >> 16;
-    zcode = zac & 0xFFFFu;
-  }
-  __syncthreads();
-  // ---- 1. bits of each segment.  The register steps are merged here, once
-  // (phase 3 only places them); steps past them are read twice ---------------
-#pragma unroll
-  for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
-    nt[k] = min(nt[k], SEG_TOK);
-    if (sub == 0 && nt[k] > 0) tq[k][0][0] = t0w[k];
-    uint32_t b = 0;
-#pragma unroll
-    for (int st = 0; st < LB_STEPS; st++) {
-      pacc[k][st] = 0;
-      pnb[k][st] = st < nst ? merge_step(tq[k][st], nt[k] - 64 * st - 4 * sub, pacc[k][st]) : 0u;
-      b += pnb[k][st];
-    }
-    bk[k] = b;
-  }
-  // steps past the registers, in rounds: one step of every segment of the
-  // row per round, their loads issued together (one memory round trip per
-  // round, not per segment and step)
-  const int ntmax = max(max(nt[0], nt[1]), max(nt[2], nt[3]));  // row-uniform
-  for (int i0 = 64 * nst; i0 < ntmax; i0 += 64 * UNR) {
-    u4v tr[UNR][LB_SEGS_PER_ROW];
-#pragma unroll
-    for (int u = 0; u < UNR; u++)
-#pragma unroll
-      for (int k = 0; k < LB_SEGS_PER_ROW; k++) tr[u][k] = load_step(k, i0 + 64 * u);
-#pragma unroll
-    for (int u = 0; u < UNR; u++)
-#pragma unroll
-      for (int k = 0; k < LB_SEGS_PER_ROW; k++)
-        if (i0 + 64 * u < nt[k]) bk[k] += step_bits(tr[u][k], nt[k] - (i0 + 64 * u) - 4 * sub);
-  }
-#pragma unroll
-  for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
-    const int sl = row + LB_ROWS * k;
-    if (sl < nsg) {  // row-uniform
-      const uint32_t b = row_scan16(bk[k]);
-      if (sub == 15) s_bits[sl] = b;
-    }
-  }
-  __syncthreads();
-  LB_STAMP(1);
-  // ---- 2. offsets inside the group and its total; the aggregate goes out
-  // at once, so later groups' look-backs need not wait for this one's packing
-  if (wave == 0) {
-    uint32_t vv[LB_VPL], v = 0;
-#pragma unroll
-    for (int i = 0; i < LB_VPL; i++) {
-      vv[i] = lane * LB_VPL + i < nsg ? s_bits[lane * LB_VPL + i] : 0u;
-      v += vv[i];
-    }
-    const uint32_t incl = wave_scan64(v);
-    uint32_t run = incl - v;
-#pragma unroll
-    for (int i = 0; i < LB_VPL; i++) {
-      if (lane * LB_VPL + i < nsg) s_off[lane * LB_VPL + i] = run;
-      run += vv[i];
-    }
-    const uint32_t T = __shfl(incl, 63);
-    if (lane == 0) {
-      s_total = T;
-      if (q > 0) __hip_atomic_store(&a.pack_state[gid], LB_AGG | T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-  const uint32_t gbits = s_total;
-  // the group's first bit in its scan: decoupled look-back over the groups
-  // before it (wave 0; publishes this group's inclusive prefix)
-  auto look_back = [&]() {
-    if (wave != 0) return;
-    const unsigned long long base = a.bit_base ? a.bit_base[f * 4 + comp] : 0u;
-    unsigned long long *stt = a.pack_state;
-    unsigned long long prefix = base;
-    if (q > 0) {
-      prefix = 0;
-      long long j = gid - 1;
-      while (true) {
-        const long long jj = j - lane;
-        unsigned long long sv = jj >= gscan0 ? __hip_atomic_load(&stt[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                             : (LB_INC | base);
-        const unsigned long long m2 = __ballot((sv >> 62) == 2), m0 = __ballot((sv >> 62) == 0);
-        const unsigned long long upto = m2 ? (m2 & (~m2 + 1)) : 0ull;  // lowest inclusive lane
-        if (m0 & (upto ? upto - 1 : ~0ull)) {  // a group before it has not published yet
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        const int kk = upto ? __ffsll((long long)m2) - 1 : 63;
-        unsigned long long add = lane <= kk ? (sv & LB_VAL) : 0ull;
-        for (int off = 32; off; off >>= 1) add += __shfl_xor(add, off);
-        prefix += add;
-        if (upto) break;
-        j -= 64;
-      }
-    }
-    if (lane == 0) {
-      __hip_atomic_store(&stt[gid], LB_INC | (prefix + gbits), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (q == nq - 1) a.scan_bits[f * 3 + comp] = prefix + gbits;
-      s_prefix = prefix;
-      if (FF) s_ffnb = q == nq - 1 ? (uint32_t)((prefix + gbits) >> 3) : ~0u;
-    }
-  };
-  // ---- 3. pack the group's tokens.  A group that fits one LDS window (all
-  // but near worst-case entropy) is placed relative to its own first bit and
-  // shifted into place as it is stored, so its look-back runs after the
-  // packing, when the groups before it have long published; a wider group
-  // takes its start bit first and packs window by window at absolute offsets.
-  uint32_t *raw_scan = a.raw + (long long)f * G.raw_fs +
-                       (comp == 0 ? 0 : G.raw_words[0] + (comp == 2 ? G.raw_words[1] : 0));
-  const bool rel = ((gbits + 31) >> 5) + 1 <= (uint32_t)PW;
-  // the group's words in the scan: [first, first + n)
-  auto group_words = [&](unsigned long long gbase, uint32_t &n) -> unsigned long long {
-    n = (uint32_t)(((gbase & 31) + gbits + 31) >> 5);
-    if ((gbase >> 5) + n + 1 > (unsigned long long)G.raw_words[comp]) {  // cannot happen for valid
-      if (tid == 0) a.err[f] = 2;                                         // tokens; never write OOB
-      n = 0;
-    }
-    return gbase >> 5;
-  };
-  // ff_pack: a stored word's 0xFF bytes counted per emit chunk (c0: the
-  // chunk of the window's first word; nb: the scan's whole bytes, known to
-  // its last group, else all)
-  auto ff_add = [&](uint32_t v, uint32_t W, uint32_t c0) {
-    const int c = ff_word(v, W, s_ffnb);
-    if (c) atomicAdd(&s_ff[W / EMIT_CW - c0], (uint32_t)c);
-  };
-  uint32_t boff = 0, nw = ((gbits + 31) >> 5) + 1;  // relative: one spare word for the shift
-  unsigned long long gw = 0;
-  if (!rel) {
-    look_back();
-    __syncthreads();
-    boff = (uint32_t)(s_prefix & 31);
-    gw = group_words(s_prefix, nw);
-  }
-  LB_STAMP(2);
-  for (uint32_t w0 = 0; w0 < nw; w0 += PW) {
-    const uint32_t wn = min((uint32_t)PW, nw - w0);
-    const uint32_t lo_bit = w0 * 32, hi_bit = (w0 + wn) * 32;
-    for (uint32_t i = tid; i < wn; i += LB_THREADS) buf[i] = 0;
-    __syncthreads();
-    // lanes merged their 4 tokens of a register step into a 64-bit string in
-    // phase 1 and OR it in with <= 3 LDS atomics.  A narrower window, or a
-    // lane whose 4 tokens exceed 64 bits, goes token by token in a second
-    // pass that reloads the tokens.
-    const bool whole = w0 == 0 && wn == nw;
-    auto decode = [&](const u4v &t, int lim, uint32_t (&L)[4], uint32_t (&code)[4], uint32_t (&nzr)[4]) {
-      uint32_t nb = 0;
-#pragma unroll
-      for (int e = 0; e < 4; e++) {
-        L[e] = lb_tok_code(tab, t[e], code[e]);
-        nzr[e] = (t[e] >> 8) & 3u;
-        if (lim <= 0) L[e] = nzr[e] = code[e] = 0u;  // (a lane past the end places nothing)
-        nb += L[e] + nzr[e] * Lz;
-      }
-      return nb;
-    };
-    // (a window of a wider group: the same merged strings, clipped to it)
-    bool slow = false;
-    // one 64-token step of a row past the registers: positions, then the
-    // lane's merged bits
-    auto fast_step = [&](const u4v &t, int lim, uint32_t &pos0) {
-      uint32_t L[4], code[4], nzr[4];
-      const uint32_t nb = decode(t, lim, L, code, nzr);
-      const uint32_t x = row_scan16(nb);
-      const uint32_t pos = pos0 + x - nb;
-      pos0 += row_last(x);
-      if (nb > 64) {
-        slow = true;
-      } else if (nb) {
-        unsigned long long acc = 0;
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-          for (uint32_t z = nzr[e]; z; z--) acc = (acc << Lz) | zcode;  // encoder.c:490-494 ZRL
-          acc = (acc << L[e]) | code[e];
-        }
-        if (whole) put_bits64(buf, pos, acc << (64 - nb), nb);
-        else put_bits64_win(buf, pos, acc << (64 - nb), nb, lo_bit, hi_bit);
-      }
-    };
-    // the same for a step merged in phase 1
-    auto placed_step = [&](unsigned long long acc, uint32_t nb, uint32_t &pos0) {
-      const uint32_t x = row_scan16(nb);
-      const uint32_t pos = pos0 + x - nb;
-      pos0 += row_last(x);
-      if (nb > 64) slow = true;
-      else if (nb && whole) put_bits64(buf, pos, acc << (64 - nb), nb);
-      else if (nb) put_bits64_win(buf, pos, acc << (64 - nb), nb, lo_bit, hi_bit);
-    };
-    {
-      uint32_t pos0[LB_SEGS_PER_ROW];
-#pragma unroll
-      for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
-        const int sl = row + LB_ROWS * k;
-        if (sl >= nsg) break;  // row-uniform
-        pos0[k] = boff + s_off[sl];
-#pragma unroll
-        for (int st = 0; st < LB_STEPS; st++) {
-          if (st >= nst || 64 * st >= nt[k]) break;  // row-uniform
-          placed_step(pacc[k][st], pnb[k][st], pos0[k]);
-        }
-      }
-      // the steps past the registers again in rounds (segments beyond the
-      // group have nt = 0)
-      for (int i0 = 64 * nst; i0 < ntmax; i0 += 64 * UNR) {
-        u4v tr[UNR][LB_SEGS_PER_ROW];
-#pragma unroll
-        for (int u = 0; u < UNR; u++)
-#pragma unroll
-          for (int k = 0; k < LB_SEGS_PER_ROW; k++) tr[u][k] = load_step(k, i0 + 64 * u);
-#pragma unroll
-        for (int u = 0; u < UNR; u++)
-#pragma unroll
-          for (int k = 0; k < LB_SEGS_PER_ROW; k++)
-            if (i0 + 64 * u < nt[k]) fast_step(tr[u][k], nt[k] - (i0 + 64 * u) - 4 * sub, pos0[k]);
-      }
-    }
-    if (__ballot(slow)) {  // second pass over this wave's rows, tokens reloaded
-      for (int k = 0; k < LB_SEGS_PER_ROW; k++) {
-        const int sl = row + LB_ROWS * k;
-        if (sl >= nsg) break;  // row-uniform
-        uint32_t pos0 = boff + s_off[sl];
-        if (pos0 >= hi_bit || pos0 + s_bits[sl] <= lo_bit) continue;  // row-uniform
-        const uint32_t *tk = a.tok + (fs0 + sl) * SEG_TOK;
-        for (int i0 = 0; i0 < nt[k]; i0 += 64) {
-          const int j = i0 + 4 * sub;
-          u4v t = j < nt[k] ? *(const u4v *)(tk + j) : u4v{0u, 0u, 0u, 0u};
-          if (j == 0 && nt[k] > 0) t[0] = a.tok0[fs0 + sl];
-          uint32_t L[4], code[4], nzr[4];
-          const uint32_t nb = decode(t, nt[k] - j, L, code, nzr);
-          const uint32_t x = row_scan16(nb);
-          uint32_t pos = pos0 + x - nb;
-          pos0 += row_last(x);
-          // the first pass placed the steps of lanes within 64 bits
-          if (nb <= 64) continue;
-          for (int e = 0; e < 4; e++) {
-            for (uint32_t z = nzr[e]; z; z--) {  // encoder.c:490-494 ZRL
-              if (pos < hi_bit && pos + Lz > lo_bit) put_bits_window(buf, pos, lo_bit, hi_bit, zcode, (int)Lz);
-              pos += Lz;
-            }
-            if (L[e] && pos < hi_bit && pos + L[e] > lo_bit) put_bits_window(buf, pos, lo_bit, hi_bit, code[e], (int)L[e]);
-            pos += L[e];
-          }
-        }
-      }
-    }
-    if (rel) {  // the start bit now, then the words shifted into place
-      look_back();
-      __syncthreads();
-      uint32_t n;
-      gw = group_words(s_prefix, n);
-      const uint32_t sh = (uint32_t)(s_prefix & 31);
-      uint32_t *raw = raw_scan + gw;
-      // the edge words may be shared with the neighbouring groups: OR (onto
-      // zero), or in seam mode (EntArgs::seam) the first word to the side
-      const uint32_t c0 = (uint32_t)gw / EMIT_CW;
-      for (uint32_t i = tid; i < n; i += LB_THREADS) {
-        const uint32_t v = __builtin_amdgcn_alignbit(i ? buf[i - 1] : 0u, buf[i], sh);
-        if (FF || a.seam) {  // every word stored whole; a shared first word goes to the seam
-          if (i == 0 && sh) {
-            a.seam[gid] = v;
-          } else {
-            raw[i] = v;
-            if (FF) ff_add(v, (uint32_t)gw + i, c0);
-          }
-        } else if (i == 0 || i == n - 1) atomicOr(&raw[i], v);
-        else raw[i] = v;
-      }
-    } else {
-      __syncthreads();
-      uint32_t *raw = raw_scan + gw;
-      const uint32_t c0 = ((uint32_t)gw + w0) / EMIT_CW;
-      for (uint32_t i = tid; i < wn; i += LB_THREADS) {
-        const uint32_t wi = w0 + i;
-        if (FF || a.seam) {
-          if (wi == 0 && boff) {
-            a.seam[gid] = buf[i];
-          } else {
-            raw[wi] = buf[i];
-            if (FF) ff_add(buf[i], (uint32_t)gw + wi, c0);
-          }
-        } else if (wi == 0 || wi == nw - 1) atomicOr(&raw[wi], buf[i]);
-        else raw[wi] = buf[i];
-      }
-    }
-    __syncthreads();
-    if (FF && tid < FFN && s_ff[tid]) {  // the window's chunk counts out, zeroed for the next
-      atomicAdd(&a.ffc[(long long)(f * 3 + comp) * emit_chunks(G) + ((uint32_t)gw + (rel ? 0u : w0)) / EMIT_CW + tid], s_ff[tid]);
-      s_ff[tid] = 0;
-    }
-  }
-#ifdef MIJ_K1_DIAG
-  LB_STAMP(3);
-  if (a.dbg && tid == 0)
-    for (int k = 0; k < 4; k++) a.dbg[(long long)gid * 4 + k] = tstamp[k];
-#endif
-#undef LB_STAMP
-}
 
 // ===========================================================================
-// k_pack_flat: k_pack_lb's job with the group's tokens as one flat stream.
-// A pack group's bitstream is its segments' token strings back to back, and
-// K1 pads every segment to a multiple of 4 tokens (LB_NOTOK, no bits), so the
-// group is a list of 4-token chunks, each inside one segment slot and 16-byte
-// aligned.  Every thread takes one chunk per round (256 chunks, 1024 tokens a
-// round; the segment of a chunk by binary search of the chunk counts' prefix),
-// merges its 4 tokens into one bit string, and a workgroup scan of the string
-// lengths places them in the LDS window relative to the group's first bit --
-// every token is read and decoded once, and no lane idles on a short segment
-// (k_pack_lb gives 16 lanes to a segment: a chroma segment of ~16 tokens kept
-// 12 of them idle, and a luma segment's tokens past the first 64 were read
-// and decoded twice).  The next round's chunk is loaded while a round is
-// placed.  Then the group's aggregate goes out, the decoupled look-back finds
-// its start bit and the window is stored shifted into place, as in k_pack_lb.
-// A group whose bits outgrow the window (near worst-case entropy) takes its
-// start bit and sweeps its chunks again once per window, at absolute offsets.
+// k_pack_flat: segment bits, scan offsets and bit packing in one pass
+// (encoder.c:434-502).  Each workgroup takes the next pack group of PACK_SEGS
+// segments of one scan (a per-scan ticket keeps groups claimed in scan order,
+// so a look-back only waits on groups that have started).  A pack group's
+// bitstream is its segments' token strings back to back, and K1 pads every
+// segment to a multiple of 4 tokens (LB_NOTOK, no bits), so the group is a
+// list of 4-token chunks, each inside one segment slot and 16-byte aligned.
+// Every thread takes PF_K chunks per round (the segment of a chunk by binary
+// search of the chunk counts' prefix), merges each chunk's 4 tokens into one
+// bit string, and a workgroup scan of the string lengths places them in the
+// LDS window relative to the group's first bit -- every token is read and
+// decoded once, and no lane idles on a short segment.  The next round's
+// chunks are loaded while a round is placed.  The group's aggregate goes out
+// as soon as the last round's scan has it; then the decoupled look-back over
+// the groups before it finds its start bit (by then they have usually
+// published; the wait is bounded, MIJ_SPIN_LIMIT) and the window is stored
+// shifted into place.  A group whose bits outgrow the window (near
+// worst-case entropy) takes its start bit and sweeps its chunks again once
+// per window, at absolute offsets.
+//
+// Seam mode (EntArgs::seam, the frame encodes): a group stores every word it
+// reaches the end of plainly; its first word, when the group before it ends
+// inside that word, goes to seam[] for k_seam_fix -- the scan buffers may
+// hold anything when the kernel starts, and no word is written twice (A/B,
+// config 3: 0.72 ms against 0.80 for the OR-onto-zero form, which the band
+// paths keep: there the buffers are all-zero on entry and a group ORs its
+// first and last word, which it may share with a neighbour).
+//
+// Tuning (profiles/r04): 2 chunks per thread per round at 8
+// workgroups per CU (1 chunk: 0.65-0.69 ms, 3 chunks at occupancy 7:
+// 1.51-1.57); the wide window (PACK_WIDE_WORDS, high quality) runs 6
+// workgroups per CU by its LDS.
 // ===========================================================================
 constexpr int PF_THREADS = 256, PF_WAVES = PF_THREADS / 64;
-// (MIJ_PACK_FLAT=0: k_pack_lb instead, for A/B)
-#ifndef MIJ_PACK_FLAT
-#define MIJ_PACK_FLAT 1
-#endif
-#ifndef MIJ_PF_K
-#define MIJ_PF_K 2
-#endif
-#ifndef MIJ_PF_OCC
-#define MIJ_PF_OCC 8
-#endif
-#ifndef MIJ_PF_K_WIDE
-#define MIJ_PF_K_WIDE MIJ_PF_K
-#endif
-// chunks per thread per round (the wide window's variant runs five
-// workgroups per CU by its LDS, with VGPRs to spare for larger rounds)
+constexpr int PF_K = 2, PF_OCC = 8, PF_OCC_WIDE = 6;
 template <int PW>
-constexpr int pf_k() { return PW > PACK_WORDS ? MIJ_PF_K_WIDE : MIJ_PF_K; }
-#ifndef MIJ_PF_PREFETCH
-#define MIJ_PF_PREFETCH 1
-#endif
-#ifndef MIJ_PF_OCC_WIDE
-#define MIJ_PF_OCC_WIDE 6
-#endif
-template <int PW>
-constexpr int pf_occ() { return PW > PACK_WORDS ? MIJ_PF_OCC_WIDE : MIJ_PF_OCC; }
+constexpr int pf_occ() { return PW > PACK_WORDS ? PF_OCC_WIDE : PF_OCC; }
 static_assert(PACK_SEGS == 64, "k_pack_flat: one wave scans the group's segments");
 template <int PW, bool FF>
 __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs a) {
-  constexpr int PF_K = pf_k<PW>();
   __shared__ uint32_t buf[PW];
   __shared__ uint32_t tab[2 * 256];
   __shared__ uint32_t s_cp[PACK_SEGS + 1];  // exclusive prefix of the segments' chunks; [64]: all
@@ -3214,17 +2624,21 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   __shared__ unsigned long long s_prefix;
   __shared__ int s_ticket;
   __shared__ uint32_t s_over;
+  __shared__ bool s_hung;
   constexpr int FFN = PW / EMIT_CW + 2;
   __shared__ uint32_t s_ff[FFN];
   __shared__ uint32_t s_ffnb;
   const Geom &G = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (FF && tid < FFN) s_ff[tid] = 0;
-  if (tid == 0) s_over = 0;
+  if (tid == 0) {
+    s_over = 0;
+    s_hung = false;
+  }
   const int gy = (G.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (G.nsc + PACK_SEGS - 1) / PACK_SEGS;
   const int gpf = gy + 2 * gc;
   // the scan from the workgroup's index, the group inside it from the scan's
-  // ticket (groups claimed in scan order, as k_pack_lb)
+  // ticket (groups claimed in scan order)
   const int f = blockIdx.x / gpf, bq = blockIdx.x - f * gpf;
   const int comp = bq < gy ? 0 : (bq < gy + gc ? 1 : 2);
   const int sbase = comp == 0 ? 0 : (comp == 1 ? G.nsy : G.nsy + G.nsc), ns = comp == 0 ? G.nsy : G.nsc;
@@ -3243,6 +2657,13 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   }
   __syncthreads();
   const int q = s_ticket;
+  // a ticket past the scan's groups (the ticket word was not reset, or was
+  // overwritten): nothing of it belongs to this launch -- flag the frame and
+  // leave the other scans' look-back words alone
+  if (q < 0 || q >= nq) {
+    if (tid == 0) a.err[f] = FERR_SPIN;
+    return;
+  }
   const int gid = gscan0 + q;
   const int s0 = q * PACK_SEGS, nsg = min(ns, s0 + PACK_SEGS) - s0;
   const long long fs0 = (long long)f * G.nseg + sbase + s0;  // the group's first segment
@@ -3299,12 +2720,9 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
       u4v t[PF_K];
 #pragma unroll
       for (int k = 0; k < PF_K; k++) t[k] = tn[k];
-      if (MIJ_PF_PREFETCH && c0 + PF_K * PF_THREADS < C) {
+      if (c0 + PF_K * PF_THREADS < C) {
 #pragma unroll
         for (int k = 0; k < PF_K; k++) chunk_load(c0 + (PF_K + k) * PF_THREADS + tid, tn[k]);
-      } else if (!MIJ_PF_PREFETCH && c0 > 0) {
-#pragma unroll
-        for (int k = 0; k < PF_K; k++) chunk_load(c0 + k * PF_THREADS + tid, t[k]);
       }
       uint32_t nb[PF_K], x[PF_K];
       unsigned long long acc[PF_K];
@@ -3381,9 +2799,11 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
     const unsigned long long base = a.bit_base ? a.bit_base[f * 4 + comp] : 0u;
     unsigned long long *stt = a.pack_state;
     unsigned long long prefix = base;
+    bool hung = false;
     if (q > 0) {
       prefix = 0;
       long long j = gid - 1;
+      const unsigned long long t_wait = __builtin_amdgcn_s_memrealtime();
       while (true) {
         const long long jj = j - lane;
         unsigned long long sv = jj >= gscan0 ? __hip_atomic_load(&stt[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
@@ -3391,6 +2811,13 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
         const unsigned long long m2 = __ballot((sv >> 62) == 2), m0 = __ballot((sv >> 62) == 0);
         const unsigned long long upto = m2 ? (m2 & (~m2 + 1)) : 0ull;  // lowest inclusive lane
         if (m0 & (upto ? upto - 1 : ~0ull)) {  // a group before it has not published yet
+          // (groups publish in claim order, so this wait is short; one that
+          // outlasts SPIN_TICKS means a lost publication: the frame fails
+          // instead of the launch hanging)
+          if (__builtin_amdgcn_s_memrealtime() - t_wait > SPIN_TICKS) {
+            hung = true;
+            break;
+          }
           __builtin_amdgcn_s_sleep(1);
           continue;
         }
@@ -3403,20 +2830,25 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
       }
     }
     if (lane == 0) {
+      // (a timed-out group still publishes, so the groups after it do not
+      // wait out the bound as well; the frame is failed)
       __hip_atomic_store(&stt[gid], LB_INC | (prefix + gbits), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (q == nq - 1) a.scan_bits[f * 3 + comp] = prefix + gbits;
       s_prefix = prefix;
       if (FF) s_ffnb = q == nq - 1 ? (uint32_t)((prefix + gbits) >> 3) : ~0u;
+      if (hung) a.err[f] = FERR_SPIN;
+      s_hung = hung;
     }
   }
   __syncthreads();
+  if (s_hung) return;  // (its start bit is unknown: nothing is stored)
   uint32_t *raw_scan = a.raw + (long long)f * G.raw_fs +
                        (comp == 0 ? 0 : G.raw_words[0] + (comp == 2 ? G.raw_words[1] : 0));
   const unsigned long long prefix = s_prefix;
   // the group's words in the scan: [first, first + n)
   uint32_t n = (uint32_t)(((prefix & 31) + gbits + 31) >> 5);
   if ((prefix >> 5) + n + 1 > (unsigned long long)G.raw_words[comp]) {  // cannot happen for valid tokens;
-    if (tid == 0) a.err[f] = 2;                                          // never write out of bounds
+    if (tid == 0) a.err[f] = FERR_OVERFLOW;                              // never write out of bounds
     n = 0;
   }
   const unsigned long long gw = prefix >> 5;
@@ -3480,7 +2912,7 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   }
 }
 
-// k_seam_fix (seam mode, EntArgs::seam): k_pack_lb stored every scan word
+// k_seam_fix (seam mode, EntArgs::seam): k_pack_flat stored every scan word
 // whole, each by the one group that reaches its end, and left a group's first
 // word, when the group before it ends inside that word, in seam[]; this ORs
 // those words in (one thread per group; atomics only because the last, short
@@ -3775,9 +3207,9 @@ __global__ __launch_bounds__(256) void k_emit_write(EntArgs a) {
   __shared__ int red[4];
   const int slot = blockIdx.x % a.emit_slots, f = blockIdx.x / a.emit_slots;
   const int tid = threadIdx.x;
-  // every scan-buffer word read here is zeroed after use: k_pack_lb needs
+  // every scan-buffer word read here is zeroed after use: the band packing needs
   // all-zero buffers (a failed frame's buffers are cleared whole) -- except
-  // in seam mode, where k_pack_lb stores whole words and nothing is zeroed
+  // in seam mode, where k_pack_flat stores whole words and nothing is zeroed
   const bool zero = a.seam == nullptr;
   if (!emit_frame_ok(a, f)) {
     uint32_t *rawf = a.raw + (long long)f * a.g.raw_fs;
@@ -3870,9 +3302,11 @@ __global__ void k_band_stuff_prep(EntArgs a, const unsigned long long *allbits, 
 }
 
 // the band's interiors in (frame, scan) order into dst: every chunk's output
-// offset (an exclusive scan of the 0xFF counts, frames and scans in order),
-// the stuffed bytes per scan into rec[0] and the band's total into *total;
-// one workgroup
+// offset inside its scan (an exclusive scan of the 0xFF counts; 32 bits: a
+// scan's stuffed bytes stay below a frame's out_cap) and every scan's first
+// byte in dst (scan_base, 64 bits: the band's buffer holds all n frames'
+// scans), the stuffed bytes per scan into rec[0] and the band's total into
+// *total; one workgroup
 __global__ __launch_bounds__(256) void k_band_stuff_scan(EntArgs a, unsigned long long *rec,
                                                          unsigned long long *total) {
   __shared__ int red[4];
@@ -3897,10 +3331,13 @@ __global__ __launch_bounds__(256) void k_band_stuff_scan(EntArgs a, unsigned lon
         tot += red[q];
       }
       __syncthreads();
-      if (c < nch) off[c] = (uint32_t)(pos + (unsigned long long)c * EMIT_CH + carry + wb + incl - v);
+      if (c < nch) off[c] = (uint32_t)((unsigned long long)c * EMIT_CH + carry + wb + incl - v);
       carry += tot;
     }
-    if (tid == 0) rec[(long long)i * BREC] = nbytes + carry;
+    if (tid == 0) {
+      rec[(long long)i * BREC] = nbytes + carry;
+      a.scan_base[i] = pos;
+    }
     pos += nbytes + carry;
   }
   if (tid == 0) *total = pos;
@@ -3959,7 +3396,7 @@ __global__ __launch_bounds__(256) void k_band_write(EntArgs a, uint8_t *dst, uns
     const uint32_t h = a.bit_base[f * 4 + comp];
     const long long ci = (long long)(f * 3 + comp) * nchmax + c;
     const int tot = (int)a.ffc[ci];
-    const unsigned long long o0 = a.choff[ci];
+    const unsigned long long o0 = a.scan_base[f * 3 + comp] + a.choff[ci];
     const unsigned long long clen = min((unsigned long long)EMIT_CH, nbytes - (unsigned long long)c * EMIT_CH) + tot;
     if (o0 + clen <= cap)  // (workgroup-uniform)
       stuff_chunk([&](unsigned long long w) { return shifted_word(raw, w, h); }, [](unsigned long long) {}, nbytes,
@@ -3968,7 +3405,7 @@ __global__ __launch_bounds__(256) void k_band_write(EntArgs a, uint8_t *dst, uns
   }
 }
 
-// the band's scan words zeroed again (k_pack_lb's band form ORs onto zero):
+// the band's scan words zeroed again (the band packing ORs onto zero):
 // the words of its bits only
 __global__ void k_band_zero(EntArgs a, const unsigned long long *rec) {
   const int i = blockIdx.y;  // f * 3 + comp
@@ -4010,7 +3447,7 @@ __global__ __launch_bounds__(256) void k_band_join(EntArgs a, const unsigned lon
   if (s_bad) {
     if (tid == 0) {
       a.out_len[f] = 0;
-      a.err[f] = a.err[f] ? a.err[f] : 3;
+      a.err[f] = a.err[f] ? a.err[f] : FERR_ASSEMBLY;
       for (int r = 0; r < world; r++)
         for (int c = 0; c < 3; c++) pieces[(((long long)f * world + r) * 3 + c) * 3 + 2] = 0;
     }
@@ -4122,7 +3559,7 @@ __global__ void k_or_pieces(uint32_t *raw, long long raw_fs, long long rw0, long
   }
 }
 
-// Band words out of the scan buffers, zeroed behind them (k_pack_lb needs
+// Band words out of the scan buffers, zeroed behind them (the band packing needs
 // all-zero buffers): piece blockIdx.y = {frame * 3 + scan, words, first
 // destination word}, from the start of the scan.
 __global__ void k_move_pieces(uint32_t *raw, long long raw_fs, long long rw0, long long rw1,
@@ -4233,7 +3670,7 @@ __global__ __launch_bounds__(256) void k_band_bound(const uint32_t *hist, const 
                                                     unsigned long long *pack_state, long long nstate,
                                                     unsigned *pack_ticket) {
   __shared__ unsigned long long s_w[4];
-  // (k_pack_lb's look-back words and tickets zeroed here, saving two fills
+  // (the packing's look-back words and tickets zeroed here, saving two fills
   // on the band stream's critical path)
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nstate; i += (long long)gridDim.x * 256)
     pack_state[i] = 0;
@@ -4406,7 +3843,7 @@ hipError_t launch_k1(const K1Args &a, int grid, int mode, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t launch_seg_dc(const EntArgs &a, hipStream_t s) {
-  hipLaunchKernelGGL(k_seg_dc, dim3(a.nframes * ((a.g.nseg + MIJ_SEGDC_WG - 1) / MIJ_SEGDC_WG)), dim3(MIJ_SEGDC_WG),
+  hipLaunchKernelGGL(k_seg_dc, dim3(a.nframes * ((a.g.nseg + SEGDC_WG - 1) / SEGDC_WG)), dim3(SEGDC_WG),
                      0, s, a);
   return hipGetLastError();
 }
@@ -4418,8 +3855,8 @@ hipError_t launch_dc_diff(int16_t *coef, const int16_t *dc, const Geom &g, int n
   return hipGetLastError();
 }
 hipError_t launch_segdc_actab(const EntArgs &a, hipStream_t s) {
-  hipLaunchKernelGGL(k_segdc_actab, dim3(a.nframes * (2 + (a.g.nseg + MIJ_SEGDC_WG - 1) / MIJ_SEGDC_WG)),
-                     dim3(MIJ_SEGDC_WG), 0, s, a);
+  hipLaunchKernelGGL(k_segdc_actab, dim3(a.nframes * (2 + (a.g.nseg + SEGDC_WG - 1) / SEGDC_WG)),
+                     dim3(SEGDC_WG), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_tables(const EntArgs &a, hipStream_t s) {
@@ -4499,7 +3936,7 @@ hipError_t launch_or_shift_pieces(uint32_t *raw, const Geom &g, const uint32_t *
   return hipGetLastError();
 }
 
-hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s, bool state_zeroed) {
+hipError_t launch_pack(const EntArgs &a, hipStream_t s, bool state_zeroed) {
   const int gy = (a.g.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (a.g.nsc + PACK_SEGS - 1) / PACK_SEGS;
   const long long groups = (long long)a.nframes * (gy + 2 * gc);
   if (!state_zeroed) {
@@ -4508,17 +3945,10 @@ hipError_t launch_pack_lb(const EntArgs &a, hipStream_t s, bool state_zeroed) {
     if (e != hipSuccess) return e;
   }
   const bool ff = a.ff_pack && a.seam;
-#if MIJ_PACK_FLAT
-  if (a.pack_wide && ff) hipLaunchKernelGGL((k_pack_flat<MIJ_PACK_WIDE_WORDS, true>), dim3((unsigned)groups), dim3(PF_THREADS), 0, s, a);
-  else if (a.pack_wide) hipLaunchKernelGGL((k_pack_flat<MIJ_PACK_WIDE_WORDS, false>), dim3((unsigned)groups), dim3(PF_THREADS), 0, s, a);
+  if (a.pack_wide && ff) hipLaunchKernelGGL((k_pack_flat<PACK_WIDE_WORDS, true>), dim3((unsigned)groups), dim3(PF_THREADS), 0, s, a);
+  else if (a.pack_wide) hipLaunchKernelGGL((k_pack_flat<PACK_WIDE_WORDS, false>), dim3((unsigned)groups), dim3(PF_THREADS), 0, s, a);
   else if (ff) hipLaunchKernelGGL((k_pack_flat<PACK_WORDS, true>), dim3((unsigned)groups), dim3(PF_THREADS), 0, s, a);
   else hipLaunchKernelGGL((k_pack_flat<PACK_WORDS, false>), dim3((unsigned)groups), dim3(PF_THREADS), 0, s, a);
-  return hipGetLastError();
-#endif
-  if (a.pack_wide && ff) hipLaunchKernelGGL((k_pack_lb<MIJ_PACK_WIDE_WORDS, true>), dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
-  else if (a.pack_wide) hipLaunchKernelGGL((k_pack_lb<MIJ_PACK_WIDE_WORDS, false>), dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
-  else if (ff) hipLaunchKernelGGL((k_pack_lb<PACK_WORDS, true>), dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
-  else hipLaunchKernelGGL((k_pack_lb<PACK_WORDS, false>), dim3((unsigned)groups), dim3(LB_THREADS), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_seam_fix(const EntArgs &a, hipStream_t s) {

@@ -314,7 +314,7 @@ static int stream_run(mij_stream *s, int n, const FillFn &fill, const DrainFn &d
     for (int i = 0; i < cnt; i++) {
       if (s->h_err[sl][i]) {
         if (failed) *failed = first + i;
-        return mij_fail(MIJ_ETABLE, "stream: frame %d: Huffman table construction failed", first + i);
+        return mij_frame_fail(s->h_err[sl][i], "stream: frame", first + i);
       }
       off[i + 1] = off[i] + (size_t)s->h_len[sl][i];
     }

@@ -71,7 +71,7 @@ class MijError(RuntimeError):
 
 # mij_batch_set_option (include/mijpeg.h: MIJ_OPT_*)
 OPTIONS = {"seam": 0, "ff_pack": 1, "actab": 2, "segdc_fused": 3, "pack_wide": 4, "emit_slots": 5,
-           "overlap_prio": 6}
+           "overlap_prio": 6, "fault_ticket": 7}
 
 
 _lib = None
@@ -353,7 +353,10 @@ class Batch:
         _check(self.lib.mij_batch_set_option(self.h_, OPTIONS[name], int(value)), f"set_option({name})")
 
     def get_option(self, name: str) -> int:
-        return int(self.lib.mij_batch_get_option(self.h_, OPTIONS[name]))
+        v = int(self.lib.mij_batch_get_option(self.h_, OPTIONS[name]))
+        if v == -2:  # mij_batch_get_option's error value (the error is set)
+            _check(self.lib.mij_last_error() or 1, "get_option")
+        return v
 
     def set_rgb(self, on: bool) -> None:
         """frames in R, G, B byte order (PPM) instead of the encoder's B, G, R"""

@@ -391,6 +391,9 @@ def encode_banded_dev(band, n: int, xch, frame_batch=None, events=None, emit: st
                 ready2 = torch.cuda.Event()
                 ready2.record(d)
             ready2.synchronize()
+            if int(h_tot.max()) > cap:  # (every rank sees the same totals: all raise)
+                raise RuntimeError(f"band stuffing: {int(h_tot.max())} stuffed bytes exceed the "
+                                   f"{cap}-byte buffer the word bound gave")
             # exact gather size (+16: the root's word copies read one word past)
             stride = (int(h_tot.max()) + 31) & ~15
             gathered = xch.gather(sbuf[:stride])

@@ -42,7 +42,7 @@ def test_partial_upload_keeps_other_region_sizes():
 def test_band_words_of_fewer_frames_than_packed_then_encode():
     """mij_band_pack over 2 frames, mij_band_words_all over only the first:
     frame 1's band words stay in its scan buffers, so the next encode must
-    clear them before k_pack_lb ORs its edge words in."""
+    clear them before the band packing ORs its edge words in."""
     W, H, n = 256, 64, 2
     frames = np.stack([recipes.config3_frame(i, H, W) for i in range(n)])
     b = mijpeg.Batch(W, H, n)
@@ -96,7 +96,7 @@ def test_assembler_refuses_pipeline_entry_points():
 
 
 def test_repeated_encodes_growing_and_shrinking_frame_counts():
-    """The encode path leaves the counts it read (and k_pack_lb's look-back
+    """The encode path leaves the counts it read (and k_pack_flat's look-back
     state) zeroed, and the next encode skips those fills only for the frames
     known clean: 1 frame, then 3 (two never zeroed), then 3 again, then 2,
     a band call in between (which writes the counts) and 3 again -- every

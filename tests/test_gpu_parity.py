@@ -352,7 +352,7 @@ def _luma_group_bits(Y, tabs, W, H, group, tiles_x):
 
 @pytest.mark.parametrize("q", [50, 100])
 def test_pack_window_paths_in_one_scan(q):
-    """k_pack_lb's two placement paths in one scan (both at Q=100, the
+    """k_pack_flat's two placement paths in one scan (both at Q=100, the
     single-window one alone at Q=50): a pack group whose bits fit one LDS
     window (4096 words; the 6144-word variant at Q >= 85) is placed relative to its own
     first bit and stored after the look-back; a wider one (noise rows: its
@@ -370,7 +370,7 @@ def test_pack_window_paths_in_one_scan(q):
     # (516k bits) and fits one at Q=50 (124k); frame 1's first (flat) fits
     b = mijpeg.Batch(W, H, 2, q)
     # the library's window at this quality (mij_batch_geometry: ent_args'
-    # pack_wide choice, whatever MIJ_PACK_WORDS / MIJ_PACK_WIDE_WORDS it was built with)
+    # pack_wide choice, whatever window sizes it was built with)
     window = b.geometry()["pack_window_words"] * 32
     Y, _, _, tabs, _ = O.cref_stages(frames[0], q)
     wide = _luma_group_bits(Y, tabs, W, H, 0, (W + 127) // 128) > window

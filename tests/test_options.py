@@ -145,3 +145,43 @@ def test_option_validation():
     with pytest.raises(mijpeg.MijError, match="unknown option"):
         mijpeg._check(b.lib.mij_batch_set_option(b.h_, 99, 0), "set_option")
     b.close()
+
+
+def test_stale_pack_ticket_fails_the_frame_instead_of_hanging():
+    """Every device-side wait is bounded (mij_internal.h SPIN_TICKS).  A
+    stale pack ticket (MIJ_OPT_FAULT_TICKET: frame 0's luma ticket starts at
+    1, so pack group 0 never runs and group 1's look-back waits for a
+    publication that never comes) fails frame 0 with MIJ_EHANG within the
+    bound, the other frames stay byte-exact, and the next encode of the same
+    batch is whole again."""
+    import time
+    frames = _frames(3)
+    want = [O.cref_encode(f) for f in frames]
+    b = mijpeg.Batch(W, H, 3)
+    b.upload(frames)
+    b.set_option("fault_ticket", 1)
+    t0 = time.time()
+    b.encode(3)
+    b.sync()
+    assert time.time() - t0 < 10.0, "the bounded wait should end in ~0.1 s"
+    with pytest.raises(mijpeg.MijError, match="outlasted its bound"):
+        b.output(0)
+    assert b.lib.mij_last_error() == 9  # MIJ_EHANG
+    for i in (1, 2):
+        assert b.output(i) == want[i]
+    assert b.get_option("fault_ticket") == 0  # consumed
+    b.encode(3)
+    _check(b, frames, 3, 50, want)
+    b.close()
+
+
+def test_get_option_error_raises():
+    b = mijpeg.Batch(W, H, 1)
+    h = b.h_
+    b.h_ = None  # a null handle: mij_batch_get_option returns -2 and sets the error
+    try:
+        with pytest.raises(mijpeg.MijError):
+            b.get_option("seam")
+    finally:
+        b.h_ = h
+        b.close()
