@@ -60,7 +60,7 @@ def parse():
     ap.add_argument("--split", action="store_true",
                     help="split pipeline: K1 writes coefficient planes and a second pass "
                          "tokenizes them (default: fused, K1 emits the symbol tokens itself)")
-    ap.add_argument("--coef-launches", type=int, default=3,
+    ap.add_argument("--coef-launches", type=int, default=5,
                     help="extra launches of the coefficient-output K1 variant after the timed "
                          "region, for its own 6 B/px roofline line (0 disables)")
     ap.add_argument("--workload", choices=["config3", "config4", "regions", "detect", "decode", "stream"],
@@ -929,25 +929,37 @@ def main():
     if args.mode == "dct":
         stage_avg = {"k1_colour_dct_quant": k1_ms}
 
+    # The coefficient-output K1 variant (BASELINE.json north_star's "fused
+    # DCT+quant kernel" at 6 B/px) is not on the default (fused) path: a few
+    # launches of it right after the timed region -- the GPU still at the
+    # clocks of the timed steps, like the dominant kernel it stands beside
+    # (launched after the seconds-long CPU verification instead, its first
+    # launches run ~20% slower while the clocks come back: 2.96-3.01 ms
+    # against 2.45-2.52 warm, profiles/r05) -- HIP events on the batch
+    # stream, one untimed launch first.  Then the same number of launches of
+    # its access pattern without the arithmetic (mij_batch_pattern_floor):
+    # K1's time beside the floor of its own memory traffic on this GPU.
+    replays = batch.replays()
+    coef_ms = floor_ms = None
+    if args.coef_launches > 0 and args.mode == "encode" and not args.split:
+        batch.set_timing(True)
+        batch.dct(F)
+        for _ in range(args.coef_launches):
+            batch.dct(F)
+        coef_ms = float(np.mean([h["k1_colour_dct_quant"]
+                                 for h in batch.stage_history(args.coef_launches)]))
+        batch.pattern_floor(F)
+        for _ in range(args.coef_launches):
+            batch.pattern_floor(F)
+        floor_ms = float(np.mean([h["k1_colour_dct_quant"]
+                                  for h in batch.stage_history(args.coef_launches)]))
+
     # correctness after timing (not timed): every distinct content against
     # the oracle and, where tests/golden holds it, the reference build's
     # sha256; then every slot of the batch against its content's bytes
     verified, pinned = 0, 0
     if args.verify and args.mode == "encode" and not os.environ.get("MIJ_K1_FLAGS"):
         verified, pinned = verify_batch(batch, frames, F, args, rank)
-
-    # the coefficient-output K1 variant (BASELINE.json north_star's "fused
-    # DCT+quant kernel" at 6 B/px) is not on the default (fused) path: a few
-    # launches of it after the timed region, HIP events on the batch stream,
-    # give its own roofline line beside the dominant kernel's
-    replays = batch.replays()
-    coef_ms = None
-    if args.coef_launches > 0 and args.mode == "encode" and not args.split:
-        batch.set_timing(True)
-        for _ in range(args.coef_launches):
-            batch.dct(F)
-        coef_ms = float(np.mean([h["k1_colour_dct_quant"]
-                                 for h in batch.stage_history(args.coef_launches)]))
 
     px_step = W * H * F
     value = px_all / el / 1e6
@@ -1017,7 +1029,11 @@ def main():
             "achieved": round(cb / (coef_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(cb / (coef_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "ms_per_launch": round(coef_ms, 4), "algorithmic_bytes_per_launch": int(cb),
-            "launches": args.coef_launches}
+            "launches": args.coef_launches,
+            # the same traffic with no arithmetic, same GPU, same call
+            "pattern_floor_ms": round(floor_ms, 4),
+            "pattern_floor_frac_of_peak": round(cb / (floor_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "frac_of_pattern_floor": round(floor_ms / coef_ms, 4)}
         u1, usrc1 = util_counters("k_mcu_dct<1>", res["config"])
         if u1 is not None:
             res["roofline_k1_coefficient_variant"].update(util_fields(u1, usrc1))

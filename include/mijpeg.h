@@ -181,6 +181,13 @@ int mij_batch_set_rgb(mij_batch *b, int on);
  * mij_batch_coefs); the split pipeline always has them */
 int mij_batch_keep_coefs(mij_batch *b, int on);
 int mij_batch_dct(mij_batch *b, int nframes);        /* K1 only, async */
+/* Measurement only (bench.py): K1's memory traffic without its arithmetic --
+ * the coefficient variant's persistent grid, tile claims, LDS-DMA of the BGR
+ * tiles one tile ahead and whole-line coefficient + raw-DC stores -- on
+ * frames 0..n-1, timed like mij_batch_dct; the coefficient planes are left
+ * holding garbage.  Its time is the floor of K1's access pattern on this GPU.
+ * Plain B, G, R batches only; async. */
+int mij_batch_pattern_floor(mij_batch *b, int nframes);
 int mij_batch_sync(mij_batch *b);
 int mij_batch_output(mij_batch *b, int frame, uint8_t *dst, size_t cap,
                      size_t *len);

@@ -218,15 +218,28 @@ static void fill_tables(int quality, Tables *t) {
   quality_tables(quality, q[0], q[1]);
   for (int c = 0; c < 2; c++)
     for (int z = 0; z < 64; z++) {
-      const int qz = q[c][k_zz[z]];
-      t->qint[c][z] = qz;
-      t->dqt[c][z] = qz;
-      // z = 0 (DC) is computed exactly from the pixel sum: no fast path
-      const double fac = 1.0 / (2097152.0 * qz);
-      // the error bound tau = fac * (0.72 L1 + 80) + 1e-6 is formed per block
-      // in K1 from the block's L1 = sum |pixel - 128|
-      t->qfac[c][z] = z ? (float)fac : 0.0f;
+      t->qint[c][z] = q[c][k_zz[z]];
+      t->dqt[c][z] = q[c][k_zz[z]];
     }
+  // The luma prescale of the A rows: zigzag group g = z / 16
+  // gets s_g = floor(log2(min luma AC q in the group)), row z the factor
+  // 2^s_g / q_z <= 1, so the weights stay inside the unscaled digit ranges
+  // and |N'| <= |N| < 2^31; a luma coefficient is then t = N' / 2^(21 + s_g).
+  int sg[4];
+  for (int g = 0; g < 4; g++) {
+    int qmin = 256;
+    for (int z = 16 * g; z < 16 * g + 16; z++)
+      if (z) qmin = t->qint[0][z] < qmin ? t->qint[0][z] : qmin;
+    int s = 0;
+    while ((2 << s) <= qmin) s++;
+    sg[g] = s;
+    t->kq[g] = 21 + s;
+  }
+  for (int z = 1; z < 64; z++) {
+    // chroma in fp32 on the luma-scaled N' (z = 0, the DC: exact from the pixel sum)
+    const double fac = (double)t->qint[0][z] / ((double)t->qint[1][z] * ldexp(1.0, 21 + sg[z >> 4]));
+    t->qfac[1][z] = (float)fac;
+  }
   // DC ties (K1 dc_tie): at |S| = 8qK the reference computes
   // (int)(((S * M_SQRT1_2) * M_SQRT1_2) / 4 / q) (encoder.c:87-109 with the
   // frequency-0 cosines exactly 1.0), which is K or K - 1
@@ -262,7 +275,7 @@ static void fill_tables(int quality, Tables *t) {
         double k = t->cosd[y * 8 + v] * t->cosd[x * 8 + u];
         if (u == 0) k *= M_SQRT1_2;
         if (v == 0) k *= M_SQRT1_2;
-        W = llround(k * 524288.0);  // 2^19
+        W = llround(k * ldexp(1.0, 19 + sg[z >> 4]) / t->qint[0][z]);  // 2^19 * 2^s_g / q_z
         const long long d0 = ((W + 64) & 127) - 64;
         const long long w1 = (W - d0) >> 7;
         const long long d1 = ((w1 + 64) & 127) - 64;
@@ -274,15 +287,16 @@ static void fill_tables(int quality, Tables *t) {
       for (int d = 0; d < 3; d++) memcpy(&t->mfma_a[(m * 3 + d) * 64 + lane], dig[d], 16);
     }
   // K1's chroma all-AC-zero test (Tables::czl): the reference's |F/q| < 1
-  // wherever |N| + 4096 (the integer DCT's error bound, L1 / 2 <= 4096)
-  // stays below 2^21 q (1 - 1e-6); the test runs where all-zero chroma
-  // N-tiles are common (smallest chroma AC quantiser >= 9: Q <= 75)
+  // wherever |N'| + 4096 (the integer DCT's error bound, L1 / 2 <= 4096)
+  // stays below (1 - 1e-6) / qfac (its unit); the test runs where all-zero
+  // chroma N-tiles are common (smallest chroma AC quantiser >= 9: Q <= 75)
   {
     int qmin = 256;
     for (int z = 0; z < 64; z++) {
-      const int qz = q[1][k_zz[z]];
-      t->czl[z] = z ? (int)(2097152.0 * qz * (1.0 - 2e-6) - 6000.0) : (1 << 30);
-      if (z) qmin = qz < qmin ? qz : qmin;
+      const double lim = z ? (double)t->qint[1][z] * ldexp(1.0, 21 + sg[z >> 4]) / t->qint[0][z] * (1.0 - 2e-6) - 6000.0
+                           : (double)(1 << 30);
+      t->czl[z] = lim > (double)(1 << 30) ? (1 << 30) : (int)lim;
+      if (z) qmin = t->qint[1][z] < qmin ? t->qint[1][z] : qmin;
     }
     t->cz_on = qmin >= 9;
   }
@@ -1143,6 +1157,22 @@ extern "C" int mij_batch_dct(mij_batch *b, int nframes) {
   next_slot(b);
   if (b->timing) HIP_TRY(hipEventRecord(b->ev[0], b->stream));
   if (run_k1(b, nframes, 1)) return g_err;  // events 1, 2
+  if (b->timing)
+    for (int k = 3; k < MIJ_NSTAGES; k++) HIP_TRY(hipEventRecord(b->ev[k], b->stream));
+  return MIJ_OK;
+}
+
+// measurement only: K1's memory traffic without its arithmetic (k_mcu_dct
+// <COEF_OUT | FLOOR>) on frames 0..n-1, timed like mij_batch_dct (stage
+// events); the coefficient planes are left holding garbage
+extern "C" int mij_batch_pattern_floor(mij_batch *b, int nframes) {
+  if (pipe_check(b, "pattern_floor")) return g_err;
+  if (nframes < 1 || nframes > b->cap) return fail(MIJ_EINVAL, "pattern_floor: bad frame count");
+  if (b->rgb || b->use_fdims) return fail(MIJ_EINVAL, "pattern_floor: plain B, G, R batches only");
+  HIP_TRY(hipSetDevice(b->dev));
+  next_slot(b);
+  if (b->timing) HIP_TRY(hipEventRecord(b->ev[0], b->stream));
+  if (run_k1(b, nframes, 1 | 64)) return g_err;  // K1M_COEF_OUT | K1M_FLOOR; events 1, 2
   if (b->timing)
     for (int k = 3; k < MIJ_NSTAGES; k++) HIP_TRY(hipEventRecord(b->ev[k], b->stream));
   return MIJ_OK;

@@ -128,14 +128,20 @@ __host__ __device__ inline FGeom frame_geom(const Geom &G, const int2 *fd, int f
 // Device-resident constant tables for one quality setting.
 struct Tables {
   int4 mfma_a[12 * 64];   // A fragments: 4 M-tiles x 3 digits x 64 lanes
-  float qfac[2][64];      // zigzag order: 1 / (2^21 * q)
+  // K1's quantisation: the A rows are prescaled for the
+  // luma table, row z by 2^s_g / q_z with s_g = floor(log2(the smallest luma
+  // AC quantiser of zigzag group g = z / 16)), so a luma N' is 2^(21 + s_g)
+  // t to within L1 / 2 and truncates by a shift (kq[g] = 21 + s_g); chroma
+  // keeps an fp32 factor: qfac[1][z] = q_luma(z) / (2^(21 + s_g) q_chroma(z))
+  float qfac[2][64];      // zigzag order; [0]: unused (luma is integer), [1]: chroma factor
+  int kq[4];              // luma shift per zigzag group of 16
   int qint[2][64];        // zigzag order: integer quantizer
   int dqt[2][64];         // zigzag order: DQT bytes
   double cosd[64];        // encoder.c:8-16 constants
   uint32_t lut[3][1024];  // colour-exception bitmaps (Y by R,G/2; Cb by G,B/2; Cr by G,R/2)
   uint32_t dctie[2][DCTIE_WORDS];  // bit K: the reference's DC at |S| = 8qK is K - 1
-  // K1's chroma all-AC-zero test: per zigzag z the limit L_z = 2^21 q_z
-  // (1 - 2e-6) - 6000 under which |N| means the reference's |F/q| < 1 (z = 0,
+  // K1's chroma all-AC-zero test: per zigzag z the limit L_z = (1 - 2e-6) /
+  // qfac[1][z] - 6000 under which |N'| means the reference's |F/q| < 1 (z = 0,
   // the DC, never fails: 2^30); cz_on = 0 where all-zero chroma N-tiles are
   // too rare to pay for the test (Q > 75)
   int czl[64];

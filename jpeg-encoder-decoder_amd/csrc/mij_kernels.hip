@@ -723,7 +723,13 @@ constexpr int K1M_COEF_IN = 4;   // read coefficient planes (DC differences) ins
 constexpr int K1M_RGB = 8;       // pixels in RGB order (PPM) instead of BGR (encoder.c:133)
 constexpr int K1M_REGIONS = 16;  // per-frame image sizes inside the canvas (region batches)
 constexpr int K1M_AUDIT = 32;    // coefficient variant + every block's straddle decisions (tests)
-constexpr int k1_base(int mode) { return mode & ~(K1M_RGB | K1M_REGIONS | K1M_AUDIT); }
+// measurement only (mij_batch_pattern_floor): the coefficient variant's
+// memory traffic -- persistent grid, tile claims, LDS-DMA one tile ahead,
+// whole-line coefficient stores and raw DCs -- with no colour, DCT or
+// quantisation: its launch time is the floor of K1's access pattern on the
+// box it runs on (bench.py reports K1 beside it)
+constexpr int K1M_FLOOR = 64;
+constexpr int k1_base(int mode) { return mode & ~(K1M_RGB | K1M_REGIONS | K1M_AUDIT | K1M_FLOOR); }
 
 // Waves per workgroup: the coefficient-only variant runs one 12-wave
 // workgroup per CU (3 waves per SIMD: 120 KB of per-wave tile buffers + the
@@ -752,6 +758,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   // audit (tests only): per block the 64 keep/replay decisions of the fast
   // path, exported so they can be compared with tests/tau_check.c's model
   constexpr bool AUDIT = MODE & K1M_AUDIT;
+  constexpr bool FLOOR = MODE & K1M_FLOOR;
   const int2 *const fdims = REG ? a.fdims : nullptr;
   __shared__ __attribute__((aligned(16))) uint8_t s_raw[PIX ? NW : 1][TILE_RAW];
   __shared__ __attribute__((aligned(16))) uint8_t s_tile[PIX ? NW : 1][LDS_WAVE];
@@ -817,6 +824,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
   uint8_t *L = s_tile[PIX ? wave : 0];
   const int g = lane >> 4, bcol = lane & 15;
   const int c4 = lane & 31, pr = lane >> 5;
+  const uint32_t kq = (uint32_t)T->kq[g];  // luma shift of this lane's zigzag group
   const int q_dc[2] = {T->qint[0][0], T->qint[1][0]};
   const bool cz_on = PIX && !AUDIT && T->cz_on;  // wave-uniform
   const Geom &G = a.g;
@@ -903,6 +911,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
       int tn = 0;
       if (lane == 0) tn = atomicAdd(&s_next, 1);
       tn = __builtin_amdgcn_readfirstlane(tn);
+      uint32_t fl_w = 0;  // FLOOR: one word of the tile, so the stores depend on its DMA
       if (PIX) {
         // ---- 1. colour convert + subsample + stage.  Wait for this tile's
         // DMA: the coefficient variant leaves the previous tile's stores in
@@ -915,7 +924,8 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
         else if (DEFER)
           dma_wait_behind_stores();
         K1_PHASE(0);
-        if (!(kflags & K1F_NO_COLOUR)) colour_stage<RGB, !LUT_LDS>(raw, L, c4, pr, lut, !(kflags & K1F_NO_LUT));
+        if (!(kflags & K1F_NO_COLOUR) && !FLOOR) colour_stage<RGB, !LUT_LDS>(raw, L, c4, pr, lut, !(kflags & K1F_NO_LUT));
+        if (FLOOR) fl_w = ((const uint32_t *)raw)[lane];
         wave_lds_sync();
         K1_PHASE(1);
         // ---- stream the wave's next tile into the freed raw buffer -----------
@@ -988,9 +998,17 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
         const auto r16 = __builtin_amdgcn_permlane16_swap(l1, l1, false, false);
         l1 = r16[0] + r16[1];
         const auto r32 = __builtin_amdgcn_permlane32_swap(l1, l1, false, false);
-        // 1.25 * (L1/2 + 64) for the integer DCT and float(N), + 0.095 L1 for
-        // the fp32 roundings of t -+ tau (<= 1.8e-7 |N| with |N| <= 2^19 L1)
-        lc = fmaf((float)(r32[0] + r32[1]), 0.72f, 80.0f);
+        const uint32_t L1 = r32[0] + r32[1];
+        if (nt < 2) {
+          // luma, integer rule: E = floor(L1 / 2) + 1 >= L1 / 2 + the
+          // reference's own FP64 rounding (< 1e-3 in N' units), kept as bits
+          lc = __uint_as_float((L1 >> 1) + 1u);
+        } else {
+          // chroma, fp32 rule: 1.25 * (L1/2 + 64) for the integer DCT and
+          // float(N'), + 0.095 L1 for the fp32 roundings of t -+ tau (<= 1.8e-7
+          // |N'| with |N'| <= 2^19 L1)
+          lc = fmaf((float)L1, 0.72f, 80.0f);
+        }
         const v4i Bf = Bp ^ (int)0x80808080;  // pixel - 128 as int8
 #pragma unroll
         for (int d = 0; d < 3; d++) dct_digit(d, acc, Bf);
@@ -1116,7 +1134,15 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
                       s_st[TOK ? wave : 0], kflags, acz);
         }
       };
-      if (PIX && do_dct) {
+      if (FLOOR) {
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++) {
+          int o[16];
+#pragma unroll
+          for (int k = 0; k < 16; k++) o[k] = (int)(fl_w >> k) & 0xFF;
+          finish(nt, o, false);
+        }
+      } else if (PIX && do_dct) {
         // token variants: N-tile nt + 1's MFMA chain is issued before N-tile
         // nt is quantised, so the wave's own quantisation covers the chain's
         // latency (two accumulator sets live; measured: token K1 3.504 ->
@@ -1178,37 +1204,65 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
               }
             }
           }
-          // trunc(t - tau) is the output; the lane's sums of trunc(t - tau)
-          // and trunc(t + tau) differ iff some coefficient's +-tau interval
-          // straddles a truncation boundary (each hi >= its lo)
-          int slo = 0, shi = 0;
+          // Luma: N' = 2^k t to within E (the A rows carry
+          // 2^s_g / q_z, k = 21 + s_g per lane group).  With a = |N'| (one's
+          // complement for negatives, so a in [|N'| - 1, |N'|]), hi = a + E + 1
+          // and lo = max(a - E, 0) (v_sub_u32 clamp), every multiple m 2^k, m
+          // >= 1, of [|N'| - E, |N'| + E] separates hi >> k from lo >> k; when
+          // none does, |trunc(t)| = hi >> k, and the signed value is ((hi ^ s)
+          // >> k) - s (floor((-x - 1) / 2^k) = -floor(x / 2^k) - 1).  The
+          // lane's hazard: some bit >= k set in the OR of (hi ^ lo).  All ops
+          // but the xor-add issue at the fast VALU rate
+          // (profiles/r05/probe/valu_rate6.txt).  Chroma keeps the fp32 rule:
+          // trunc(t - tau) is the output, and the lane's sums of trunc(t -
+          // tau) and trunc(t + tau) differ iff some coefficient straddles.
+          uint32_t hz;
+          auto lquant = [&](int n, uint32_t E1, uint32_t EE, uint32_t kq, uint32_t &x) -> int {
+            const int sgn = n >> 31;
+            uint32_t hi;
+            asm("v_xad_u32 %0, %1, %2, %3" : "=v"(hi) : "v"(n), "v"(sgn), "v"(E1));
+            uint32_t lo;
+            asm("v_sub_u32_e64 %0, %1, %2 clamp" : "=v"(lo) : "v"(hi), "v"(EE));
+            x = __builtin_amdgcn_bitop3_b32(x, hi, lo, 0xF6);  // x | (hi ^ lo)
+            return ((int)(hi ^ (uint32_t)sgn) >> kq) - sgn;
+          };
           if (kflags & K1F_NO_QUANT) {
 #pragma unroll
             for (int k = 0; k < 16; k++) o[k] = acc[k >> 2][k & 3];
-          } else
+            hz = 0;
+          } else if (nt < 2) {
+            const uint32_t E = __float_as_uint(lc);
+            const uint32_t E1 = E + 1u, EE = 2u * E + 1u;  // hi - EE = a - E
+            uint32_t x = 0;
 #pragma unroll
-          for (int m = 0; m < 4; m++) {
-            const float4 fac = *(const float4 *)&s_fac[comp][16 * g + 4 * m];
-            const f2v lc2 = {lc, lc};
+            for (int k = 0; k < 16; k++) o[k] = lquant(acc[k >> 2][k & 3], E1, EE, kq, x);
+            hz = x >> kq;  // nonzero iff a hazard
+          } else {
+            int slo = 0, shi = 0;
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-              const f2v fa = h ? f2v{fac.z, fac.w} : f2v{fac.x, fac.y};
-              const f2v nf = {(float)acc[m][2 * h], (float)acc[m][2 * h + 1]};
-              // tau = fac * lc + 1e-6, packed over two coefficients
-              const f2v tv = __builtin_elementwise_fma(fa, lc2, (f2v)1.0e-6f);
-              const f2v lo = __builtin_elementwise_fma(nf, fa, -tv);
-              const f2v hi = __builtin_elementwise_fma(nf, fa, tv);
-              const float lo0 = lo[0], lo1 = lo[1], hi0 = hi[0], hi1 = hi[1];
-              const int l0 = (int)lo0, l1 = (int)lo1;
-              o[4 * m + 2 * h] = l0;
-              o[4 * m + 2 * h + 1] = l1;
-              slo += l0 + l1;
-              shi += (int)hi0 + (int)hi1;
+            for (int m = 0; m < 4; m++) {
+              const float4 fac = *(const float4 *)&s_fac[comp][16 * g + 4 * m];
+              const f2v lc2 = {lc, lc};
+#pragma unroll
+              for (int h = 0; h < 2; h++) {
+                const f2v fa = h ? f2v{fac.z, fac.w} : f2v{fac.x, fac.y};
+                const f2v nf = {(float)acc[m][2 * h], (float)acc[m][2 * h + 1]};
+                // tau = fac * lc + 1e-6, packed over two coefficients
+                const f2v tv = __builtin_elementwise_fma(fa, lc2, (f2v)1.0e-6f);
+                const f2v lo = __builtin_elementwise_fma(nf, fa, -tv);
+                const f2v hi = __builtin_elementwise_fma(nf, fa, tv);
+                const float lo0 = lo[0], lo1 = lo[1], hi0 = hi[0], hi1 = hi[1];
+                const int l0 = (int)lo0, l1 = (int)lo1;
+                o[4 * m + 2 * h] = l0;
+                o[4 * m + 2 * h + 1] = l1;
+                slo += l0 + l1;
+                shi += (int)hi0 + (int)hi1;
+              }
             }
+            hz = (uint32_t)(slo ^ shi);  // nonzero iff a hazard
           }
-          const uint32_t hz = (uint32_t)(slo ^ shi);  // nonzero iff a hazard
           // the lane's straddling coefficients, one bit each (same arithmetic
-          // as the sums above, coefficient by coefficient)
+          // as above, coefficient by coefficient)
           auto straddle_mask = [&]() {
             uint32_t mm = 0;
 #pragma unroll
@@ -1216,10 +1270,17 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
 #pragma unroll
               for (int r = 0; r < 4; r++) {
                 const int k = 4 * m + r;
-                const float nf = (float)acc[m][r];
-                const float fa = s_fac[comp][16 * g + k];
-                const float tv = fmaf(fa, lc, 1.0e-6f);
-                mm |= (uint32_t)((int)fmaf(nf, fa, -tv) != (int)fmaf(nf, fa, tv)) << k;
+                if (nt < 2) {
+                  const uint32_t E = __float_as_uint(lc);
+                  uint32_t x = 0;
+                  (void)lquant(acc[m][r], E + 1u, 2u * E + 1u, kq, x);
+                  mm |= (uint32_t)((x >> kq) != 0) << k;
+                } else {
+                  const float nf = (float)acc[m][r];
+                  const float fa = s_fac[comp][16 * g + k];
+                  const float tv = fmaf(fa, lc, 1.0e-6f);
+                  mm |= (uint32_t)((int)fmaf(nf, fa, -tv) != (int)fmaf(nf, fa, tv)) << k;
+                }
               }
             return mm;
           };
@@ -3772,6 +3833,7 @@ int k1_grid(int device, long long ntiles, int mode) {
   int per_cu = 1, nw = 4;
   switch (mode) {
     case K1M_COEF_OUT:
+    case K1M_COEF_OUT | K1M_FLOOR:  // (the grid of the variant it stands for)
       per_cu = k1_blocks_per_cu<K1M_COEF_OUT>();
       nw = k1_waves<K1M_COEF_OUT>();
       break;
@@ -3823,6 +3885,10 @@ hipError_t launch_k1(const K1Args &a, int grid, int mode, hipStream_t s) {
       } else if (a.rgb) launch_k1_mode<K1M_COEF_OUT | K1M_RGB>(a, grid, s);
       else if (a.fdims) launch_k1_mode<K1M_COEF_OUT | K1M_REGIONS>(a, grid, s);
       else launch_k1_mode<K1M_COEF_OUT>(a, grid, s);
+      break;
+    case K1M_COEF_OUT | K1M_FLOOR:
+      if (a.rgb || a.fdims) return hipErrorInvalidValue;  // (plain B, G, R batches only)
+      launch_k1_mode<K1M_COEF_OUT | K1M_FLOOR>(a, grid, s);
       break;
     case K1M_TOK_OUT:
       if (a.rgb) launch_k1_mode<K1M_TOK_OUT | K1M_RGB>(a, grid, s);

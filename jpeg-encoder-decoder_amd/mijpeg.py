@@ -22,7 +22,7 @@ EXPORTS = [
     "mij_set_input_stride", "mij_set_quality", "mij_last_error", "mij_strerror", "mij_last_message",
     "mij_max_jpg_bytes", "mij_encode",
     "mij_batch_create", "mij_batch_destroy", "mij_batch_upload", "mij_batch_set_input",
-    "mij_batch_encode", "mij_batch_keep_coefs", "mij_batch_set_split", "mij_batch_set_overlap", "mij_batch_set_option", "mij_batch_get_option", "mij_batch_dct", "mij_batch_sync", "mij_batch_output",
+    "mij_batch_encode", "mij_batch_keep_coefs", "mij_batch_set_split", "mij_batch_set_overlap", "mij_batch_set_option", "mij_batch_get_option", "mij_batch_dct", "mij_batch_pattern_floor", "mij_batch_sync", "mij_batch_output",
     "mij_batch_lengths", "mij_batch_coefs", "mij_batch_tables", "mij_batch_set_timing",
     "mij_batch_stage_ms", "mij_batch_stage_history", "mij_batch_token_count", "mij_batch_geometry", "mij_batch_replays", "mij_batch_stream", "mij_batch_audit", "mij_batch_build_tables",
     "mij_band_analyze", "mij_band_histograms", "mij_band_tables", "mij_band_pack", "mij_band_words",
@@ -115,6 +115,7 @@ def load() -> C.CDLL:
     lib.mij_batch_set_option.argtypes = [p, i, i]
     lib.mij_batch_get_option.argtypes = [p, i]
     lib.mij_batch_dct.argtypes = [p, i]
+    lib.mij_batch_pattern_floor.argtypes = [p, i]
     lib.mij_batch_audit.argtypes = [p, i, p]
     lib.mij_band_analyze_async.argtypes = [p, i, p]
     lib.mij_band_histograms_async.argtypes = [p, i, p, p]
@@ -404,6 +405,11 @@ class Batch:
 
     def dct(self, n: int) -> None:
         _check(self.lib.mij_batch_dct(self.h_, n), "dct")
+
+    def pattern_floor(self, n: int) -> None:
+        """measurement only: K1's memory traffic without its arithmetic
+        (mij_batch_pattern_floor); leaves garbage in the coefficient planes"""
+        _check(self.lib.mij_batch_pattern_floor(self.h_, n), "pattern_floor")
 
     def sync(self) -> None:
         _check(self.lib.mij_batch_sync(self.h_), "sync")

@@ -10,9 +10,11 @@ issue costs measured on the box (wave-cycles per wave64 instruction at 3
 waves per SIMD, profiles/r03/probe/valu_rate3.txt, valu_rate4.txt,
 profiles/r04/probe/valu_rate5.txt):
 
-  fast class ~2.4: fp32 add/sub/mul/fma/fmac/fmamk, add/sub_u32, and/or/xor,
-                   bitop3, lshrrev/ashrrev, mov_b32 (plain VOP1/VOP2/VOP3
-                   encodings; an SDWA or DPP form is slow)
+  fast class ~2.4: fp32 add/sub/mul/fma/fmac/fmamk, add/sub_u32 (clamp too),
+                   and/or/xor, bitop3, lshrrev/ashrrev, mov_b32 with VGPR,
+                   inline-constant or literal sources (an SGPR source, an
+                   SDWA or a DPP form makes them slow,
+                   profiles/r05/probe/valu_rate6.txt)
   slow class ~4.3: every other VALU (conversions, left shifts, min/max,
                    compares, cndmask, perm, packed ops, bfe, ffbh, bcnt, ...)
   permlane*_swap 8.3, transcendentals 8, an MFMA 16x16 blocks VALU issue 8.
@@ -44,9 +46,17 @@ def cost(op, args):
     if base in TRANS:
         return 8.0
     if base in FAST and "sdwa" not in op and "dpp" not in args and "row_" not in args and "quad_perm" not in args \
-            and "op_sel" not in args and "sel:" not in args:
+            and "op_sel" not in args and "sel:" not in args and not sgpr_src(args):
         return 2.4
     return 4.3
+
+
+def sgpr_src(args):
+    """an SGPR source operand (v_xor_b32 v, s, v issues at 4.4 wave-cycles
+    where the all-VGPR or literal form issues at 2.4:
+    profiles/r05/probe/valu_rate6.txt)"""
+    ops = [o.strip() for o in args.split(",")]
+    return any(re.match(r"^-?\|?s(\d+|\[)", o) for o in ops[1:])
 
 
 def compile_asm(extra):
@@ -130,6 +140,7 @@ def main():
         cur = (0, 0)
         cnt = defaultdict(lambda: [0, 0.0, 0, 0])  # valu, cycles, mfma, lds
         ops = defaultdict(lambda: defaultdict(int))
+        lines = defaultdict(lambda: defaultdict(int))
         for l in body.splitlines():
             s = l.strip()
             mm = re.match(r"\.loc\s+(\d+)\s+(\d+)", s)
@@ -149,6 +160,8 @@ def main():
                     cnt[ph][0] += 1
                 cnt[ph][1] += c
                 ops[ph][re.sub(r"_e(32|64)$", "", op)] += 1
+                if not op.startswith("v_mfma"):
+                    lines[ph][cur[1]] += 1
             elif op.startswith("ds_"):
                 cnt[ph][3] += 1
         print(name)
@@ -159,6 +172,14 @@ def main():
             for i in range(4):
                 tot[i] += v[i]
         print(f"{'total (static)':48s} {tot[0]:6d} {tot[1]:8.0f} {tot[2]:5d} {tot[3]:5d}")
+        for a in sys.argv:
+            if a.startswith("--phase="):
+                want = a.split("=", 1)[1]
+                for ph in ops:
+                    if want in ph:
+                        print(f"  {ph}: " + ", ".join(f"{o[2:]}x{n}" for o, n in
+                                                     sorted(ops[ph].items(), key=lambda kv: -kv[1])))
+                        print("    lines: " + ", ".join(f"{l}:{n}" for l, n in sorted(lines[ph].items())))
         if "-v" in sys.argv:
             for ph in sorted(ops):
                 top = sorted(ops[ph].items(), key=lambda kv: -kv[1])[:14]

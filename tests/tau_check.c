@@ -1,26 +1,30 @@
 /*
  * tests/tau_check.c -- TEST INFRASTRUCTURE: machine check of K1's fast-path
- * decision rule against the reference's FP64 DCT.
+ * decision rules against the reference's FP64 DCT.
  *
  * K1 (jpeg-encoder-decoder_amd/csrc/mij_kernels.hip, k_mcu_dct) computes each
- * AC coefficient as the exact integer N = sum_k W[z][k] * (p_k - 128), with
- * W = llround(C C s_u s_v * 2^19) split into three base-128 int8 digits
- * (fill_tables, mij_api.hip), and quantises it in fp32:
- *     fac = (float)(1 / (2^21 q)),  lc = fmaf(L1, 0.72f, 80.0f),
- *     tv  = fmaf(fac, lc, 1e-6f),  lo = fmaf(N, fac, -tv),  hi = fmaf(N, fac, tv)
- * and keeps trunc(lo) when trunc(lo) == trunc(hi); otherwise it replays the
- * coefficient in FP64 the reference's way.  This program restates those
- * steps bit for bit (C fmaf is the correctly rounded fused multiply-add the
- * GPU's v_fma_f32 / v_pk_fma_f32 perform) and checks, over generated blocks
- * and EVERY quantiser value q that some quality 1..100 produces at that
- * zigzag position of either table (original.c:504-509), that a kept value
- * always equals the reference's (int)(F / q) clipped to [-2048, 2047]
+ * AC coefficient as the exact integer N' = sum_k W'[z][k] * (p_k - 128) of
+ * fill_tables' (mij_api.hip) prescaled matrix: W' = llround(C C s_u s_v *
+ * 2^(19 + s_g) / ql_z), s_g = floor(log2(min luma AC q of zigzag group g =
+ * z / 16)) at the batch's quality, split into three base-128 int8 digits.
+ *   luma (integer rule): E = floor(L1 / 2) + 1, k = 21 + s_g, sgn = N' >> 31,
+ *     hi = (N' ^ sgn) + E + 1, lo = max(hi - (2E + 1), 0); a hazard when
+ *     (hi ^ lo) >> k != 0, else the value ((hi ^ sgn) >> k) - sgn;
+ *   chroma (fp32 rule on the luma-scaled N'): fac = (float)(ql_z / (qc_z
+ *     2^(21 + s_g))), lc = fmaf(L1, 0.72f, 80.0f), tv = fmaf(fac, lc, 1e-6f),
+ *     lo = fmaf(N', fac, -tv), hi = fmaf(N', fac, tv); a hazard when
+ *     trunc(lo) != trunc(hi), else trunc(lo).
+ * This program restates those steps bit for bit (C fmaf is the correctly
+ * rounded fused multiply-add the GPU's v_fma_f32 / v_pk_fma_f32 perform) and
+ * checks, over generated blocks and EVERY quality 1..100 (original.c:504-509:
+ * the weights, shifts and factors all depend on it), that a kept value always
+ * equals the reference's (int)(F / q) clipped to [-2048, 2047]
  * (encoder.c:108-109), F from the oracle's cref_dct_block_f64 (the pinned
  * FP64 restatement of encoder.c:81-106).
  *
  *   tau_check <nblocks> <seed> <threads>
- * prints one JSON line: blocks, checks, kept, hazards, misses, worst ratio of
- * |N - 2^21 F| to the bound L1/2 + 64 the tau formula assumes.
+ * prints one JSON line: blocks, qualities, checks, kept, hazards, misses (luma
+ * and chroma), worst ratio of |N' - 2^(21 + s) F / ql| to the luma bound L1/2.
  * Exit status 1 if any kept value differs from the reference.
  */
 #include <math.h>
@@ -37,12 +41,13 @@ static const int k_zz[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18,
                              35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
                              58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
-static int64_t W[64][64];      /* [zigzag z][pixel k], the digits' value */
-static int qset[64][256];      /* distinct q per zigzag position over Q = 1..100, both tables */
-static int nq[64];
-static float qfac[256];        /* (float)(1 / (2^21 q)) as fill_tables stores it */
-static double qinv[256];       /* 1 / q, the fast screen of the reference's f / q */
-static double basis[8][8];     /* cos((2x+1) u pi / 16), the generators' inverse DCT */
+/* per quality 1..100 (index Q): fill_tables' prescaled weights, shifts, factors */
+static int32_t Wq[101][64][64];    /* [Q][zigzag z][pixel k] */
+static int kq[101][4];             /* 21 + s_g */
+static float facc[101][64];        /* chroma factor */
+static int ql[101][64], qc[101][64];  /* quantisers in zigzag order */
+static double Kx[64][64];          /* C C s_u s_v, exact double */
+static double basis[8][8];         /* cos((2x+1) u pi / 16), the generators' inverse DCT */
 
 static void build_tables(void) {
     double cosd[64];
@@ -54,36 +59,67 @@ static void build_tables(void) {
             double k = cosd[y * 8 + v] * cosd[x * 8 + u];
             if (u == 0) k *= M_SQRT1_2;
             if (v == 0) k *= M_SQRT1_2;
-            const long long w = llround(k * 524288.0);
-            /* the base-128 digits of fill_tables recombine to w exactly */
-            const long long d0 = ((w + 64) & 127) - 64, w1 = (w - d0) >> 7;
-            const long long d1 = ((w1 + 64) & 127) - 64, d2 = (w1 - d1) >> 7;
-            if (d2 < -128 || d2 > 127 || ((d2 << 14) + (d1 << 7) + d0) != w) {
-                fprintf(stderr, "digit split fails at z=%d p=%d\n", z, p);
-                exit(2);
-            }
-            W[z][p] = w;
+            Kx[z][p] = k;
         }
     }
     for (int x = 0; x < 8; x++)
         for (int u = 0; u < 8; u++) basis[x][u] = cos((2 * x + 1) * u * M_PI / 16);
-    for (int q = 1; q < 256; q++) {
-        qfac[q] = (float)(1.0 / (2097152.0 * q));
-        qinv[q] = 1.0 / q;
-    }
-    static unsigned char seen[64][256];
     for (int Q = 1; Q <= 100; Q++) {
         int lq[64], cq[64];
         cref_quality_tables(Q, lq, cq);
-        for (int z = 1; z < 64; z++)
-            for (int t = 0; t < 2; t++) {
-                const int q = t ? cq[k_zz[z]] : lq[k_zz[z]];
-                if (!seen[z][q]) {
-                    seen[z][q] = 1;
-                    qset[z][nq[z]++] = q;
+        for (int z = 0; z < 64; z++) {
+            ql[Q][z] = lq[k_zz[z]];
+            qc[Q][z] = cq[k_zz[z]];
+        }
+        int sg[4];
+        for (int g = 0; g < 4; g++) {
+            int qmin = 256;
+            for (int z = 16 * g; z < 16 * g + 16; z++)
+                if (z && ql[Q][z] < qmin) qmin = ql[Q][z];
+            int s = 0;
+            while ((2 << s) <= qmin) s++;
+            sg[g] = s;
+            kq[Q][g] = 21 + s;
+        }
+        for (int z = 1; z < 64; z++) {
+            facc[Q][z] = (float)((double)ql[Q][z] / ((double)qc[Q][z] * ldexp(1.0, 21 + sg[z >> 4])));
+            for (int p = 0; p < 64; p++) {
+                const long long w = llround(Kx[z][p] * ldexp(1.0, 19 + sg[z >> 4]) / ql[Q][z]);
+                /* the base-128 digits of fill_tables recombine to w exactly */
+                const long long d0 = ((w + 64) & 127) - 64, w1 = (w - d0) >> 7;
+                const long long d1 = ((w1 + 64) & 127) - 64, d2 = (w1 - d1) >> 7;
+                if (d2 < -128 || d2 > 127 || ((d2 << 14) + (d1 << 7) + d0) != w) {
+                    fprintf(stderr, "digit split fails at Q=%d z=%d p=%d\n", Q, z, p);
+                    exit(2);
                 }
+                Wq[Q][z][p] = (int32_t)w;
             }
+        }
     }
+}
+
+/* the luma integer rule: returns 1 on a hazard, else the value in *v */
+static inline int luma_rule(int32_t n, uint32_t E, int k, int *v) {
+    const int32_t sgn = n >> 31;
+    const uint32_t hi = ((uint32_t)n ^ (uint32_t)sgn) + E + 1u;
+    const uint32_t ee = 2u * E + 1u;
+    const uint32_t lo = hi > ee ? hi - ee : 0u;
+    if (((hi ^ lo) >> k) != 0) return 1;
+    *v = ((int32_t)(hi ^ (uint32_t)sgn) >> k) - sgn;
+    return 0;
+}
+/* the chroma fp32 rule */
+static inline int chroma_rule(int32_t n, float fa, float lc, int *v) {
+    const float nf = (float)n;
+    const float tv = fmaf(fa, lc, 1.0e-6f);
+    const int lo = (int)fmaf(nf, fa, -tv), hi = (int)fmaf(nf, fa, tv);
+    if (lo != hi) return 1;
+    *v = lo;
+    return 0;
+}
+static inline int ref_q(double f, int q) {
+    int r = (int)(int16_t)(int)(f / q); /* encoder.c:108 */
+    return r < -2048 ? -2048 : (r > 2047 ? 2047 : r);
 }
 
 /* xorshift64* */
@@ -192,54 +228,39 @@ static void *worker(void *arg) {
             X[k] = px[k] - 128;
             L1 += X[k] < 0 ? -X[k] : X[k];
         }
+        const uint32_t E = (uint32_t)(L1 >> 1) + 1u;
         const float lc = fmaf((float)L1, 0.72f, 80.0f);
-        for (int z = 1; z < 64; z++) {
-            int64_t N = 0;
-            for (int k = 0; k < 64; k++) N += W[z][k] * X[k];
-            const double f = F[k_zz[z]];
-            const double r = fabs((double)N - 2097152.0 * f) / (0.5 * L1 + 64.0);
-            if (r > j->worst) j->worst = r;
-            const float nf = (float)(int32_t)N;
-            /* branch-free over the q values (vectorises); the reference's
-             * (int)(f / q) is formed as trunc(f * (1/q)) and recomputed with
-             * the true division below wherever f / q is near an integer */
-            const int n = nq[z];
-            const int *qs = qset[z];
-            int hz = 0, bad = 0, near = 0;
-            for (int i = 0; i < n; i++) {
-                const int q = qs[i];
-                const float fa = qfac[q];
-                const float tv = fmaf(fa, lc, 1.0e-6f);
-                const int lo = (int)fmaf(nf, fa, -tv), hi = (int)fmaf(nf, fa, tv);
-                const double t = f * qinv[q];
-                const double tr = trunc(t);
-                const double d = fabs(t - tr);
-                near |= (d < 1e-9) | (d > 1.0 - 1e-9);
-                hz += lo != hi;
-                bad += (lo == hi) & (lo != (int)tr);
-            }
-            j->checks += n;
-            j->hazards += hz;
-            j->kept += n - hz;
-            if (bad || near) {  /* exact reference semantics, one q at a time */
-                bad = 0;
-                for (int i = 0; i < n; i++) {
-                    const int q = qs[i];
-                    const float fa = qfac[q];
-                    const float tv = fmaf(fa, lc, 1.0e-6f);
-                    const int lo = (int)fmaf(nf, fa, -tv), hi = (int)fmaf(nf, fa, tv);
-                    if (lo != hi) continue;
-                    int ref = (int)(int16_t)(int)(f / q); /* encoder.c:108 */
-                    ref = ref < -2048 ? -2048 : (ref > 2047 ? 2047 : ref);
-                    if (lo != ref) {
-                        if (!j->misses && !bad) {
+        for (int Q = 1; Q <= 100; Q++) {
+            for (int z = 1; z < 64; z++) {
+                int64_t N = 0;
+                const int32_t *w = Wq[Q][z];
+                for (int k = 0; k < 64; k++) N += (int64_t)w[k] * X[k];
+                if (N > INT32_MAX || N < INT32_MIN) {
+                    fprintf(stderr, "N' overflows int32 at Q=%d z=%d\n", Q, z);
+                    exit(2);
+                }
+                const int kk = kq[Q][z >> 4];
+                const double f = F[k_zz[z]];
+                const double r = fabs((double)N - ldexp(f, kk) / ql[Q][z]) / (0.5 * L1 + 1e-9);
+                if (L1 && r > j->worst) j->worst = r;
+                int v;
+                for (int t = 0; t < 2; t++) {
+                    const int q = t ? qc[Q][z] : ql[Q][z];
+                    const int hz = t ? chroma_rule((int32_t)N, facc[Q][z], lc, &v) : luma_rule((int32_t)N, E, kk, &v);
+                    j->checks++;
+                    if (hz) {
+                        j->hazards++;
+                        continue;
+                    }
+                    j->kept++;
+                    if (v != ref_q(f, q)) {
+                        if (!j->misses) {
                             j->first_miss_z = z;
-                            j->first_miss_q = q;
+                            j->first_miss_q = Q * (t ? -1 : 1);
                         }
-                        bad++;
+                        j->misses++;
                     }
                 }
-                j->misses += bad;
             }
         }
     }
@@ -247,14 +268,11 @@ static void *worker(void *arg) {
 }
 
 /* tau_check dump <nblocks> <seed> <Q> <out>: the generated blocks and, for
- * each, the rule's decision at every AC position under the LUMA table of
+ * each, the rule's decision at every AC position under the LUMA rule of
  * quality Q, for tests/test_tau_kernel.py to compare with K1's own decisions
  * (mij_batch_audit).  Writes <out>.px (nblocks x 64 bytes, row-major) and
- * <out>.mask (nblocks uint64, bit z = zigzag coefficient z straddles a
- * truncation boundary, i.e. trunc(lo) != trunc(hi)). */
+ * <out>.mask (nblocks uint64, bit z = zigzag coefficient z is a hazard). */
 static int dump(long long nblocks, long long seed, int Q, const char *out) {
-    int lq[64], cq[64];
-    cref_quality_tables(Q, lq, cq);
     char path[4096];
     snprintf(path, sizeof path, "%s.px", out);
     FILE *fp = fopen(path, "wb");
@@ -271,15 +289,13 @@ static int dump(long long nblocks, long long seed, int Q, const char *out) {
             X[k] = px[k] - 128;
             L1 += X[k] < 0 ? -X[k] : X[k];
         }
-        const float lc = fmaf((float)L1, 0.72f, 80.0f);
+        const uint32_t E = (uint32_t)(L1 >> 1) + 1u;
         uint64_t m = 0;
         for (int z = 1; z < 64; z++) {
             int64_t N = 0;
-            for (int k = 0; k < 64; k++) N += W[z][k] * X[k];
-            const float nf = (float)(int32_t)N;
-            const float fa = qfac[lq[k_zz[z]]];
-            const float tv = fmaf(fa, lc, 1.0e-6f);
-            if ((int)fmaf(nf, fa, -tv) != (int)fmaf(nf, fa, tv)) m |= 1ull << z;
+            for (int k = 0; k < 64; k++) N += (int64_t)Wq[Q][z][k] * X[k];
+            int v;
+            if (luma_rule((int32_t)N, E, kq[Q][z >> 4], &v)) m |= 1ull << z;
         }
         fwrite(px, 1, 64, fp);
         fwrite(&m, 8, 1, fm);
@@ -310,26 +326,24 @@ int main(int argc, char **argv) {
     }
     job_t tot;
     memset(&tot, 0, sizeof(tot));
-    tot.first_miss_z = tot.first_miss_q = -1;
+    tot.first_miss_z = tot.first_miss_q = 0;
     for (int t = 0; t < nth; t++) {
         pthread_join(th[t], NULL);
         tot.blocks += jobs[t].blocks;
         tot.checks += jobs[t].checks;
         tot.kept += jobs[t].kept;
         tot.hazards += jobs[t].hazards;
-        if (jobs[t].misses && tot.first_miss_z < 0) {
+        if (jobs[t].misses && !tot.misses) {
             tot.first_miss_z = jobs[t].first_miss_z;
             tot.first_miss_q = jobs[t].first_miss_q;
         }
         tot.misses += jobs[t].misses;
         if (jobs[t].worst > tot.worst) tot.worst = jobs[t].worst;
     }
-    int nqt = 0;
-    for (int z = 1; z < 64; z++) nqt += nq[z];
-    printf("{\"blocks\": %lld, \"seed\": %lld, \"q_values_per_block\": %d, \"checks\": %lld, \"kept\": %lld, "
-           "\"hazards\": %lld, \"misses\": %lld, \"first_miss_z\": %d, \"first_miss_q\": %d, "
+    printf("{\"blocks\": %lld, \"seed\": %lld, \"qualities\": 100, \"checks\": %lld, \"kept\": %lld, "
+           "\"hazards\": %lld, \"misses\": %lld, \"first_miss_z\": %d, \"first_miss_Q\": %d, "
            "\"worst_err_over_bound\": %.6f}\n",
-           tot.blocks, seed, nqt, tot.checks, tot.kept, tot.hazards, tot.misses, tot.first_miss_z,
+           tot.blocks, seed, tot.checks, tot.kept, tot.hazards, tot.misses, tot.first_miss_z,
            tot.first_miss_q, tot.worst);
     return tot.misses ? 1 : 0;
 }

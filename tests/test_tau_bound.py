@@ -1,18 +1,20 @@
-"""CPU test: machine check of K1's fast-path quantisation rule (DESIGN.md §5.2,
-verdict r01 item 7).
+"""CPU test: machine check of K1's fast-path quantisation rules (DESIGN.md §5.2,
+verdict r01 item 7, integer-domain luma rule since round 5).
 
 tests/tau_check.c restates bit for bit what k_mcu_dct does per AC coefficient
--- the exact three-digit integer DCT N of fill_tables' int8 matrix, then
-fp32 t -+ tau with tau = fac (0.72 L1 + 80) + 1e-6 -- and asserts that every
-value the kernel keeps (trunc(t - tau) == trunc(t + tau)) equals the
-reference's (int)(F / q) (encoder.c:81-109, F from the oracle's FP64
-restatement), for every quantiser value any quality 1..100 gives at that
-zigzag position of either table (original.c:504-509).  Blocks: random,
-flat, checkerboards, ramps, near-flat noise, 0/255 extremes, DCT basis
-patterns and blocks synthesised onto quantisation boundaries.
+-- the exact three-digit integer DCT N' of fill_tables' int8 matrix, whose
+rows carry the luma prescale 2^s_g / q_z of the batch's quality; then the
+luma integer rule (hi = |N'| + E + 1, lo = max(|N'| - E, 0), a hazard when
+they differ above bit k = 21 + s_g, else a shift) and the chroma fp32 rule
+(t -+ tau with tau = fac (0.72 L1 + 80) + 1e-6 on the luma-scaled N') -- and
+asserts that every value the kernel keeps equals the reference's (int)(F /
+q) (encoder.c:81-109, F from the oracle's FP64 restatement), for every
+quality 1..100 (original.c:504-509) and both tables.  Blocks: random, flat,
+checkerboards, ramps, near-flat noise, 0/255 extremes, DCT basis patterns
+and blocks synthesised onto quantisation boundaries.
 
-Default size 10^6 blocks x 8169 quantiser values (~8e9 decisions, every Q);
-MIJ_TAU_BLOCKS raises it.  tests/golden/tau_check_1e7.json records a 10^7
+Default size 2 x 10^5 blocks x 100 qualities x 126 decisions (~2.5e9);
+MIJ_TAU_BLOCKS raises it.  tests/golden/tau_check_int_1e7.json records a 10^7
 block run of the same program."""
 import json
 import os
@@ -46,19 +48,19 @@ def run(exe, blocks, seed):
 
 
 def test_tau_rule_never_keeps_a_wrong_value(tau_check):
-    n = int(os.environ.get("MIJ_TAU_BLOCKS", "1000000"))
+    n = int(os.environ.get("MIJ_TAU_BLOCKS", "200000"))
     rc, out = run(tau_check, n, 11)
     assert out["misses"] == 0 and rc == 0, out
-    assert out["blocks"] == n and out["q_values_per_block"] > 8000
-    # the integer DCT's error stays inside the bound the rule assumes
-    # (|N - 2^21 F| <= L1/2 + 64), with margin
-    assert out["worst_err_over_bound"] < 0.8, out
+    assert out["blocks"] == n and out["qualities"] == 100
+    # the integer DCT's error stays inside the bound the luma rule assumes
+    # (|N' - 2^k F / q| <= L1/2, the rule's E = floor(L1 / 2) + 1)
+    assert out["worst_err_over_bound"] <= 1.0, out
     # the rule is not vacuous: it keeps nearly everything and flags a few
     assert out["kept"] > 0.999 * out["checks"] and out["hazards"] > 0
 
 
 def test_recorded_1e7_run():
-    with open(os.path.join(HERE, "golden", "tau_check_1e7.json")) as f:
+    with open(os.path.join(HERE, "golden", "tau_check_int_1e7.json")) as f:
         rec = json.load(f)
     assert rec["blocks"] >= 10_000_000 and rec["misses"] == 0
-    assert rec["q_values_per_block"] > 8000
+    assert rec["qualities"] == 100 and rec["worst_err_over_bound"] <= 1.0
