@@ -2678,7 +2678,7 @@ constexpr int pf_occ() { return PW > PACK_WORDS ? PF_OCC_WIDE : PF_OCC; }
 static_assert(PACK_SEGS == 64, "k_pack_flat: one wave scans the group's segments");
 template <int PW, bool FF>
 __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs a) {
-  __shared__ uint32_t buf[PW];
+  __shared__ __attribute__((aligned(16))) uint32_t buf[PW];
   __shared__ uint32_t tab[2 * 256];
   __shared__ uint32_t s_cp[PACK_SEGS + 1];  // exclusive prefix of the segments' chunks; [64]: all
   __shared__ uint32_t s_ws[2][PF_K][PF_WAVES];  // a round's bits per chunk set and wave (two rounds in turn)
@@ -2709,7 +2709,6 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   const int chroma = comp != 0;
   for (int i = tid; i < 512; i += PF_THREADS)
     tab[i] = lb_tab_entry(a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + i], (uint32_t)i & 255u);
-  for (int i = tid; i < PW; i += PF_THREADS) buf[i] = 0;
   uint32_t Lz, zcode;
   {  // the ZRL code (AC symbol 0xF0: cls 0, so the entry is code / length)
     const uint32_t zac = a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + 256 + 0xF0];
@@ -2737,6 +2736,14 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   }
   __syncthreads();
   const uint32_t C = s_cp[PACK_SEGS];
+  // The window is zeroed as far as the group can need it at <= 96 bits per
+  // chunk (3C + 2 words: a chroma group of ~256 chunks zeroes ~770 words, not
+  // the whole window; config-3 luma groups run ~20 bits per chunk at Q=50,
+  // ~70 at Q=90); a chunk that would place past it takes the
+  // window-by-window path, which zeroes its own windows.  16-byte stores;
+  // the sweep's first barrier orders them before any placement.
+  const uint32_t wz = min((uint32_t)PW, (3u * C + 2u + 3u) & ~3u);
+  for (uint32_t i = 4u * tid; i < wz; i += 4u * PF_THREADS) *(u4v *)&buf[i] = u4v{0u, 0u, 0u, 0u};
   const uint32_t *tokg = a.tok + fs0 * SEG_TOK;
   // chunk c's 4 tokens (c < C): its segment s is the last with s_cp[s] <= c
   auto chunk_load = [&](uint32_t c, u4v &t) {
@@ -2771,7 +2778,7 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   // aggregate goes out as soon as the last round's scan has it, before that
   // round is placed.
   auto sweep = [&](bool whole, uint32_t boff, uint32_t lo_bit, uint32_t hi_bit, bool publish) -> uint32_t {
-    const uint32_t lim = (PW - 1) * 32;  // one spare word for the shifted store
+    const uint32_t lim = (wz - 1) * 32;  // the zeroed words, one spare for the shifted store
     uint32_t run = boff;
     bool over = false;
     u4v tn[PF_K];  // the next round's chunks, loaded while a round is placed
