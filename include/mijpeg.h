@@ -159,7 +159,10 @@ int mij_batch_set_overlap(mij_batch *b, int nsub);
  *                         (pack group 0 never runs, the groups after it wait
  *                         on its look-back word); the frame must fail with
  *                         MIJ_EHANG within the wait bound instead of hanging
- *                         the launch.  Consumed by that encode. */
+ *                         the launch.  Consumed by that encode.
+ *   MIJ_OPT_PACK_SEGS     -1 (default: chosen from the quality); otherwise
+ *                         ly + 3 * lc (0..8): the packing's groups take
+ *                         64 << ly luma and 64 << lc chroma segments */
 enum {
   MIJ_OPT_SEAM = 0,
   MIJ_OPT_FF_PACK = 1,
@@ -169,7 +172,8 @@ enum {
   MIJ_OPT_EMIT_SLOTS = 5,
   MIJ_OPT_OVERLAP_PRIO = 6,
   MIJ_OPT_FAULT_TICKET = 7,
-  MIJ_OPT_COUNT = 8
+  MIJ_OPT_PACK_SEGS = 8,
+  MIJ_OPT_COUNT = 9
 };
 int mij_batch_set_option(mij_batch *b, int opt, int value);
 int mij_batch_get_option(mij_batch *b, int opt);

@@ -372,7 +372,7 @@ struct mij_batch {
   hipEvent_t ov_k1[16] = {}, ov_done = nullptr;
   bool timing = false;
   // mij_batch_set_option (include/mijpeg.h): entropy-stage variants
-  int opt[MIJ_OPT_COUNT] = {1, 1, 1, 0, -1, 0, 1, 0};
+  int opt[MIJ_OPT_COUNT] = {1, 1, 1, 0, -1, 0, 1, 0, -1};
   static constexpr int HIST = 64;
   hipEvent_t evh[HIST][MIJ_NSTAGES] = {};  // per-step events while timing is on
   hipEvent_t *ev = evh[0];       // current step's events
@@ -455,9 +455,9 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
     HIP_TRY(dalloc(&b->d_seg_off, F * g.nseg));
     HIP_TRY(dalloc(&b->d_fixmask, F * g.tiles_per_frame * 3));
     HIP_TRY(hipMemsetAsync(b->d_fixmask, 0, sizeof(uint16_t) * F * g.tiles_per_frame * 3, b->stream));
-    HIP_TRY(dalloc(&b->d_pack_state, F * ((g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((g.nsc + PACK_SEGS - 1) / PACK_SEGS))));
+    HIP_TRY(dalloc(&b->d_pack_state, F * pack_stride(g)));
     HIP_TRY(dalloc(&b->d_pack_ticket, F * 3));  // one per scan
-    HIP_TRY(dalloc(&b->d_seam, F * ((g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((g.nsc + PACK_SEGS - 1) / PACK_SEGS))));
+    HIP_TRY(dalloc(&b->d_seam, F * pack_stride(g)));
     HIP_TRY(dalloc(&b->d_regions, F));
   }
   HIP_TRY(dalloc(&b->d_hist, F * 4 * 257));
@@ -589,6 +589,24 @@ static int ent_args_pack_wide(const mij_batch *b) {
   return v >= 0 ? v : (b->quality >= PACK_WIDE_MIN_Q ? 1 : 0);
 }
 
+// the packing's group sizes (64 << ls segments): larger groups spread the
+// per-group fixed cost (ticket, counts, look-back) over more tokens, as long
+// as the group's bits stay inside one LDS window at the quality's typical
+// entropy (MIJ_OPT_PACK_SEGS overrides; A/B profiles/r05/pack_segs)
+static void ent_args_pack_ls(const mij_batch *b, int ls[2]) {
+  const int v = b->opt[MIJ_OPT_PACK_SEGS];
+  if (v >= 0) {
+    ls[0] = v % 3;
+    ls[1] = v / 3;
+    return;
+  }
+  // (config 3, profiles/r05/pack_segs: Q=50 luma 128 / chroma 256 0.43 ms
+  // against 0.63 at 64 / 64; Q=90 luma 64 / chroma 256 1.25 against 1.38;
+  // luma 128 outgrows the window from Q=60: 0.67 against 0.61 at 64)
+  ls[0] = b->quality <= 55 ? 1 : 0;
+  ls[1] = 2;
+}
+
 // band: the mij_band_* calls, whose per-frame DC predictors and in-word scan
 // start bits live in d_dcpred / d_bitbase; every other pipeline reads both as
 // 0 (null), so a band call leaves no state behind for the next encode
@@ -635,9 +653,10 @@ static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0, bool band = false
                  : ((long long)b->g.w * b->g.h >= (8 << 20)) ? 1536
                                                            : 192;
   a.pack_wide = ent_args_pack_wide(b);
+  ent_args_pack_ls(b, a.pack_ls);
   if (f0) {  // sub-batch: frames f0.. of the batch (every per-frame array shifted)
     const Geom &g = b->g;
-    const long long F = f0, gpf = (g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((g.nsc + PACK_SEGS - 1) / PACK_SEGS);
+    const long long F = f0, gpf = pack_stride(g);
     a.coef += F * g.coef_fs;
     a.dc += F * g.nblk;
     a.hist += F * 4 * 257;
@@ -870,7 +889,7 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   // k_emit_write does not zero them after reading.  The other paths (bands,
   // assembly) still OR onto zero: they clear what this leaves (raw_dirty).
   if (b->opt[MIJ_OPT_SEAM] && b->d_seam) {
-    a.seam = b->d_seam + (long long)f0 * ((b->g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((b->g.nsc + PACK_SEGS - 1) / PACK_SEGS));
+    a.seam = b->d_seam + (long long)f0 * pack_stride(b->g);
     // the 0xFF bytes of every emit chunk counted as the words are stored
     // (no k_emit_count pass over the scan words; A/B: MIJ_OPT_FF_PACK=0)
     a.ff_pack = b->opt[MIJ_OPT_FF_PACK] != 0;
@@ -881,18 +900,17 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   }
   // diagnostics (MIJ_PACK_TIME with the diag build): per-group phase times of k_pack_flat
   static const bool ptime = diag_env("MIJ_PACK_TIME", 0) != 0;
-  const long long ngroups = (long long)nframes * ((b->g.nsy + PACK_SEGS - 1) / PACK_SEGS +
-                                                  2 * ((b->g.nsc + PACK_SEGS - 1) / PACK_SEGS));
+  const long long nwords = (long long)nframes * pack_stride(b->g);  // per-group words (look-back, seam)
   if (ptime) {
-    HIP_TRY(hipMalloc(&a.dbg, sizeof(unsigned long long) * 4 * ngroups));
-    HIP_TRY(hipMemsetAsync(a.dbg, 0, sizeof(unsigned long long) * 4 * ngroups, st));
+    HIP_TRY(hipMalloc(&a.dbg, sizeof(unsigned long long) * 6 * nwords));
+    HIP_TRY(hipMemsetAsync(a.dbg, 0, sizeof(unsigned long long) * 6 * nwords, st));
   }
   if (b->opt[MIJ_OPT_FAULT_TICKET] && f0 == 0) {
     // fault injection (tests): frame 0's luma ticket starts past group 0
     const int v = b->opt[MIJ_OPT_FAULT_TICKET];
     b->opt[MIJ_OPT_FAULT_TICKET] = 0;
     if (!a.zero_pack) {
-      HIP_TRY(hipMemsetAsync(a.pack_state, 0, sizeof(unsigned long long) * ngroups, st));
+      HIP_TRY(hipMemsetAsync(a.pack_state, 0, sizeof(unsigned long long) * nwords, st));
       HIP_TRY(hipMemsetAsync(a.pack_ticket, 0, sizeof(unsigned) * 3 * nframes, st));
     }
     HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)a.pack_ticket, v, 1, st));
@@ -902,22 +920,36 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   }
   if (a.seam) HIP_TRY(launch_seam_fix(a, st));
   if (ptime) {
-    std::vector<unsigned long long> h(4 * ngroups);
-    HIP_TRY(hipMemcpyAsync(h.data(), a.dbg, sizeof(unsigned long long) * 4 * ngroups, hipMemcpyDeviceToHost, st));
+    std::vector<unsigned long long> h(6 * nwords);
+    HIP_TRY(hipMemcpyAsync(h.data(), a.dbg, sizeof(unsigned long long) * 6 * nwords, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     HIP_TRY(hipFree(a.dbg));
     a.dbg = nullptr;
-    double ph[3] = {0};
+    // k_pack_flat's stamps: start, counts ready, sweep done, look-back done,
+    // end, [5] ticket and code table in (groups on the windowed path are not
+    // stamped); luma and chroma groups apart
+    const PackGrid P = pack_grid(a);
+    double ph[2][5] = {{0}};
+    long long cnt[2] = {0, 0};
     unsigned long long t0 = ~0ull, t1 = 0;
-    for (long long g = 0; g < ngroups; g++) {
-      const unsigned long long *r = &h[4 * g];
-      for (int k = 0; k < 3; k++) ph[k] += (double)(r[k + 1] - r[k]);
+    for (long long g = 0; g < nwords; g++) {
+      const unsigned long long *r = &h[6 * g];
+      if (!r[4]) continue;
+      const int kind = (g % P.stride) >= P.gy;
+      for (int k = 0; k < 4; k++) ph[kind][k] += (double)(r[k + 1] - r[k]);
+      ph[kind][4] += (double)(r[5] - r[0]);
+      cnt[kind]++;
       t0 = std::min(t0, r[0]);
-      t1 = std::max(t1, r[3]);
+      t1 = std::max(t1, r[4]);
     }
     // s_memrealtime ticks at 100 MHz
-    fprintf(stderr, "pack groups %lld: span %.1f us, per group: ticket+bits %.2f us, look-back %.2f us, pack %.2f us\n",
-            ngroups, (t1 - t0) / 100.0, ph[0] / ngroups / 100.0, ph[1] / ngroups / 100.0, ph[2] / ngroups / 100.0);
+    for (int kind = 0; kind < 2; kind++)
+      if (cnt[kind])
+        fprintf(stderr, "pack %s groups %lld (%d segments): span %.1f us, per group: ticket+counts %.2f us "
+                "(ticket + code table %.2f), sweep %.2f us, look-back %.2f us, store %.2f us\n",
+                kind ? "chroma" : "luma", cnt[kind], PACK_SEGS << a.pack_ls[kind], (t1 - t0) / 100.0,
+                ph[kind][0] / cnt[kind] / 100.0, ph[kind][4] / cnt[kind] / 100.0, ph[kind][1] / cnt[kind] / 100.0,
+                ph[kind][2] / cnt[kind] / 100.0, ph[kind][3] / cnt[kind] / 100.0);
   }
   if (t) HIP_TRY(hipEventRecord(b->ev[6], st));
   HIP_TRY(launch_emit(a, st));
@@ -1134,10 +1166,12 @@ extern "C" int mij_batch_set_overlap(mij_batch *b, int nsub) {
 extern "C" int mij_batch_set_option(mij_batch *b, int opt, int value) {
   if (pipe_check(b, "set_option")) return g_err;
   if (opt < 0 || opt >= MIJ_OPT_COUNT) return fail(MIJ_EINVAL, "set_option: unknown option %d", opt);
-  const bool binary = opt != MIJ_OPT_PACK_WIDE && opt != MIJ_OPT_EMIT_SLOTS && opt != MIJ_OPT_FAULT_TICKET;
+  const bool binary = opt != MIJ_OPT_PACK_WIDE && opt != MIJ_OPT_EMIT_SLOTS && opt != MIJ_OPT_FAULT_TICKET &&
+                      opt != MIJ_OPT_PACK_SEGS;
   if ((binary && value != 0 && value != 1) || (opt == MIJ_OPT_PACK_WIDE && (value < -1 || value > 1)) ||
       (opt == MIJ_OPT_EMIT_SLOTS && (value < 0 || value > 4096)) ||
-      (opt == MIJ_OPT_FAULT_TICKET && (value < 0 || value > 1 << 20)))
+      (opt == MIJ_OPT_FAULT_TICKET && (value < 0 || value > 1 << 20)) ||
+      (opt == MIJ_OPT_PACK_SEGS && (value < -1 || value > 8)))
     return fail(MIJ_EINVAL, "set_option: value %d out of range for option %d", value, opt);
   if (opt == MIJ_OPT_OVERLAP_PRIO && b->stream2)
     return fail(MIJ_EINVAL, "set_option: the overlap stream exists already (set the priority before set_overlap)");

@@ -2408,8 +2408,8 @@ __global__ __launch_bounds__(64) void k_tables_1w(EntArgs a) {
   const int nt = a.tab_dc_only ? 2 : 4, lane = threadIdx.x;
   const int f = blockIdx.x / nt, idx = blockIdx.x - f * nt, t = a.tab_dc_only ? 2 * idx : idx;
   if (a.zero_pack) {  // (k_pack_flat runs next: its state, zeroed here instead of two fills)
-    const long long gpf = (a.g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((a.g.nsc + PACK_SEGS - 1) / PACK_SEGS);
-    for (long long i = 64 * idx + lane; i < gpf; i += 64 * nt) a.pack_state[f * gpf + i] = 0;
+    const long long st = pack_stride(a.g);
+    for (long long i = 64 * idx + lane; i < st; i += 64 * nt) a.pack_state[f * st + i] = 0;
     if (t == 0 && lane < 3) a.pack_ticket[f * 3 + lane] = 0;
   }
 #ifdef MIJ_K1_DIAG
@@ -2530,8 +2530,9 @@ __global__ void k_scan(EntArgs a) {
       if (wh >= (unsigned long long)a.g.raw_words[comp]) {
         a.err[f] = FERR_OVERFLOW;
       } else {
-        if (i % PACK_SEGS == 0) raw[wl] = 0;
-        if (i % PACK_SEGS == PACK_SEGS - 1 || i == ns - 1) raw[wh] = 0;
+        const int gsz = PACK_SEGS << a.pack_ls[comp != 0];  // (the pack groups' first / last words)
+        if (i % gsz == 0) raw[wl] = 0;
+        if (i % gsz == gsz - 1 || i == ns - 1) raw[wh] = 0;
       }
     }
     carry += __shfl(x, 63);
@@ -2569,7 +2570,7 @@ __device__ __forceinline__ void put_bits_window(uint32_t *buf, uint32_t pos, uin
 }
 
 // Pack groups' look-back words (EntArgs::pack_state, one per group of
-// PACK_SEGS segments of one scan): flag << 62 | bits, flag 1 = the group's
+// 64 << pack_ls segments of one scan): flag << 62 | bits, flag 1 = the group's
 // own bit count (aggregate), 2 = the inclusive prefix of its scan.
 constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1;
 
@@ -2639,7 +2640,7 @@ constexpr int EMIT_CW = EMIT_CH / 4;  // stream words per emit chunk
 
 // ===========================================================================
 // k_pack_flat: segment bits, scan offsets and bit packing in one pass
-// (encoder.c:434-502).  Each workgroup takes the next pack group of PACK_SEGS
+// (encoder.c:434-502).  Each workgroup takes the next pack group of 64 << ls
 // segments of one scan (a per-scan ticket keeps groups claimed in scan order,
 // so a look-back only waits on groups that have started).  A pack group's
 // bitstream is its segments' token strings back to back, and K1 pads every
@@ -2675,12 +2676,13 @@ constexpr int PF_THREADS = 256, PF_WAVES = PF_THREADS / 64;
 constexpr int PF_K = 2, PF_OCC = 8, PF_OCC_WIDE = 6;
 template <int PW>
 constexpr int pf_occ() { return PW > PACK_WORDS ? PF_OCC_WIDE : PF_OCC; }
-static_assert(PACK_SEGS == 64, "k_pack_flat: one wave scans the group's segments");
+static_assert(PACK_SEGS_MAX == PF_THREADS, "k_pack_flat: a thread per segment of the widest group");
 template <int PW, bool FF>
 __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t buf[PW];
   __shared__ uint32_t tab[2 * 256];
-  __shared__ uint32_t s_cp[PACK_SEGS + 1];  // exclusive prefix of the segments' chunks; [64]: all
+  __shared__ uint32_t s_cp[PACK_SEGS_MAX + 1];  // exclusive prefix of the segments' chunks; [MAX]: all
+  __shared__ uint32_t s_wt[PF_WAVES];
   __shared__ uint32_t s_ws[2][PF_K][PF_WAVES];  // a round's bits per chunk set and wave (two rounds in turn)
   __shared__ unsigned long long s_prefix;
   __shared__ int s_ticket;
@@ -2689,6 +2691,15 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   constexpr int FFN = PW / EMIT_CW + 2;
   __shared__ uint32_t s_ff[FFN];
   __shared__ uint32_t s_ffnb;
+#ifdef MIJ_K1_DIAG
+  // per-group phase stamps (MIJ_PACK_TIME): start, chunk counts ready, sweep
+  // done, look-back done, end; [5] ticket and code table in
+  unsigned long long pst[6];
+  pst[0] = __builtin_amdgcn_s_memrealtime();
+#define PF_STAMP(k) pst[k] = __builtin_amdgcn_s_memrealtime()
+#else
+#define PF_STAMP(k)
+#endif
   const Geom &G = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (FF && tid < FFN) s_ff[tid] = 0;
@@ -2696,14 +2707,15 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
     s_over = 0;
     s_hung = false;
   }
-  const int gy = (G.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (G.nsc + PACK_SEGS - 1) / PACK_SEGS;
-  const int gpf = gy + 2 * gc;
+  const PackGrid P = pack_grid(a);
+  const int gy = P.gy, gc = P.gc, gpf = P.gpf;
   // the scan from the workgroup's index, the group inside it from the scan's
   // ticket (groups claimed in scan order)
   const int f = blockIdx.x / gpf, bq = blockIdx.x - f * gpf;
   const int comp = bq < gy ? 0 : (bq < gy + gc ? 1 : 2);
   const int sbase = comp == 0 ? 0 : (comp == 1 ? G.nsy : G.nsy + G.nsc), ns = comp == 0 ? G.nsy : G.nsc;
-  const int gscan0 = f * gpf + (comp == 0 ? 0 : gy + (comp == 2 ? gc : 0));
+  const int gscan0 = f * P.stride + (comp == 0 ? 0 : gy + (comp == 2 ? gc : 0));
+  const int pseg = PACK_SEGS << a.pack_ls[comp != 0];  // the group's segments (64, 128 or 256)
   const int nq = comp == 0 ? gy : gc;
   if (tid == 0) s_ticket = (int)atomicAdd(&a.pack_ticket[f * 3 + comp], 1u);
   const int chroma = comp != 0;
@@ -2716,6 +2728,7 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
     zcode = zac & 0xFFFFu;
   }
   __syncthreads();
+  PF_STAMP(5);
   const int q = s_ticket;
   // a ticket past the scan's groups (the ticket word was not reset, or was
   // overwritten): nothing of it belongs to this launch -- flag the frame and
@@ -2725,17 +2738,27 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
     return;
   }
   const int gid = gscan0 + q;
-  const int s0 = q * PACK_SEGS, nsg = min(ns, s0 + PACK_SEGS) - s0;
+  const int s0 = q * pseg, nsg = min(ns, s0 + pseg) - s0;
   const long long fs0 = (long long)f * G.nseg + sbase + s0;  // the group's first segment
-  if (wave == 0) {  // chunks per segment (K1 padded each to a multiple of 4 tokens)
-    const uint32_t nt = lane < nsg ? min(a.seg_ntok[fs0 + lane], (uint32_t)SEG_TOK) : 0u;
+  {  // chunks per segment (K1 padded each to a multiple of 4 tokens), a thread per segment
+    const uint32_t nt = tid < nsg ? min(a.seg_ntok[fs0 + tid], (uint32_t)SEG_TOK) : 0u;
     const uint32_t ch = (nt + 3u) >> 2;
     const uint32_t incl = wave_scan64(ch);
-    s_cp[lane] = lane < nsg ? incl - ch : 0xFFFFFFFFu;  // (no chunk maps past the group)
-    if (lane == 63) s_cp[PACK_SEGS] = incl;
+    if (lane == 63) s_wt[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < PF_WAVES; w++) {
+      const uint32_t v = s_wt[w];
+      tot += v;
+      before += w < wave ? v : 0u;
+    }
+    s_cp[tid] = tid < nsg ? before + incl - ch : 0xFFFFFFFFu;  // (no chunk maps past the group)
+    if (tid == 0) s_cp[PACK_SEGS_MAX] = tot;
   }
   __syncthreads();
-  const uint32_t C = s_cp[PACK_SEGS];
+  const uint32_t C = s_cp[PACK_SEGS_MAX];
+  PF_STAMP(1);
   // The window is zeroed as far as the group can need it at <= 96 bits per
   // chunk (3C + 2 words: a chroma group of ~256 chunks zeroes ~770 words, not
   // the whole window; config-3 luma groups run ~20 bits per chunk at Q=50,
@@ -2751,7 +2774,7 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
     if (c >= C) return;
     int s = 0;
 #pragma unroll
-    for (int step = 32; step; step >>= 1)
+    for (int step = PACK_SEGS_MAX / 2; step; step >>= 1)  // (entries past the group read ~0)
       if (s_cp[s + step] <= c) s += step;
     const uint32_t o = 4u * (c - s_cp[s]);
     t = *(const u4v *)(tokg + (long long)s * SEG_TOK + o);
@@ -2859,6 +2882,7 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   };
   // (the group's aggregate goes out inside the sweep; an empty group's here)
   const uint32_t gbits = sweep(true, 0u, 0u, 0u, true);
+  PF_STAMP(2);
   if (C == 0 && tid == 0 && q > 0)
     __hip_atomic_store(&a.pack_state[gid], LB_AGG | 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // its start bit by decoupled look-back over the groups before it (wave 0;
@@ -2909,6 +2933,7 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
     }
   }
   __syncthreads();
+  PF_STAMP(3);
   if (s_hung) return;  // (its start bit is unknown: nothing is stored)
   uint32_t *raw_scan = a.raw + (long long)f * G.raw_fs +
                        (comp == 0 ? 0 : G.raw_words[0] + (comp == 2 ? G.raw_words[1] : 0));
@@ -2951,6 +2976,11 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
       else raw[i] = v;
     }
     ff_flush((uint32_t)gw);
+#ifdef MIJ_K1_DIAG
+    PF_STAMP(4);
+    if (a.dbg && tid == 0)
+      for (int k = 0; k < 6; k++) a.dbg[(long long)gid * 6 + k] = pst[k];
+#endif
     return;
   }
   // wider than the window: window by window at offsets from the group's
@@ -2989,10 +3019,12 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
 // no zeroing in k_emit_write.
 __global__ __launch_bounds__(256) void k_seam_fix(EntArgs a) {
   const Geom &G = a.g;
-  const int gy = (G.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (G.nsc + PACK_SEGS - 1) / PACK_SEGS, gpf = gy + 2 * gc;
-  const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (g >= (long long)a.nframes * gpf) return;
-  const int f = (int)(g / gpf), bq = (int)(g - (long long)f * gpf);
+  const PackGrid P = pack_grid(a);
+  const int gy = P.gy, gc = P.gc, gpf = P.gpf;
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (long long)a.nframes * gpf) return;
+  const int f = (int)(t / gpf), bq = (int)(t - (long long)f * gpf);
+  const long long g = (long long)f * P.stride + bq;  // the group's look-back word
   const int comp = bq < gy ? 0 : (bq < gy + gc ? 1 : 2);
   const int q = bq - (comp == 0 ? 0 : (comp == 1 ? gy : gy + gc));
   if (q == 0 || a.err[f]) return;  // (a failed frame is dropped by the assembly)
@@ -3984,7 +4016,7 @@ hipError_t launch_band_last(const int16_t *dc, const Geom &g, int n, int16_t *la
 }
 hipError_t launch_band_bound(const EntArgs &a, unsigned long long *acc, unsigned long long *bound, hipStream_t s) {
   const int n = a.nframes;
-  const long long nstate = (long long)n * ((a.g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((a.g.nsc + PACK_SEGS - 1) / PACK_SEGS));
+  const long long nstate = (long long)n * pack_stride(a.g);
   const unsigned grid = (unsigned)std::max((n + 3) / 4, (int)std::min<long long>((nstate + 255) / 256, 64));
   hipLaunchKernelGGL(k_band_bound, dim3(grid), dim3(256), 0, s, a.hist, a.ehuf, n, acc, bound, a.pack_state, nstate,
                      a.pack_ticket);
@@ -4010,10 +4042,9 @@ hipError_t launch_or_shift_pieces(uint32_t *raw, const Geom &g, const uint32_t *
 }
 
 hipError_t launch_pack(const EntArgs &a, hipStream_t s, bool state_zeroed) {
-  const int gy = (a.g.nsy + PACK_SEGS - 1) / PACK_SEGS, gc = (a.g.nsc + PACK_SEGS - 1) / PACK_SEGS;
-  const long long groups = (long long)a.nframes * (gy + 2 * gc);
+  const long long groups = (long long)a.nframes * pack_grid(a).gpf;
   if (!state_zeroed) {
-    hipError_t e = hipMemsetAsync(a.pack_state, 0, sizeof(unsigned long long) * groups, s);
+    hipError_t e = hipMemsetAsync(a.pack_state, 0, sizeof(unsigned long long) * a.nframes * pack_stride(a.g), s);
     if (e == hipSuccess) e = hipMemsetAsync(a.pack_ticket, 0, sizeof(unsigned) * 3 * a.nframes, s);
     if (e != hipSuccess) return e;
   }
@@ -4025,8 +4056,7 @@ hipError_t launch_pack(const EntArgs &a, hipStream_t s, bool state_zeroed) {
   return hipGetLastError();
 }
 hipError_t launch_seam_fix(const EntArgs &a, hipStream_t s) {
-  const long long gpf = (a.g.nsy + PACK_SEGS - 1) / PACK_SEGS + 2 * ((a.g.nsc + PACK_SEGS - 1) / PACK_SEGS);
-  const long long n = (long long)a.nframes * gpf;
+  const long long n = (long long)a.nframes * pack_grid(a).gpf;
   hipLaunchKernelGGL(k_seam_fix, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
