@@ -161,8 +161,8 @@ int mij_batch_set_overlap(mij_batch *b, int nsub);
  *                         MIJ_EHANG within the wait bound instead of hanging
  *                         the launch.  Consumed by that encode.
  *   MIJ_OPT_PACK_SEGS     -1 (default: chosen from the quality); otherwise
- *                         ly + 3 * lc (0..8): the packing's groups take
- *                         64 << ly luma and 64 << lc chroma segments */
+ *                         ly + 4 * lc (0..15): the packing's groups take
+ *                         32 << ly luma and 32 << lc chroma segments */
 enum {
   MIJ_OPT_SEAM = 0,
   MIJ_OPT_FF_PACK = 1,

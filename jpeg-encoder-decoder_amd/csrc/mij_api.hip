@@ -589,22 +589,22 @@ static int ent_args_pack_wide(const mij_batch *b) {
   return v >= 0 ? v : (b->quality >= PACK_WIDE_MIN_Q ? 1 : 0);
 }
 
-// the packing's group sizes (64 << ls segments): larger groups spread the
+// the packing's group sizes (32 << ls segments): larger groups spread the
 // per-group fixed cost (ticket, counts, look-back) over more tokens, as long
 // as the group's bits stay inside one LDS window at the quality's typical
 // entropy (MIJ_OPT_PACK_SEGS overrides; A/B profiles/r05/pack_segs)
 static void ent_args_pack_ls(const mij_batch *b, int ls[2]) {
   const int v = b->opt[MIJ_OPT_PACK_SEGS];
   if (v >= 0) {
-    ls[0] = v % 3;
-    ls[1] = v / 3;
+    ls[0] = v % 4;
+    ls[1] = v / 4;
     return;
   }
-  // (config 3, profiles/r05/pack_segs: Q=50 luma 128 / chroma 256 0.43 ms
-  // against 0.63 at 64 / 64; Q=90 luma 64 / chroma 256 1.25 against 1.38;
-  // luma 128 outgrows the window from Q=60: 0.67 against 0.61 at 64)
-  ls[0] = b->quality <= 55 ? 1 : 0;
-  ls[1] = 2;
+  // (config 3, profiles/r05/pack_segs/ab.txt: luma 128 segments to Q=70,
+  // 64 to Q=92, 32 above; chroma 256 to Q=97, 128 above.  At Q=50 that is
+  // 0.43 ms against 0.63 with 64 / 64; at Q=95 2.0 against 3.6)
+  ls[0] = b->quality <= 70 ? 2 : (b->quality <= 92 ? 1 : 0);
+  ls[1] = b->quality <= 97 ? 3 : 2;
 }
 
 // band: the mij_band_* calls, whose per-frame DC predictors and in-word scan
@@ -1171,7 +1171,7 @@ extern "C" int mij_batch_set_option(mij_batch *b, int opt, int value) {
   if ((binary && value != 0 && value != 1) || (opt == MIJ_OPT_PACK_WIDE && (value < -1 || value > 1)) ||
       (opt == MIJ_OPT_EMIT_SLOTS && (value < 0 || value > 4096)) ||
       (opt == MIJ_OPT_FAULT_TICKET && (value < 0 || value > 1 << 20)) ||
-      (opt == MIJ_OPT_PACK_SEGS && (value < -1 || value > 8)))
+      (opt == MIJ_OPT_PACK_SEGS && (value < -1 || value > 15)))
     return fail(MIJ_EINVAL, "set_option: value %d out of range for option %d", value, opt);
   if (opt == MIJ_OPT_OVERLAP_PRIO && b->stream2)
     return fail(MIJ_EINVAL, "set_option: the overlap stream exists already (set the priority before set_overlap)");

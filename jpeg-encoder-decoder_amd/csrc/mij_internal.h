@@ -37,15 +37,15 @@ constexpr unsigned long long SPIN_TICKS = 10000000ull;
 constexpr int MAX_BLOCK_TOK = 65;                 // DC + 63 AC + EOB
 constexpr int SEG_TOK = 16 * MAX_BLOCK_TOK;       // 1040 tokens per segment slot
 constexpr int SEG_PER_WG = 64;                    // k_seg_bits segments per workgroup
-constexpr int PACK_SEGS = 64;          // segments per k_pack workgroup (at pack_ls 0)
-constexpr int PACK_LS_MAX = 2;         // pack groups of 64 << ls segments, ls <= 2
+constexpr int PACK_SEGS = 32;          // segments per k_pack workgroup at pack_ls 0
+constexpr int PACK_LS_MAX = 3;         // pack groups of 32 << ls segments, ls <= 3
 constexpr int PACK_SEGS_MAX = PACK_SEGS << PACK_LS_MAX;
 constexpr int MAX_BLOCK_BITS = 1729;              // 28 DC + 63 * 27 AC bits
 // k_pack assembles a group in LDS windows of PACK_WORDS words; a group wider
 // than one window (only near worst-case entropy) is packed in several passes.
 constexpr int PACK_WORDS = 4096;
 // the window of the high-quality variant (EntArgs::pack_wide, Q >= 85)
-constexpr int PACK_WIDE_WORDS = 6144;
+constexpr int PACK_WIDE_WORDS = 5888;  // (6 workgroups per CU by LDS)
 static_assert(PACK_WIDE_WORDS > PACK_WORDS, "the wide pack window must be wider than the default one");
 constexpr int PACK_WIDE_MIN_Q = 85;  // qualities from which the wide window is launched
 // JFIF assembly: scans are written in EMIT_CH-byte chunks by EntArgs::
@@ -224,7 +224,7 @@ struct EntArgs {
                                    // set: k_seam_fix ORs them in, nothing needs zeroed buffers)
   int emit_slots;                  // k_emit_count / k_emit_write workgroups per frame (0: EMIT_SLOTS)
   int pack_wide;                   // k_pack_flat with a 2 * PACK_WORDS window (high quality)
-  int pack_ls[2];                  // k_pack_flat groups: 64 << pack_ls[chroma] segments of a scan
+  int pack_ls[2];                  // k_pack_flat groups: 32 << pack_ls[chroma] segments of a scan
   int zero_pack;                   // k_tables_1w also zeroes k_pack_flat's look-back words and tickets
   int seg_dc;                      // k_tables: compute the segment-first DC tokens first (k_seg_dc)
   int tab_dc_only;                 // k_tables_1w: the DC tables only (k_segdc_actab built the AC ones)
@@ -234,13 +234,13 @@ struct EntArgs {
 };
 
 // The packing's groups (k_pack_flat, k_seam_fix): per frame gy luma groups,
-// then gc Cb and gc Cr, of 64 << pack_ls[chroma] segments each; their
-// per-group arrays (pack_state, seam) keep the stride of the 64-segment
+// then gc Cb and gc Cr, of 32 << pack_ls[chroma] segments each; their
+// per-group arrays (pack_state, seam) keep the stride of the 32-segment
 // groups whatever the group size, so per-frame offsets do not depend on it.
 struct PackGrid {
   int gy, gc, gpf, stride;
 };
-__host__ __device__ inline int pack_groups(int ns, int ls) { return (ns + (PACK_SEGS << ls) - 1) >> (6 + ls); }
+__host__ __device__ inline int pack_groups(int ns, int ls) { return (ns + (PACK_SEGS << ls) - 1) >> (5 + ls); }
 __host__ __device__ inline int pack_stride(const Geom &g) { return pack_groups(g.nsy, 0) + 2 * pack_groups(g.nsc, 0); }
 __host__ __device__ inline PackGrid pack_grid(const EntArgs &a) {
   PackGrid p;

@@ -2570,7 +2570,7 @@ __device__ __forceinline__ void put_bits_window(uint32_t *buf, uint32_t pos, uin
 }
 
 // Pack groups' look-back words (EntArgs::pack_state, one per group of
-// 64 << pack_ls segments of one scan): flag << 62 | bits, flag 1 = the group's
+// 32 << pack_ls segments of one scan): flag << 62 | bits, flag 1 = the group's
 // own bit count (aggregate), 2 = the inclusive prefix of its scan.
 constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1;
 
@@ -2640,7 +2640,7 @@ constexpr int EMIT_CW = EMIT_CH / 4;  // stream words per emit chunk
 
 // ===========================================================================
 // k_pack_flat: segment bits, scan offsets and bit packing in one pass
-// (encoder.c:434-502).  Each workgroup takes the next pack group of 64 << ls
+// (encoder.c:434-502).  Each workgroup takes the next pack group of 32 << ls
 // segments of one scan (a per-scan ticket keeps groups claimed in scan order,
 // so a look-back only waits on groups that have started).  A pack group's
 // bitstream is its segments' token strings back to back, and K1 pads every
@@ -2683,6 +2683,12 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   __shared__ uint32_t tab[2 * 256];
   __shared__ uint32_t s_cp[PACK_SEGS_MAX + 1];  // exclusive prefix of the segments' chunks; [MAX]: all
   __shared__ uint32_t s_wt[PF_WAVES];
+  // the first pass's bit offset at every round start (the windowed path
+  // starts a window's sweep at the round it begins in), and the first bit it
+  // could not place
+  constexpr int PF_ROUNDS = (PACK_SEGS_MAX * (SEG_TOK / 4) + PF_K * PF_THREADS - 1) / (PF_K * PF_THREADS);
+  __shared__ uint32_t s_run[PF_ROUNDS + 1];
+  __shared__ uint32_t s_p1;
   __shared__ uint32_t s_ws[2][PF_K][PF_WAVES];  // a round's bits per chunk set and wave (two rounds in turn)
   __shared__ unsigned long long s_prefix;
   __shared__ int s_ticket;
@@ -2706,6 +2712,8 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   if (tid == 0) {
     s_over = 0;
     s_hung = false;
+    s_p1 = ~0u;
+    s_run[0] = 0;
   }
   const PackGrid P = pack_grid(a);
   const int gy = P.gy, gc = P.gc, gpf = P.gpf;
@@ -2715,7 +2723,7 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   const int comp = bq < gy ? 0 : (bq < gy + gc ? 1 : 2);
   const int sbase = comp == 0 ? 0 : (comp == 1 ? G.nsy : G.nsy + G.nsc), ns = comp == 0 ? G.nsy : G.nsc;
   const int gscan0 = f * P.stride + (comp == 0 ? 0 : gy + (comp == 2 ? gc : 0));
-  const int pseg = PACK_SEGS << a.pack_ls[comp != 0];  // the group's segments (64, 128 or 256)
+  const int pseg = PACK_SEGS << a.pack_ls[comp != 0];  // the group's segments (32 to 256)
   const int nq = comp == 0 ? gy : gc;
   if (tid == 0) s_ticket = (int)atomicAdd(&a.pack_ticket[f * 3 + comp], 1u);
   const int chroma = comp != 0;
@@ -2795,19 +2803,28 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   };
   // one sweep over the group's chunks: positions relative to the group's
   // first bit (+ boff); whole: every bit into the window (a chunk past it
-  // sets the overflow flag), else only the bits inside [lo_bit, hi_bit).
-  // A round takes PF_K chunks per thread (chunk c0 + 256 k + tid), all
-  // loaded at once, and needs one barrier; with `publish` the group's
-  // aggregate goes out as soon as the last round's scan has it, before that
-  // round is placed.
+  // sets the overflow flag and is left out), else only the bits inside
+  // [lo_bit, hi_bit), from the round that window starts in to the round that
+  // passes its end.  A round takes PF_K chunks per thread (chunk c0 + 256 k +
+  // tid), all loaded at once, and needs one barrier; with `publish` the
+  // group's aggregate goes out as soon as the last round's scan has it,
+  // before that round is placed.
   auto sweep = [&](bool whole, uint32_t boff, uint32_t lo_bit, uint32_t hi_bit, bool publish) -> uint32_t {
     const uint32_t lim = (wz - 1) * 32;  // the zeroed words, one spare for the shifted store
-    uint32_t run = boff;
+    uint32_t r0 = 0;
+    if (!whole) {  // the last round starting at or before lo_bit (s_run from the whole pass)
+      const uint32_t nr = (C + PF_K * PF_THREADS - 1) / (PF_K * PF_THREADS);
+#pragma unroll
+      for (uint32_t step = 128; step; step >>= 1)
+        if (r0 + step < nr && boff + s_run[r0 + step] <= lo_bit) r0 += step;
+    }
+    uint32_t run = boff + s_run[r0];
     bool over = false;
     u4v tn[PF_K];  // the next round's chunks, loaded while a round is placed
 #pragma unroll
-    for (int k = 0; k < PF_K; k++) chunk_load(k * PF_THREADS + tid, tn[k]);
-    for (uint32_t c0 = 0, r = 0; c0 < C; c0 += PF_K * PF_THREADS, r++) {
+    for (int k = 0; k < PF_K; k++) chunk_load(r0 * PF_K * PF_THREADS + k * PF_THREADS + tid, tn[k]);
+    for (uint32_t c0 = r0 * PF_K * PF_THREADS, r = r0; c0 < C && (whole || run < hi_bit);
+         c0 += PF_K * PF_THREADS, r++) {
       u4v t[PF_K];
 #pragma unroll
       for (int k = 0; k < PF_K; k++) t[k] = tn[k];
@@ -2847,12 +2864,14 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
       }
       if (publish && c0 + PF_K * PF_THREADS >= C && tid == 0 && q > 0)
         __hip_atomic_store(&a.pack_state[gid], LB_AGG | (run - boff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (whole && tid == 0) s_run[r + 1] = run;  // (read after the look-back's barrier)
 #pragma unroll
       for (int k = 0; k < PF_K; k++) {
         const uint32_t n = nb[k], p0 = pos[k];
         if (!n) continue;
         if (whole && p0 + n > lim) {
           over = true;
+          atomicMin(&s_p1, p0);
         } else if (n <= 64) {
           if (whole) put_bits64(buf, p0, acc[k] << (64 - n), n);
           else put_bits64_win(buf, p0, acc[k] << (64 - n), n, lo_bit, hi_bit);
@@ -2983,10 +3002,29 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
 #endif
     return;
   }
-  // wider than the window: window by window at offsets from the group's
-  // first word (boff = its first bit inside that word)
+  // wider than the window: the words the first pass completed (every bit
+  // before the first chunk it left out), then window by window from there at
+  // offsets from the group's first word (boff = its first bit inside that
+  // word), each window's sweep from the round it begins in
   const uint32_t boff = (uint32_t)(prefix & 31);
-  for (uint32_t w0 = 0; w0 < n; w0 += PW) {
+  const uint32_t k1 = min(n, (uint32_t)(((unsigned long long)s_p1 + boff) >> 5));
+  {
+    const uint32_t c0 = (uint32_t)gw / EMIT_CW;
+    for (uint32_t i = tid; i < k1; i += PF_THREADS) {
+      const uint32_t v = __builtin_amdgcn_alignbit(i ? buf[i - 1] : 0u, buf[i], boff);
+      if (FF || a.seam) {
+        if (i == 0 && boff) {
+          a.seam[gid] = v;
+        } else {
+          raw[i] = v;
+          if (FF) ff_add(v, (uint32_t)gw + i, c0);
+        }
+      } else if (i == 0) atomicOr(&raw[i], v);
+      else raw[i] = v;
+    }
+    ff_flush((uint32_t)gw);
+  }
+  for (uint32_t w0 = k1; w0 < n; w0 += PW) {
     const uint32_t wn = min((uint32_t)PW, n - w0);
     __syncthreads();
     for (uint32_t i = tid; i < wn; i += PF_THREADS) buf[i] = 0;

@@ -106,10 +106,11 @@ CASES = [
     ("pack_wide", 0, 90, 20),
     ("emit_slots", 8, 50, 20),
     ("emit_slots", 512, 90, 3),
-    ("pack_segs", 0, 50, 20),  # 64-segment groups throughout
-    ("pack_segs", 8, 50, 20),  # 256-segment groups throughout
-    ("pack_segs", 8, 90, 4),  # (groups past the window: the window-by-window path)
-    ("pack_segs", 4, 75, 6),  # 128 / 128
+    ("pack_segs", 0, 50, 20),  # 32-segment groups throughout
+    ("pack_segs", 5, 50, 20),  # 64 / 64
+    ("pack_segs", 15, 50, 20),  # 256-segment groups throughout
+    ("pack_segs", 15, 90, 4),  # (groups past the window: the window-by-window path)
+    ("pack_segs", 10, 75, 6),  # 128 / 128
 ]
 
 
@@ -143,7 +144,7 @@ def test_overlap_low_priority_same_bytes():
 
 def test_option_validation():
     b = mijpeg.Batch(64, 64, 1)
-    for opt, bad in (("seam", 2), ("pack_wide", 3), ("emit_slots", -1), ("pack_segs", 9), ("pack_segs", -2)):
+    for opt, bad in (("seam", 2), ("pack_wide", 3), ("emit_slots", -1), ("pack_segs", 16), ("pack_segs", -2)):
         with pytest.raises(mijpeg.MijError, match="out of range"):
             b.set_option(opt, bad)
     with pytest.raises(mijpeg.MijError, match="unknown option"):
