@@ -330,12 +330,19 @@ constexpr uint32_t MAGIC_BITS = 0x4B400000u;
 // differences, a min of the Y fractions); the bitmap corrections are
 // applied by y_fix / chroma_fix to the values already staged in LDS, so the
 // common path carries no merge copies.
-// Outputs: y = Y values, cbm/crm = chroma in magic form, fy = fract(Y+.0005),
-// cc/cy = the run holds a possible Cb/Cr resp. Y exception.
+// Y in magic form too (round 5): fl(Y + 1.5 * 2^13) rounds Y to a multiple
+// of 2^-10, so its bits are 0x46400000 + round(1024 Y); with the fp32 chain
+// within 2e-5 of the exact value, floor(Y) is bits 10-17 and an integer Y
+// is exactly "low 10 bits zero" (non-integers are >= 1e-3 away: their low
+// bits lie in [1, 1023]).  tests/colour_check.c checks both over all 2^24
+// colours.  This replaced a +0.0005 bias, a truncating conversion and a
+// fract per pixel (two slow-class VALU ops) by one fast shift and one AND.
+// Outputs: yb = Y in magic form, cbm/crm = chroma in magic form, cc/cy = the
+// run holds a possible Cb/Cr resp. Y exception.
+constexpr float YMAGIC = 12288.0f;  // 1.5 * 2^13
 struct Run4 {
-  int y[4];
+  uint32_t yb[4];
   uint32_t cbm[4], crm[4];
-  float fy[4];
   bool cc, cy;
 };
 
@@ -355,7 +362,7 @@ __device__ __forceinline__ void convert4(uint32_t w0, uint32_t w1, uint32_t w2, 
     db[h] = fb[h] - fg[h];
     const f2v yf = pk_add_k(__builtin_elementwise_fma((f2v)0.114f, db[h],
                                                       __builtin_elementwise_fma((f2v)0.299f, dr[h], fg[h])),
-                            0.0005f);
+                            YMAGIC);
     const f2v cb = pk_add_k(__builtin_elementwise_fma((f2v)-0.168736f, dr[h],
                                                       __builtin_elementwise_fma((f2v)0.5f, db[h], (f2v)CH_BIAS)),
                             MAGIC);
@@ -367,8 +374,7 @@ __device__ __forceinline__ void convert4(uint32_t w0, uint32_t w1, uint32_t w2, 
       // (element copies first: __builtin_bit_cast of a vector element
       // subscript yields element 0 with this compiler)
       const float ye = yf[e], cbe = cb[e], cre = cr[e];
-      o.y[2 * h + e] = (int)ye;
-      o.fy[2 * h + e] = __builtin_amdgcn_fractf(ye);
+      o.yb[2 * h + e] = __float_as_uint(ye);
       o.cbm[2 * h + e] = __float_as_uint(cbe);
       o.crm[2 * h + e] = __float_as_uint(cre);
     }
@@ -377,18 +383,43 @@ __device__ __forceinline__ void convert4(uint32_t w0, uint32_t w1, uint32_t w2, 
   // differences is 0 (|product| <= 255^8, no underflow or overflow)
   const f2v pd = (dr[0] * db[0]) * (dr[1] * db[1]);
   o.cc = pd[0] * pd[1] == 0.0f;
-  // some pixel has an exact-integer Y: fract(Y + 0.0005) < 0.001
-  o.cy = fminf(fminf(o.fy[0], o.fy[1]), fminf(o.fy[2], o.fy[3])) < 0.001f;
+  // some pixel has an exact-integer Y: the low 10 bits of its magic form are 0
+  const uint32_t m01 = min(o.yb[0] & 0x3FFu, o.yb[1] & 0x3FFu), m23 = min(o.yb[2] & 0x3FFu, o.yb[3] & 0x3FFu);
+  o.cy = min(m01, m23) == 0u;
+}
+
+// The reference's colour expressions in FP64, operation for operation
+// (encoder.c:133-135: left to right, no contraction), truncated to uint8_t
+// (k_fix_blocks' recomputation of listed blocks).
+__device__ __forceinline__ int y_f64(uint32_t R, uint32_t G, uint32_t B) {
+  const double y = __dadd_rn(__dadd_rn(__dmul_rn(0.299, (double)R), __dmul_rn(0.587, (double)G)),
+                             __dmul_rn(0.114, (double)B));
+  return (int)(uint8_t)(int)y;
+}
+__device__ __forceinline__ int cb_f64(uint32_t R, uint32_t G, uint32_t B) {
+  const double v = __dadd_rn(__dadd_rn(__dadd_rn(128.0, -__dmul_rn(0.168736, (double)R)),
+                                       -__dmul_rn(0.331264, (double)G)),
+                             __dmul_rn(0.5, (double)B));
+  return (int)(uint8_t)(int)v;
+}
+__device__ __forceinline__ int cr_f64(uint32_t R, uint32_t G, uint32_t B) {
+  const double v = __dadd_rn(__dadd_rn(__dadd_rn(128.0, __dmul_rn(0.5, (double)R)),
+                                       -__dmul_rn(0.418688, (double)G)),
+                             -__dmul_rn(0.081312, (double)B));
+  return (int)(uint8_t)(int)v;
 }
 
 // Rare path: the Y corrections of a run as a packed byte-wise subtrahend.
 // Only the pixel slots that hold an exact-integer Y in some lane pay for a
 // bitmap read (one wave-uniform branch per slot), and the read walks the
 // lanes that need it with scalar loads: a vector load's s_waitcnt vmcnt(0)
-// would also wait for every token store still in flight.
+// would also wait for every token store still in flight.  (Measured and
+// dropped, round 5: the flagged lanes evaluating the reference's FP64
+// expression (y_f64) instead of the walk -- token K1 2.96 -> 3.01 ms at Q=50,
+// 4.56 -> 4.63 at Q=90: more code and SGPR spills in the colour stage.)
 // (GLOBAL_LUT false: the bitmap is in LDS, read per lane)
 template <bool RGB, bool GLOBAL_LUT>
-__device__ __forceinline__ uint32_t y_fix(uint32_t w0, uint32_t w1, uint32_t w2, const float (&fy)[4],
+__device__ __forceinline__ uint32_t y_fix(uint32_t w0, uint32_t w1, uint32_t w2, const uint32_t (&yb)[4],
                                           const uint32_t *__restrict__ lut, int lane) {
   const uint32_t Gv[4] = {(w0 >> 8) & 255, w1 & 255, w1 >> 24, (w2 >> 16) & 255};
   const uint32_t B0[4] = {w0 & 255, w0 >> 24, (w1 >> 16) & 255, (w2 >> 8) & 255};
@@ -399,7 +430,7 @@ __device__ __forceinline__ uint32_t y_fix(uint32_t w0, uint32_t w1, uint32_t w2,
   uint32_t corr = 0;
 #pragma unroll
   for (int p = 0; p < 4; p++) {
-    const bool ey = fy[p] < 0.001f;
+    const bool ey = (yb[p] & 0x3FFu) == 0u;
     unsigned long long m = __ballot(ey);
     if (m && !GLOBAL_LUT) {
       const uint32_t i = (Rv[p] << 7) | (Gv[p] >> 1);  // integer Y needs R == G (mod 2)
@@ -461,8 +492,11 @@ __device__ __forceinline__ void chroma_fix(uint32_t w0, uint32_t w1, uint32_t w2
   }
 }
 
-__device__ __forceinline__ uint32_t pack_y(const int (&y)[4]) {
-  return (uint32_t)y[0] | ((uint32_t)y[1] << 8) | ((uint32_t)y[2] << 16) | ((uint32_t)y[3] << 24);
+// the four floor(Y) bytes of a run (bits 10-17 of the magic forms): fast
+// right shifts, then two byte permutes and an OR
+__device__ __forceinline__ uint32_t pack_y(const uint32_t (&yb)[4]) {
+  const uint32_t s0 = yb[0] >> 10, s1 = yb[1] >> 10, s2 = yb[2] >> 10, s3 = yb[3] >> 10;
+  return __builtin_amdgcn_perm(s1, s0, 0x0c0c0400u) | __builtin_amdgcn_perm(s3, s2, 0x04000c0cu);
 }
 
 // encoder.c:137-138 -- floor((a+b+c+d)/4) of the truncated values of the
@@ -501,7 +535,7 @@ __device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int
       const int yrow = 2 * rp + dy;  // 0..15
       const int by = yrow >> 3, bx = c4 >> 1;
       Yd[dy] = (uint32_t *)(L + (by * 16 + bx) * LDS_BLK + (yrow & 7) * 8 + (c4 & 1) * 4);
-      py[dy] = pack_y(r[dy].y);
+      py[dy] = pack_y(r[dy].yb);
       *Yd[dy] = py[dy];
     }
     uint8_t *C0 = L + (32 + (c4 >> 2)) * LDS_BLK + rp * 8 + ((2 * c4) & 7);
@@ -512,7 +546,7 @@ __device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int
 #pragma unroll
     for (int dy = 0; dy < 2; dy++)
       if (__ballot(r[dy].cy)) {
-        const uint32_t corr = y_fix<RGB, GLOBAL_LUT>(w[it][dy][0], w[it][dy][1], w[it][dy][2], r[dy].fy, lut,
+        const uint32_t corr = y_fix<RGB, GLOBAL_LUT>(w[it][dy][0], w[it][dy][1], w[it][dy][2], r[dy].yb, lut,
                                                      c4 | (pr << 5));
         if (corr) *Yd[dy] = py[dy] - corr;  // no borrows: a corrected Y is >= 1
       }
@@ -622,14 +656,16 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
   const int dc0 = o[0];
   const int prev = (int)row_shr0<1>((uint32_t)dc0);
   wave_lds_sync();
+  if (pos == (chroma ? 7 : 15)) {
+    if (g == 0) *segcnt = incl;
+    // the segment's token count padded to a multiple of 4 with LB_NOTOK
+    // (k_pack_flat decodes 4-token chunks: a lane's slots are then all
+    // tokens or all padding, and no token needs a mask); the last block's
+    // lanes g < pads write one slot each (all four hold the same incl), where
+    // a loop in one lane cost the wave a dozen instructions per pad
+    if ((uint32_t)g < ((0u - incl) & 3u)) tok_at(segtok, segoff + incl + (uint32_t)g) = LB_NOTOK;
+  }
   if (g == 0) {
-    if (pos == (chroma ? 7 : 15)) {
-      *segcnt = incl;
-      // the segment's token count padded to a multiple of 4 with LB_NOTOK
-      // (k_pack_flat decodes 4-token chunks: a lane's slots are then all
-      // tokens or all padding, and no token needs a mask)
-      for (uint32_t i = incl; i & 3u; i++) tok_at(segtok, segoff + i) = LB_NOTOK;
-    }
     if (valid) {
       if (dc_diffed || pos != 0 || first_pred) {
         const int diff = dc_diffed ? dc0 : dc0 - (pos != 0 ? prev : pred0);  // :168-177
@@ -1224,7 +1260,10 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
             uint32_t lo;
             asm("v_sub_u32_e64 %0, %1, %2 clamp" : "=v"(lo) : "v"(hi), "v"(EE));
             x = __builtin_amdgcn_bitop3_b32(x, hi, lo, 0xF6);  // x | (hi ^ lo)
-            return ((int)(hi ^ (uint32_t)sgn) >> kq) - sgn;
+            // without a hazard hi >> k == lo >> k, and |N'| lies between them:
+            // the truncation is (N' >> k) - sgn (floor, +1 for negatives),
+            // two fast ops (tests/tau_check.c restates this form)
+            return (n >> kq) - sgn;
           };
           if (kflags & K1F_NO_QUANT) {
 #pragma unroll
@@ -1453,23 +1492,9 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
 // coefficient l.  Persistent grid over the device-side list length.
 // ===========================================================================
 // px = B, G, R (ib = 0, ir = 2) or R, G, B (ib = 2, ir = 0)
-__device__ __forceinline__ int y_ref(const uint8_t *px, int ib, int ir) {
-  const double y = __dadd_rn(__dadd_rn(__dmul_rn(0.299, (double)px[ir]), __dmul_rn(0.587, (double)px[1])),
-                             __dmul_rn(0.114, (double)px[ib]));
-  return (int)(uint8_t)(int)y;
-}
-__device__ __forceinline__ int cb_ref(const uint8_t *px, int ib, int ir) {
-  const double v = __dadd_rn(__dadd_rn(__dadd_rn(128.0, -__dmul_rn(0.168736, (double)px[ir])),
-                                       -__dmul_rn(0.331264, (double)px[1])),
-                             __dmul_rn(0.5, (double)px[ib]));
-  return (int)(uint8_t)(int)v;
-}
-__device__ __forceinline__ int cr_ref(const uint8_t *px, int ib, int ir) {
-  const double v = __dadd_rn(__dadd_rn(__dadd_rn(128.0, __dmul_rn(0.5, (double)px[ir])),
-                                       -__dmul_rn(0.418688, (double)px[1])),
-                             -__dmul_rn(0.081312, (double)px[ib]));
-  return (int)(uint8_t)(int)v;
-}
+__device__ __forceinline__ int y_ref(const uint8_t *px, int ib, int ir) { return y_f64(px[ir], px[1], px[ib]); }
+__device__ __forceinline__ int cb_ref(const uint8_t *px, int ib, int ir) { return cb_f64(px[ir], px[1], px[ib]); }
+__device__ __forceinline__ int cr_ref(const uint8_t *px, int ib, int ir) { return cr_f64(px[ir], px[1], px[ib]); }
 
 // The blocks come from K1's per-N-tile fix masks (K1Args::fix_mask): each
 // wave scans 64 masks per step, takes the nonzero ones in turn, zeroes them

@@ -9,7 +9,8 @@
  * z / 16)) at the batch's quality, split into three base-128 int8 digits.
  *   luma (integer rule): E = floor(L1 / 2) + 1, k = 21 + s_g, sgn = N' >> 31,
  *     hi = (N' ^ sgn) + E + 1, lo = max(hi - (2E + 1), 0); a hazard when
- *     (hi ^ lo) >> k != 0, else the value ((hi ^ sgn) >> k) - sgn;
+ *     (hi ^ lo) >> k != 0, else the value (N' >> k) - sgn (round 5; equal to
+ *     ((hi ^ sgn) >> k) - sgn whenever no hazard: N' lies between lo and hi);
  *   chroma (fp32 rule on the luma-scaled N'): fac = (float)(ql_z / (qc_z
  *     2^(21 + s_g))), lc = fmaf(L1, 0.72f, 80.0f), tv = fmaf(fac, lc, 1e-6f),
  *     lo = fmaf(N', fac, -tv), hi = fmaf(N', fac, tv); a hazard when
@@ -105,7 +106,7 @@ static inline int luma_rule(int32_t n, uint32_t E, int k, int *v) {
     const uint32_t ee = 2u * E + 1u;
     const uint32_t lo = hi > ee ? hi - ee : 0u;
     if (((hi ^ lo) >> k) != 0) return 1;
-    *v = ((int32_t)(hi ^ (uint32_t)sgn) >> k) - sgn;
+    *v = (n >> k) - sgn;
     return 0;
 }
 /* the chroma fp32 rule */
