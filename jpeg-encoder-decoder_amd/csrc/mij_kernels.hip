@@ -620,13 +620,16 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
   // flag at bit 2k and 2k+1's at bit 16+2k
   // (v_pk_min_u16 in asm: the compiler rewrites min(h, 1) into compares and
   // selects, three times the instructions)
-  uint32_t pm = 0;
+  // (the flags gathered by a v_lshl_or chain: left to itself the compiler
+  // emits a separate shift per word and v_or3 trees, ~1.5x the cycles)
+  uint32_t pm;
+  asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(pm) : "v"(c0[0]));
 #pragma unroll
-  for (int k = 0; k < 8; k++) {
+  for (int k = 1; k < 8; k++) {
     const uint32_t w = k < 4 ? c0[k] : c1[k - 4];
     uint32_t h;
     asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(h) : "v"(w));
-    pm |= h << (2 * k);
+    asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(pm) : "v"(h), "i"(2 * k), "v"(pm));
   }
   uint32_t m16 = (pm & 0x5555u) | ((pm >> 15) & 0xAAAAu);
   if (g == 0) m16 &= ~1u;  // the DC is not part of the AC run structure
@@ -644,14 +647,12 @@ __device__ __forceinline__ void emit_tokens(const int (&o)[16], int lane, int g,
   // 8-block segments: Cb | Cr; a luma row is one 16-block segment, where the
   // zero fill of row_shr already stops the scan at the row start)
   const int pos = chroma ? (bcol & 7) : bcol;
-  uint32_t incl = (uint32_t)n;
-  if (chroma) {
-    incl += row_shr0<1>(incl) & (pos >= 1 ? ~0u : 0u);
-    incl += row_shr0<2>(incl) & (pos >= 2 ? ~0u : 0u);
-    incl += row_shr0<4>(incl) & (pos >= 4 ? ~0u : 0u);
-  } else {
-    incl = row_scan16(incl);
-  }
+  // (chroma: the row's scan minus, in the Cr half, the Cb half's total --
+  // DPP row_newbcast:7 -- where three masked half-row steps cost twice the
+  // cycles with their lane-mask selects)
+  uint32_t incl = row_scan16((uint32_t)n);
+  if (chroma)
+    incl -= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x157, 0xF, 0xF, false) & (0u - (uint32_t)(bcol >> 3));
   const int base = (int)incl - n;
   const int dc0 = o[0];
   const int prev = (int)row_shr0<1>((uint32_t)dc0);
@@ -1253,6 +1254,10 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
           // trunc(t - tau) is the output, and the lane's sums of trunc(t -
           // tau) and trunc(t + tau) differ iff some coefficient straddles.
           uint32_t hz;
+          // per M-tile: luma, the OR of (hi ^ lo) of its 4 coefficients;
+          // chroma, [0] and [1] the sums of trunc(t - tau) and trunc(t + tau)
+          // over M-tiles 0-1, [2] and [3] over M-tiles 2-3
+          uint32_t xq[4] = {0u, 0u, 0u, 0u};
           auto lquant = [&](int n, uint32_t E1, uint32_t EE, uint32_t kq, uint32_t &x) -> int {
             const int sgn = n >> 31;
             uint32_t hi;
@@ -1272,10 +1277,11 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
           } else if (nt < 2) {
             const uint32_t E = __float_as_uint(lc);
             const uint32_t E1 = E + 1u, EE = 2u * E + 1u;  // hi - EE = a - E
-            uint32_t x = 0;
+            // one OR per M-tile (4 coefficients): the rare path recomputes only
+            // the M-tiles some lane flags
 #pragma unroll
-            for (int k = 0; k < 16; k++) o[k] = lquant(acc[k >> 2][k & 3], E1, EE, kq, x);
-            hz = x >> kq;  // nonzero iff a hazard
+            for (int k = 0; k < 16; k++) o[k] = lquant(acc[k >> 2][k & 3], E1, EE, kq, xq[k >> 2]);
+            hz = (xq[0] | xq[1] | xq[2] | xq[3]) >> kq;  // nonzero iff a hazard
           } else {
             int slo = 0, shi = 0;
 #pragma unroll
@@ -1297,15 +1303,25 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
                 slo += l0 + l1;
                 shi += (int)hi0 + (int)hi1;
               }
+              if (m == 1) {
+                xq[0] = (uint32_t)slo;
+                xq[1] = (uint32_t)shi;
+              }
             }
+            xq[2] = (uint32_t)slo;
+            xq[3] = (uint32_t)shi;
             hz = (uint32_t)(slo ^ shi);  // nonzero iff a hazard
           }
           // the lane's straddling coefficients, one bit each (same arithmetic
-          // as above, coefficient by coefficient)
-          auto straddle_mask = [&]() {
+          // as above, coefficient by coefficient), in the M-tiles `need` flags
+          // for some lane of the wave (a wave-uniform branch per M-tile: a
+          // hazard usually sits in one of them, where recomputing all 16
+          // coefficients cost the wave ~100 instructions per rare-path entry)
+          auto straddle_mask = [&](uint32_t need) {
             uint32_t mm = 0;
 #pragma unroll
-            for (int m = 0; m < 4; m++)
+            for (int m = 0; m < 4; m++) {
+              if (!__ballot((need >> m) & 1u)) continue;
 #pragma unroll
               for (int r = 0; r < 4; r++) {
                 const int k = 4 * m + r;
@@ -1321,11 +1337,23 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
                   mm |= (uint32_t)((int)fmaf(nf, fa, -tv) != (int)fmaf(nf, fa, tv)) << k;
                 }
               }
+            }
             return mm;
+          };
+          // the M-tiles with a hazard in this lane
+          auto need_mtiles = [&]() -> uint32_t {
+            if (nt < 2) {
+              uint32_t nd = 0;
+#pragma unroll
+              for (int m = 0; m < 4; m++) nd |= (uint32_t)((xq[m] >> kq) != 0u) << m;
+              return nd;
+            }
+            const uint32_t d01 = xq[0] != xq[1], d23 = (xq[2] - xq[0]) != (xq[3] - xq[1]);
+            return d01 * 3u + d23 * 12u;
           };
           if constexpr (AUDIT) {
             int blk;
-            if (block_of(nt, blk)) a.audit[((long long)p.f * G.nblk + blk) * 4 + g] = (uint16_t)straddle_mask();
+            if (block_of(nt, blk)) a.audit[((long long)p.f * G.nblk + blk) * 4 + g] = (uint16_t)straddle_mask(0xFu);
           }
           {  // z = 0: exact from the pixel sum (fac = 0 above)
             bool tie;
@@ -1355,7 +1383,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
           if (!DEFER && __ballot(hz != 0) && !(kflags & K1F_NO_REPLAY)) {
             // rare path: find the straddling coefficients (same arithmetic) and
             // recompute them in FP64 exactly as encoder.c:87-109
-            uint32_t mm = straddle_mask();
+            uint32_t mm = straddle_mask(need_mtiles());
             nrep += (uint32_t)__popc(mm);
             if constexpr (TOK) {
               // The wave's straddles listed (lane << 4 | k, in the wave's
@@ -1407,6 +1435,11 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
                 }
                 wave_lds_sync();
                 {
+                  // (Measured and dropped, round 5: per slot some lane replayed
+                  // a wave-uniform branch, or a wave-uniform walk of the list
+                  // writing o[k] by scalar index -- both no faster at Q=50 and
+                  // 0.3-0.5% slower at Q=90 than this per-lane select chain,
+                  // the first with three times the SGPR spills.)
                   uint32_t m2 = mm;
                   for (int idx = base; m2; idx++) {
                     const int k = __ffs(m2) - 1;
