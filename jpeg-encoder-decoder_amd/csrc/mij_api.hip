@@ -593,7 +593,7 @@ static int ent_args_pack_wide(const mij_batch *b) {
 // per-group fixed cost (ticket, counts, look-back) over more tokens, as long
 // as the group's bits stay inside one LDS window at the quality's typical
 // entropy (MIJ_OPT_PACK_SEGS overrides; A/B profiles/r05/pack_segs)
-static void ent_args_pack_ls(const mij_batch *b, int ls[2]) {
+static void ent_args_pack_ls(const mij_batch *b, int nframes, int ls[2]) {
   const int v = b->opt[MIJ_OPT_PACK_SEGS];
   if (v >= 0) {
     ls[0] = v % 4;
@@ -605,6 +605,13 @@ static void ent_args_pack_ls(const mij_batch *b, int ls[2]) {
   // 0.43 ms against 0.63 with 64 / 64; at Q=95 2.0 against 3.6)
   ls[0] = b->quality <= 70 ? 2 : (b->quality <= 92 ? 1 : 0);
   ls[1] = b->quality <= 97 ? 3 : 2;
+  // A small batch cannot fill the GPU with large groups, and then a group's
+  // latency is the packing's: smaller groups until the launch has about half
+  // of the 2048 workgroups 256 CUs hold (one 1920x1280 frame: 32-segment
+  // groups, pack 31 -> 23 us)
+  const long long nf = nframes > 0 ? nframes : 1;
+  while (ls[0] > 0 && nf * pack_groups(b->g.nsy, ls[0]) < 1024) ls[0]--;
+  while (ls[1] > 0 && nf * 2 * pack_groups(b->g.nsc, ls[1]) < 1024) ls[1]--;
 }
 
 // band: the mij_band_* calls, whose per-frame DC predictors and in-word scan
@@ -653,7 +660,7 @@ static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0, bool band = false
                  : ((long long)b->g.w * b->g.h >= (8 << 20)) ? 1536
                                                            : 192;
   a.pack_wide = ent_args_pack_wide(b);
-  ent_args_pack_ls(b, a.pack_ls);
+  ent_args_pack_ls(b, nframes, a.pack_ls);
   if (f0) {  // sub-batch: frames f0.. of the batch (every per-frame array shifted)
     const Geom &g = b->g;
     const long long F = f0, gpf = pack_stride(g);
