@@ -371,6 +371,7 @@ struct mij_batch {
   hipStream_t stream2 = nullptr;
   hipEvent_t ov_k1[16] = {}, ov_done = nullptr;
   bool timing = false;
+  int k1_err_zero = 0;  // frames whose error words the next run_k1 zeroes
   // mij_batch_set_option (include/mijpeg.h): entropy-stage variants
   int opt[MIJ_OPT_COUNT] = {1, 1, 1, 0, -1, 0, 1, 0, -1};
   static constexpr int HIST = 64;
@@ -717,6 +718,11 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int se
   k.audit = b->audit && mode == 1 ? b->d_audit : nullptr;
   k.rgb = b->rgb && (mode & 4) == 0;  // pixel-input variants
   k.fdims = b->use_fdims ? b->d_fdims : nullptr;
+  if (b->k1_err_zero) {  // the encode's first K1 zeroes its error words
+    k.err_zero = b->d_err;
+    k.nerr_zero = b->k1_err_zero;
+    b->k1_err_zero = 0;
+  }
   if (f0) {  // sub-batch: frames f0.. (per-frame arrays shifted; mode 2 only)
     const Geom &g = b->g;
     const long long F = f0;
@@ -925,7 +931,7 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   } else {
     HIP_TRY(launch_pack(a, st, a.zero_pack != 0));
   }
-  if (a.seam) HIP_TRY(launch_seam_fix(a, st));
+  if (a.seam && !a.ff_pack) HIP_TRY(launch_seam_fix(a, st));  // (else inside k_emit_scan)
   if (ptime) {
     std::vector<unsigned long long> h(6 * nwords);
     HIP_TRY(hipMemcpyAsync(h.data(), a.dbg, sizeof(unsigned long long) * 6 * nwords, hipMemcpyDeviceToHost, st));
@@ -973,7 +979,9 @@ static int encode_frames(mij_batch *b, int nframes) {
   if (b->use_fdims && b->rgb) return fail(MIJ_EINVAL, "encode: region batches read B, G, R frames");
   if (b->use_fdims)
     HIP_TRY(hipMemsetAsync(b->d_seg_ntok, 0, sizeof(uint32_t) * nframes * b->g.nseg, b->stream));
-  HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * nframes, b->stream));
+  // (d_err: zeroed by the first K1 below -- nothing before k_tables writes it;
+  // a memset launch is 4-5 us of a one-frame step)
+  b->k1_err_zero = nframes;
   if (b->timing) HIP_TRY(hipEventRecord(b->ev[0], b->stream));
   const int nsub = std::min(b->overlap, nframes);
   if (!b->split && !b->keep_coefs && nsub > 1) {

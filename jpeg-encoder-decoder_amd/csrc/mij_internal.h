@@ -179,6 +179,8 @@ struct K1Args {
   const int2 *fdims;        // per-frame image size (region batches), null: the canvas
   uint16_t *audit;          // tests (mij_batch_audit): per frame, block, lane group g the 16
                             // straddle bits of zigzag 16g..16g+15; null in every product launch
+  int *err_zero;            // an encode's first K1: workgroup 0 zeroes these per-frame error
+  int nerr_zero;            // words (k_tables on write them), instead of a memset launch
 };
 constexpr int K1_WTIME_WORDS = 8;
 // K1 diagnostic switches (timing attribution; outputs are wrong when set)

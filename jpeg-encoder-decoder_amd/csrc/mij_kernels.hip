@@ -854,6 +854,8 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
     s_fac[i >> 6][i & 63] = T->qfac[i >> 6][i & 63];
   }
   if (threadIdx.x == 0) s_next = (int)blockIdx.x * a.per_wg + NW;
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < a.nerr_zero; i += NT) a.err_zero[i] = 0;
   __syncthreads();
 
   const int lane = threadIdx.x & 63;
@@ -1800,6 +1802,18 @@ struct TabScratch2 {
   int seq[257];   // chain order -> symbol
 };
 
+// a uniform int the compiler cannot follow (keeps it from strength-reducing
+// rare-path LDS addresses into per-iteration VALU adds)
+__device__ __forceinline__ int opq(int x) {
+  asm volatile("" : "+s"(x));
+  return x;
+}
+// v_writelane: v with lane idx (uniform) set to x (uniform)
+__device__ __forceinline__ uint32_t wl32(uint32_t v, uint32_t x, int idx) {
+  // (two scalar operands: the lane select goes through m0, gfx9's one-SGPR constant bus)
+  asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(x), "s"(idx) : "m0");
+  return v;
+}
 __device__ __forceinline__ unsigned long long rl64(unsigned long long v, int idx) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, idx);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), idx);
@@ -2020,7 +2034,177 @@ __device__ __forceinline__ void build_table_wave2(const uint32_t *hist, const ui
   const uint32_t total_count = __builtin_amdgcn_readlane((int)wave_scan64(fsum), 63) + 1u;
   int root_label = 256;
   uint32_t total = 1;
+  bool narrow_done = false;
   if (total_count < (1u << 23)) {
+    // Short form (every table whose merged nodes queue in creation order, i.e.
+    // no insert below): the loop carries only what decides the merges -- the
+    // narrow keys of the four queue heads and the leaf counts of the merged
+    // ones -- and records per merge which heads it took (2 bits) and v1's
+    // leaf count.  The queue places, hence the node ids (leaf = its place,
+    // merge j = nl + j), follow after the loop from a prefix sum of the taken
+    // leaves: each merge takes two heads, so mh = 2 step - lh.  New entries
+    // go into the merged-key window by v_writelane (to LDS only past it); an
+    // insert abandons this form for the general loop below.
+    int lw = 0, mw = 0, lh = 0, mh = 0, step = 0;
+    uint32_t wlk, wmk = ~0u, wms = 0, rec = 0, mlast = 0;
+    {
+      const unsigned long long v = S->ql[lane];
+      wlk = ((uint32_t)(v >> 32) << 9) | ((uint32_t)v >> 19);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+    }
+    const int nsteps = nl - 1;
+    bool ok = true;
+    while (step < nsteps) {
+      if (lh - lw > 30) {  // (early reloads: the runs below stay long)
+        lw = lh;
+        const unsigned long long v = S->ql[lw + lane];
+        wlk = ((uint32_t)(v >> 32) << 9) | ((uint32_t)v >> 19);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      }
+      if (mh - mw > 30) {
+        // the window's entries to LDS, then the window from the merged head
+        if (mw + lane < step) S->qm[mw + lane] = ((unsigned long long)wms << 32) | wmk;
+        wave_lds_sync();
+        mw = mh;
+        const unsigned long long v = S->qm[mw + lane];
+        wmk = (uint32_t)v;
+        wms = (uint32_t)(v >> 32);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+      }
+      // merges the windows hold: the heads' readlanes in range (two heads
+      // taken per merge), each new entry in the merged window, the records in
+      // one 64-lane row
+      int bud = nsteps - step;
+      bud = min(bud, (63 - (lh - lw)) >> 1);
+      bud = min(bud, (63 - (mh - mw)) >> 1);
+      bud = min(bud, 64 - (step - mw));
+      bud = min(bud, 64 - (step & 63));
+      if (bud < 1) {  // more than a window of merged nodes queued: the general loop
+        ok = false;
+        break;
+      }
+      uint32_t il = lh - lw, im = mh - mw, mwl = step - mw, rl = step & 63, st = step;
+      // (the budget's min may land in a VGPR: its end made scalar for the asm)
+      const uint32_t send = (uint32_t)__builtin_amdgcn_readfirstlane(step + bud);
+      uint32_t flag, K, sz, t1, t2, t3, t4, t5;
+      // One merge per pass, all scalar but the readlanes and writelanes:
+      //   a, b = leaf heads; c, d = merged heads (sc, sd their leaf counts)
+      //   ac = a < c; k1 = min; x = ac ? b : a; y = ac ? c : d; bx = x < y
+      //   K = k1 + (k2 & ~511) (counts add, v1's label stays)
+      //   rec lane (step & 63) = ac | bx << 1 | leaves(v1) << 2
+      // An entry below the last appended key (a possible insert) leaves the
+      // loop before its append (flag = 1).  (s_nop 4 first: the operands may
+      // come from VALU writes just before.)
+      asm volatile(
+          "s_nop 4\n"
+          "1:\n\t"
+          "s_add_u32 %[t5], %[il], 1\n\t"
+          "s_add_u32 %[t4], %[im], 1\n\t"
+          "v_readlane_b32 %[K], %[wlk], %[il]\n\t"
+          "v_readlane_b32 %[t1], %[wlk], %[t5]\n\t"
+          "v_readlane_b32 %[t2], %[wmk], %[im]\n\t"
+          "v_readlane_b32 %[t3], %[wmk], %[t4]\n\t"
+          "v_readlane_b32 %[sz], %[wms], %[im]\n\t"
+          "v_readlane_b32 %[t4], %[wms], %[t4]\n\t"
+          // K = a, t1 = b, t2 = c, t3 = d, sz = sc, t4 = sd
+          "s_cmp_lt_u32 %[K], %[t2]\n\t"
+          "s_cselect_b32 %[t5], %[K], %[t2]\n\t"   // t5 = k1
+          "s_cselect_b32 %[K], %[t1], %[K]\n\t"    // K = x
+          "s_cselect_b32 %[t1], %[t2], %[t3]\n\t"  // t1 = y
+          "s_cselect_b32 %[t2], 1, %[sz]\n\t"      // t2 = s1
+          "s_cselect_b32 %[t3], %[sz], %[t4]\n\t"  // t3 = sy
+          "s_cselect_b32 %[t4], 1, 0\n\t"          // t4 = ac
+          "s_cmp_lt_u32 %[K], %[t1]\n\t"
+          "s_cselect_b32 %[K], %[K], %[t1]\n\t"    // K = k2
+          "s_cselect_b32 %[t3], 1, %[t3]\n\t"      // t3 = s2
+          "s_cselect_b32 %[t1], 1, 0\n\t"          // t1 = bx
+          "s_and_b32 %[K], %[K], 0xfffffe00\n\t"
+          "s_add_u32 %[K], %[K], %[t5]\n\t"        // K
+          "s_add_u32 %[sz], %[t2], %[t3]\n\t"      // sz = s1 + s2
+          "s_add_u32 %[t3], %[t4], %[t1]\n\t"      // t3 = leaves taken
+          "s_lshl1_add_u32 %[t1], %[t1], %[t4]\n\t"
+          "s_lshl2_add_u32 %[t1], %[t2], %[t1]\n\t"  // record
+          "s_mov_b32 m0, %[rl]\n\t"
+          "v_writelane_b32 %[rec], %[t1], m0\n\t"
+          "s_add_u32 %[il], %[il], %[t3]\n\t"
+          "s_sub_u32 %[im], %[im], %[t3]\n\t"
+          "s_add_u32 %[im], %[im], 2\n\t"
+          "s_cmp_gt_u32 %[ml], %[K]\n\t"
+          "s_cbranch_scc1 2f\n\t"
+          "s_mov_b32 m0, %[mwl]\n\t"
+          "v_writelane_b32 %[wmk], %[K], m0\n\t"
+          "v_writelane_b32 %[wms], %[sz], m0\n\t"
+          "s_mov_b32 %[ml], %[K]\n\t"
+          "s_add_u32 %[mwl], %[mwl], 1\n\t"
+          "s_add_u32 %[rl], %[rl], 1\n\t"
+          "s_add_u32 %[st], %[st], 1\n\t"
+          "s_cmp_lg_u32 %[st], %[send]\n\t"
+          "s_cbranch_scc1 1b\n\t"
+          "s_mov_b32 %[flag], 0\n\t"
+          "s_branch 3f\n"
+          "2:\n\t"
+          "s_mov_b32 %[flag], 1\n"
+          "3:"
+          : [il] "+s"(il), [im] "+s"(im), [mwl] "+s"(mwl), [rl] "+s"(rl), [st] "+s"(st), [ml] "+s"(mlast),
+            [rec] "+v"(rec), [wmk] "+v"(wmk), [wms] "+v"(wms), [flag] "=&s"(flag), [K] "=&s"(K), [sz] "=&s"(sz),
+            [t1] "=&s"(t1), [t2] "=&s"(t2), [t3] "=&s"(t3), [t4] "=&s"(t4), [t5] "=&s"(t5)
+          : [wlk] "v"(wlk), [send] "s"(send)
+          : "m0", "scc");
+      step = (int)st;
+      lh = lw + (int)il;
+      mh = mw + (int)im;
+      if (flag) {
+        if (step > mh) {  // an equal-count node with a smaller key is queued: the general loop
+          ok = false;
+          break;
+        }
+        wmk = wl32(wmk, K, step - mw);  // (step - mw < 64: the budget)
+        wms = wl32(wms, sz, step - mw);
+        mlast = K;
+        step++;
+      }
+      if ((step & 63) == 0) S->rec[step - 64 + lane] = (int)rec;
+    }
+    const uint32_t klast = mlast;
+    if (ok) {
+      {
+        const int b0 = nsteps & ~63;
+        if (b0 + lane < nsteps) S->rec[b0 + lane] = (int)rec;
+      }
+      wave_lds_sync();
+      // the merges' children: leaf places by a prefix sum of the leaves taken
+      int carry = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int j = lane + 64 * i;
+        const uint32_t r = j < nsteps ? (uint32_t)S->rec[j] : 0u;
+        const int e = (int)(r & 1u) + (int)((r >> 1) & 1u);
+        const int incl = (int)wave_scan64((uint32_t)e);
+        const int lb = carry + incl - e, mb = 2 * j - lb;
+        carry += __builtin_amdgcn_readlane(incl, 63);
+        if (j < nsteps) {
+          const bool ac = r & 1u, bx = r & 2u;
+          const int c1 = ac ? lb : nl + mb;
+          const int c2 = bx ? (ac ? lb + 1 : lb) : (ac ? nl + mb : nl + mb + 1), node = nl + j;
+          S->par[c1] = node;
+          S->par[c2] = node;
+          S->off[c1] = 0;
+          S->off[c2] = (int)(r >> 2);  // v2's chain follows v1's (:223-226)
+        }
+      }
+      if (nsteps > 0) {
+        root_label = 256 - (int)(klast & 511u);
+        total = klast >> 9;
+      }
+      narrow_done = true;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 5; i++)
+        if (lane + 64 * i < 320) S->qm[lane + 64 * i] = ~0ull;
+      wave_lds_sync();
+    }
+  }
+  if (total_count < (1u << 23) && !narrow_done) {
     int lw = 0, mw = 0, lh = 0, mh = 0, mt = 0;
     uint32_t wlk, wla, wmk = ~0u, wma = ~0u, rec = 0;
     auto split = [](unsigned long long v, uint32_t &key, uint32_t &aux) {
@@ -2107,7 +2291,7 @@ __device__ __forceinline__ void build_table_wave2(const uint32_t *hist, const ui
         S->off[c2] = (int)(r >> 20);
       }
     }
-  } else {
+  } else if (total_count >= (1u << 23)) {
     // the merges (encoder.c:196-226) on uniform values; v1 = the least key, v2
     // the next; K = the merged node, queued at its key's place
     // (keys as two 32-bit words -- freq, then label | leaves | node -- so the
@@ -3113,17 +3297,14 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
 // group of a scan may start inside the same word as the one before it).
 // Nothing then needs zeroed scan buffers: no OR-ing onto zero in the packing,
 // no zeroing in k_emit_write.
-__global__ __launch_bounds__(256) void k_seam_fix(EntArgs a) {
+// One group's seam word (frame f, group bq of the frame's gpf).
+__device__ __forceinline__ void seam_fix_group(const EntArgs &a, const PackGrid &P, int f, int bq) {
   const Geom &G = a.g;
-  const PackGrid P = pack_grid(a);
-  const int gy = P.gy, gc = P.gc, gpf = P.gpf;
-  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (t >= (long long)a.nframes * gpf) return;
-  const int f = (int)(t / gpf), bq = (int)(t - (long long)f * gpf);
+  const int gy = P.gy, gc = P.gc;
   const long long g = (long long)f * P.stride + bq;  // the group's look-back word
   const int comp = bq < gy ? 0 : (bq < gy + gc ? 1 : 2);
   const int q = bq - (comp == 0 ? 0 : (comp == 1 ? gy : gy + gc));
-  if (q == 0 || a.err[f]) return;  // (a failed frame is dropped by the assembly)
+  if (q == 0) return;
   const unsigned long long start = a.pack_state[g - 1] & LB_VAL;  // the group's first bit
   if (!(start & 31)) return;
   uint32_t *raw = a.raw + (long long)f * G.raw_fs + (comp == 0 ? 0 : G.raw_words[0] + (comp == 2 ? G.raw_words[1] : 0));
@@ -3133,6 +3314,18 @@ __global__ __launch_bounds__(256) void k_seam_fix(EntArgs a) {
     const int d = ff_word(old | sv, W, nb) - ff_word(old, W, nb);
     if (d) atomicAdd(&a.ffc[(long long)(f * 3 + comp) * emit_chunks(G) + W / EMIT_CW], (uint32_t)d);
   }
+}
+
+// Its own launch only when the 0xFF bytes are counted after the packing
+// (MIJ_OPT_FF_PACK=0: k_emit_count reads the fixed words); otherwise
+// k_emit_scan fixes its frame's seams first (one launch fewer per encode).
+__global__ __launch_bounds__(256) void k_seam_fix(EntArgs a) {
+  const PackGrid P = pack_grid(a);
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (long long)a.nframes * P.gpf) return;
+  const int f = (int)(t / P.gpf), bq = (int)(t - (long long)f * P.gpf);
+  if (a.err[f]) return;  // (a failed frame is dropped by the assembly)
+  seam_fix_group(a, P, f, bq);
 }
 
 // ===========================================================================
@@ -3266,6 +3459,15 @@ __global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
   }
   uint8_t *out = a.out + (long long)f * a.g.out_cap;
   const long long nchmax = emit_chunks(a.g);
+  // seam mode with the packing's 0xFF counts: the frame's seam words first
+  // (their OR-s and count adds land in L2; the counts and the pad words below
+  // are read past this CU's L1, which may hold lines of a neighbouring frame)
+  const bool seams = a.seam && a.ff_pack;
+  if (seams) {
+    const PackGrid P = pack_grid(a);
+    for (int bq = tid; bq < P.gpf; bq += 256) seam_fix_group(a, P, f, bq);
+    __threadfence();
+  }
   __shared__ int s_n[4];
   const int hlen = emit_headers(a, f, out, s_n);
   unsigned long long pos = (unsigned long long)hlen;
@@ -3283,7 +3485,8 @@ __global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
     unsigned long long carry = 0;  // 0xFF bytes of the earlier chunks
     for (long long c0 = 0; c0 < nch; c0 += 256) {
       const long long c = c0 + tid;
-      const int v = c < nch ? (int)cnt[c] : 0;
+      const int v = c < nch ? (int)(seams ? __hip_atomic_load(cnt + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                          : cnt[c]) : 0;
       const int incl = (int)wave_scan64((uint32_t)v);
       if (lane == 63) red[wave] = incl;
       __syncthreads();
@@ -3302,7 +3505,9 @@ __global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
       const int r = (int)(nbits & 7);
       uint8_t pad = 0xFF;
       if (r) {
-        const uint8_t part = (uint8_t)(raw[nbytes >> 2] >> (24 - 8 * (nbytes & 3)));
+        const uint32_t w = seams ? __hip_atomic_load(raw + (nbytes >> 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                 : raw[nbytes >> 2];
+        const uint8_t part = (uint8_t)(w >> (24 - 8 * (nbytes & 3)));
         pad = (uint8_t)(part | ((1u << (8 - r)) - 1u));
       }
       out[pos] = pad;
@@ -4010,6 +4215,7 @@ template <int MODE>
 static void launch_k1_mode(const K1Args &a, int grid, hipStream_t s) {
   hipLaunchKernelGGL((k_mcu_dct<MODE>), dim3(grid), dim3(64 * k1_waves<MODE>()), 0, s, a);
 }
+// diagnostics: an empty kernel (dispatch-gap probes, MIJ_NOP_AFTER_K1 in the diag build)
 hipError_t launch_k1(const K1Args &a, int grid, int mode, hipStream_t s) {
   if (a.rgb && a.fdims) return hipErrorInvalidValue;  // not instantiated (the API refuses it)
   switch (mode) {
