@@ -931,7 +931,11 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   } else {
     HIP_TRY(launch_pack(a, st, a.zero_pack != 0));
   }
-  if (a.seam && !a.ff_pack) HIP_TRY(launch_seam_fix(a, st));  // (else inside k_emit_scan)
+  // the seam fixes inside k_emit_scan on small batches (one frame: 0.080 ->
+  // 0.073 ms with the error words zeroed by K1; at config 3 the per-frame
+  // serial fixes cost emit ~20 us, more than the launch)
+  a.seam_in_scan = a.seam && a.ff_pack && nframes < 16;
+  if (a.seam && !a.seam_in_scan) HIP_TRY(launch_seam_fix(a, st));
   if (ptime) {
     std::vector<unsigned long long> h(6 * nwords);
     HIP_TRY(hipMemcpyAsync(h.data(), a.dbg, sizeof(unsigned long long) * 6 * nwords, hipMemcpyDeviceToHost, st));

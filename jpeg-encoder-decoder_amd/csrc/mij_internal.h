@@ -233,6 +233,9 @@ struct EntArgs {
   int ff_pack;                     // seam mode: k_pack_flat / k_seam_fix count the 0xFF bytes of every
                                    // EMIT_CH chunk into ffc as they store (k_emit_count not run;
                                    // k_emit_write leaves the counts zeroed)
+  int seam_in_scan;                // seam mode with ff_pack: k_emit_scan fixes its frame's seams
+                                   // first, no k_seam_fix launch (small batches: one launch fewer;
+                                   // on large ones the per-frame serial fixes cost more than it)
 };
 
 // The packing's groups (k_pack_flat, k_seam_fix): per frame gy luma groups,

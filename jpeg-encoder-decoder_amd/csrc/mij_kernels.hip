@@ -3316,9 +3316,8 @@ __device__ __forceinline__ void seam_fix_group(const EntArgs &a, const PackGrid 
   }
 }
 
-// Its own launch only when the 0xFF bytes are counted after the packing
-// (MIJ_OPT_FF_PACK=0: k_emit_count reads the fixed words); otherwise
-// k_emit_scan fixes its frame's seams first (one launch fewer per encode).
+// Its own launch unless k_emit_scan does it (EntArgs::seam_in_scan: small
+// batches with the packing's 0xFF counts, one launch fewer per encode).
 __global__ __launch_bounds__(256) void k_seam_fix(EntArgs a) {
   const PackGrid P = pack_grid(a);
   const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -3462,7 +3461,7 @@ __global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
   // seam mode with the packing's 0xFF counts: the frame's seam words first
   // (their OR-s and count adds land in L2; the counts and the pad words below
   // are read past this CU's L1, which may hold lines of a neighbouring frame)
-  const bool seams = a.seam && a.ff_pack;
+  const bool seams = a.seam && a.ff_pack && a.seam_in_scan;
   if (seams) {
     const PackGrid P = pack_grid(a);
     for (int bq = tid; bq < P.gpf; bq += 256) seam_fix_group(a, P, f, bq);
