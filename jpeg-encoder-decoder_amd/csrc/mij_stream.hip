@@ -11,7 +11,8 @@
 //   Frames stay in PPM byte order (R, G, B): K1 swaps channels as it loads.
 //   Three pinned input buffers: the reader threads fill chunk k+1 while chunk
 //   k uploads and the bytes of chunk k-1 are written, so the PCIe upload
-//   (the bound of a host-fed stream) runs back to back.
+//   (the bound of a host-fed stream) runs back to back; each frame's upload is
+//   enqueued by its reader thread as soon as the frame is in pinned memory.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>
@@ -279,7 +280,16 @@ static int stream_run(mij_stream *s, int n, const FillFn &fill, const DrainFn &d
       const int first = k * s->chunk, cnt = count(k);
       uint8_t *dst = s->h_in[k % NIN];
       const double t0 = now_s();
-      r.rc = parallel_for(cnt, rthreads, [&](int i) { return fill(first + i, dst + (size_t)i * s->fbytes); }, &r.bad);
+      // each frame's upload enqueued as soon as it is read (the copies run
+      // while the chunk's other files are read: no chunk-long read before the
+      // first byte crosses PCIe); batch k & 1's stream orders them after chunk
+      // k - 2's encode, which was enqueued before this thread started
+      mij_batch *bk = s->b[k & 1];
+      r.rc = parallel_for(cnt, rthreads, [&](int i) {
+        uint8_t *fd = dst + (size_t)i * s->fbytes;
+        const int rc = fill(first + i, fd);
+        return rc ? rc : mij_batch_upload_slot_async(bk, fd, i);
+      }, &r.bad);
       if (r.rc && r.bad >= 0) r.bad += first;
       r.secs = now_s() - t0;
     });
@@ -295,7 +305,8 @@ static int stream_run(mij_stream *s, int n, const FillFn &fill, const DrainFn &d
   auto enqueue = [&](int k) -> int {
     const int sl = k & 1, cnt = count(k);
     int rc;
-    if ((rc = mij_batch_upload_async(s->b[sl], s->h_in[k % NIN], cnt))) return rc;
+    // (the frames' uploads were enqueued by the reader threads: buffer k % NIN
+    // is free once the copies enqueued before this event are done)
     S_TRY(hipEventRecord(s->ev_up[k % NIN], s->st[sl]));
     S_TRY(hipEventRecord(s->ev_t0[sl], s->st[sl]));
     if ((rc = mij_batch_encode(s->b[sl], cnt))) return rc;
