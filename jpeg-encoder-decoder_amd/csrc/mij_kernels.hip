@@ -2384,16 +2384,18 @@ __device__ __forceinline__ void build_table_wave2(const uint32_t *hist, const ui
   }
   wave_lds_sync();
   TAB_T(3);
-  // depth and chain place of every node: pointer jumping to the root
+  // depth and chain place of every merged node (nodes nl..nn-1, parents among
+  // them): pointer jumping to the root; then each leaf from its parent's
   {
-    int pp[9], dd[9], oo[9];
+    const int ni = nn - nl;  // merged nodes (<= 256)
+    int pp[4], dd[4], oo[4];
 #pragma unroll
-    for (int i = 0; i < 9; i++) {
-      const int nd = lane + 64 * i;
+    for (int i = 0; i < 4; i++) {
+      const int nd = nl + lane + 64 * i;
       pp[i] = 0xFFFF;
       dd[i] = 0;
       oo[i] = 0;
-      if (64 * i < nn && nd < nn) {
+      if (64 * i < ni && nd < nn) {
         pp[i] = S->par[nd];
         oo[i] = S->off[nd];
         dd[i] = pp[i] != 0xFFFF;
@@ -2404,15 +2406,15 @@ __device__ __forceinline__ void build_table_wave2(const uint32_t *hist, const ui
     for (int round = 0; round < 10; round++) {
       bool more = false;
 #pragma unroll
-      for (int i = 0; i < 9; i++) more |= pp[i] != 0xFFFF;
+      for (int i = 0; i < 4; i++) more |= pp[i] != 0xFFFF;
       if (!__ballot(more)) break;
-      int nd2[9], no2[9], np2[9];
+      int nd2[4], no2[4], np2[4];
 #pragma unroll
-      for (int i = 0; i < 9; i++) {
+      for (int i = 0; i < 4; i++) {
         nd2[i] = dd[i];
         no2[i] = oo[i];
         np2[i] = pp[i];
-        if (64 * i < nn && pp[i] != 0xFFFF) {
+        if (64 * i < ni && pp[i] != 0xFFFF) {
           nd2[i] += S->dep[pp[i]];
           no2[i] += S->off[pp[i]];
           np2[i] = S->par[pp[i]];
@@ -2420,12 +2422,12 @@ __device__ __forceinline__ void build_table_wave2(const uint32_t *hist, const ui
       }
       wave_lds_sync();
 #pragma unroll
-      for (int i = 0; i < 9; i++) {
-        const int nd = lane + 64 * i;
+      for (int i = 0; i < 4; i++) {
+        const int nd = nl + lane + 64 * i;
         dd[i] = nd2[i];
         oo[i] = no2[i];
         pp[i] = np2[i];
-        if (64 * i < nn && nd < nn) {
+        if (64 * i < ni && nd < nn) {
           S->dep[nd] = dd[i];
           S->off[nd] = oo[i];
           S->par[nd] = pp[i];
@@ -2433,15 +2435,18 @@ __device__ __forceinline__ void build_table_wave2(const uint32_t *hist, const ui
       }
       wave_lds_sync();
     }
-    // leaves (nodes 0..nl-1): their symbols' lengths and chain places
+    // leaves (nodes 0..nl-1): one edge to the parent plus the parent's path;
+    // their symbols' lengths and chain places
 #pragma unroll
     for (int i = 0; i < 5; i++) {
       const int q = lane + 64 * i;
       if (q < nl && nl > 1) {
+        const int pq = S->par[q];
+        const int d = 1 + S->dep[pq], o = S->off[q] + S->off[pq];
         const int sy = 256 - (int)((S->ql[q] >> 19) & 511);
-        S->scl[sy] = dd[i];
-        S->spos[sy] = oo[i];
-        S->seq[oo[i]] = sy;
+        S->scl[sy] = d;
+        S->spos[sy] = o;
+        S->seq[o] = sy;
       }
     }
   }
