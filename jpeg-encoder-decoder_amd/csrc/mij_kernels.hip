@@ -2475,24 +2475,25 @@ __device__ __forceinline__ void build_table_wave2(const uint32_t *hist, const ui
   // code_len_freq (all 257 symbols) and counts of 0..255, length L in lane L;
   // the nl leaves (nl - 1 of them symbols 0..255) are all counted by the
   // longest length
-  int clf = 0, cnt = 0, maxl = 0;
+  // (by LDS atomics into the merge records' words, free by now: a ballot
+  // per length and register cost ~20 instructions per length)
   const int nlc = nl > 1 ? nl : 0;
-  for (int L = 1, seen = 0; seen < nlc && L < 32; L++) {
-    int c = 0;
+  if (lane < 32) S->rec[lane] = 0;
+  wave_lds_sync();
 #pragma unroll
-    for (int i = 0; i < 4; i++) c += __popcll(__ballot(cl[i] == L));
-    const int c256 = __popcll(__ballot(lane == 0 && cl[4] == L));
-    if (lane == L) {
-      clf = c + c256;
-      cnt = c;
-    }
-    seen += c + c256;
-    maxl = L;
-  }
+  for (int i = 0; i < 5; i++)
+    if (cl[i] > 0 && (i < 4 || lane == 0)) atomicAdd(&S->rec[cl[i]], 1);
+  wave_lds_sync();
+  int clf = lane < 32 ? S->rec[lane] : 0;
+  const int l256 = __builtin_amdgcn_readfirstlane(cl[4]);  // symbol 256's length (lane 0)
+  const int cnt = clf - (l256 > 0 && lane == l256 ? 1 : 0);  // symbols 0..255
+  const unsigned long long lens = __ballot(clf > 0);
+  const int maxl = lens ? 63 - __clzll(lens) : 0;
   bool fail = nlc < 2;
   if (!fail) {
-    // :239-259 limit to 16 bits
-    int i = 31;
+    // :239-259 limit to 16 bits (the lengths above the longest are empty:
+    // the walk down from 31 starts there)
+    int i = max(maxl, 17);
     for (int guard = 0; guard < 4096; guard++) {
       if (__builtin_amdgcn_readlane(clf, i) > 0) {
         const unsigned long long m = __ballot(clf > 0) & ((1ull << (i - 1)) - 1ull);
