@@ -20,7 +20,7 @@ for sec in ${SECTIONS:-bench q single c4 stream probe}; do
     single) run single 300 --frames 1 --width 1920 --height 1280 --steps 200 --warmup 20 --no-cpu-baseline --coef-launches 0 ;;
     c4) run c4_root 300 --workload config4 --steps 20 --warmup 3 --band-emit root --verify -1
         run c4_bands 300 --workload config4 --steps 20 --warmup 3 --band-emit bands --verify -1 ;;
-    stream) run stream 600 --workload stream --steps 3 --warmup 1 ;;
+    stream) run stream 600 --workload stream --steps 8 --warmup 2 ;;
     probe) timeout -k 10 300 scripts/micro/tile_stream > $out/tile_stream.txt 2>&1 || { echo "probe failed"; tail -5 $out/tile_stream.txt; exit 1; }
            cat $out/tile_stream.txt ;;
   esac
