@@ -2061,8 +2061,10 @@ __device__ __forceinline__ void build_table_wave2(const uint32_t *hist, const ui
         wlk = ((uint32_t)(v >> 32) << 9) | ((uint32_t)v >> 19);
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
       }
-      if (mh - mw > 30) {
+      if (mh - mw > 30 || step - mw >= 48) {
         // the window's entries to LDS, then the window from the merged head
+        // (also when the appended entries near its end: a queue of up to 63
+        // merged nodes stays in this form)
         if (mw + lane < step) S->qm[mw + lane] = ((unsigned long long)wms << 32) | wmk;
         wave_lds_sync();
         mw = mh;

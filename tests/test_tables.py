@@ -86,3 +86,41 @@ def test_table_failure_matches_oracle():
     with pytest.raises(mijpeg.MijError, match="frame 1"):
         b.build_tables(2, hist)
     b.close()
+
+
+def test_tables_match_oracle_on_random_histograms():
+    """Randomised shapes for the merge loop's forms (the scalar short form,
+    its window reloads, and the general loop it leaves for on an insert or a
+    merged queue longer than its window): power laws of random slope, flat
+    and near-flat counts, few and many symbols, heavy ties -- 256 tables
+    against the oracle, every field."""
+    rng = np.random.default_rng(77)
+    n = 64
+    hist = np.zeros((n, 4, 257), np.uint32)
+    for f in range(n):
+        for t in range(4):
+            k = int(rng.integers(2, 254))  # coded symbols
+            kind = (4 * f + t) % 5
+            if kind == 0:  # power law
+                v = (rng.integers(1000, 200000) / (1 + np.arange(k)) ** rng.uniform(0.5, 2.5)).astype(np.int64) + 1
+            elif kind == 1:  # flat
+                v = np.full(k, int(rng.integers(1, 50)))
+            elif kind == 2:  # near-flat
+                v = rng.integers(100, 104, k)
+            elif kind == 3:  # heavy ties from a small alphabet of counts
+                v = rng.choice(np.array([1, 2, 3, 5, 8]), k)
+            else:  # wide spread
+                v = rng.integers(1, 1 << int(rng.integers(2, 20)), k)
+            h = np.zeros(256, np.int64)
+            h[rng.permutation(256)[:k]] = v
+            hist[f, t, :256] = h.astype(np.uint32)
+    b = mijpeg.Batch(16, 16, n)
+    b.build_tables(n, hist)
+    for f in range(n):
+        got = b.tables(f)
+        for t in range(4):
+            rc, want = O.cref_build_table(hist[f, t, :256])
+            assert rc == 0, (f, t)
+            for fld in FIELDS:
+                assert list(getattr(got[t], fld)) == list(getattr(want, fld)), (f, t, fld)
+    b.close()
