@@ -1135,12 +1135,12 @@ extern "C" int mij_batch_upload_regions(mij_batch *b, const uint8_t *bgr, int st
 
 // ---- asynchronous host transfers for the streaming engine (mij_stream.hip):
 // queued on the batch stream, no synchronisation
-int mij_batch_upload_slot_async(mij_batch *b, const uint8_t *host, int slot) {
+int mij_batch_upload_slot_async(mij_batch *b, const uint8_t *host, int slot, void *stream) {
   if (!b || b->assembler || !host || slot < 0 || slot >= b->cap || !b->own_in || b->use_fdims)
     return fail(MIJ_EINVAL, "upload_slot_async: bad args");
   HIP_TRY(hipSetDevice(b->dev));
   HIP_TRY(hipMemcpyAsync(b->d_in + (long long)slot * b->in_fs, host, (size_t)b->in_fs, hipMemcpyHostToDevice,
-                         b->stream));
+                         stream ? (hipStream_t)stream : b->stream));
   return MIJ_OK;
 }
 int mij_batch_lengths_async(mij_batch *b, uint64_t *h_len, int *h_err, int nframes) {

@@ -14,11 +14,11 @@ void mij_clear_error();
 int mij_frame_fail(int ferr, const char *what, int frame);
 
 // asynchronous transfers on the batch's stream (no synchronisation)
-// one frame into slot `slot` on the batch stream, for host threads uploading
+// one frame into slot `slot` on the batch stream (or `stream`), for host threads uploading
 // the frames of a chunk as each is read: distinct slots may be uploaded from
 // different threads at once (only the copy is enqueued: a stream's batches never hold region
 // sizes, which mij_batch_upload resets)
-int mij_batch_upload_slot_async(mij_batch *b, const uint8_t *host, int slot);
+int mij_batch_upload_slot_async(mij_batch *b, const uint8_t *host, int slot, void *stream = nullptr);
 int mij_batch_lengths_async(mij_batch *b, uint64_t *h_len, int *h_err, int nframes);
 int mij_batch_output_async(mij_batch *b, int frame, uint8_t *dst, size_t n);
 

@@ -15,6 +15,7 @@
 //   enqueued by its reader thread as soon as the frame is in pinned memory.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -143,6 +144,11 @@ struct mij_stream {
   hipStream_t st[2] = {nullptr, nullptr};
   uint8_t *h_in[NIN] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_up[NIN] = {};  // the upload out of h_in[i] has completed
+  // uploads on a stream of their own, so that a chunk's uploads never queue
+  // ahead of another chunk's D2H copies on a batch stream; ev_in_free[i]:
+  // batch i's encode has read its input (the next chunk may overwrite it)
+  hipStream_t st_up = nullptr;
+  hipEvent_t ev_in_free[2] = {};
   uint64_t *h_len[2] = {nullptr, nullptr};
   int *h_err[2] = {nullptr, nullptr};
   uint8_t *h_out[2] = {nullptr, nullptr};
@@ -159,7 +165,12 @@ static void stream_free(mij_stream *s) {
     if (s->h_in[i]) hipHostFree(s->h_in[i]);
     if (s->ev_up[i]) hipEventDestroy(s->ev_up[i]);
   }
+  if (s->st_up) {
+    hipStreamSynchronize(s->st_up);
+    hipStreamDestroy(s->st_up);
+  }
   for (int i = 0; i < 2; i++) {
+    if (s->ev_in_free[i]) hipEventDestroy(s->ev_in_free[i]);
     if (s->st[i]) hipStreamSynchronize(s->st[i]);
     if (s->b[i]) mij_batch_destroy(s->b[i]);
     if (s->h_len[i]) hipHostFree(s->h_len[i]);
@@ -185,6 +196,8 @@ static int stream_init(mij_stream *s, int device, int w, int h, int chunk, int q
     s->st[i] = (hipStream_t)mij_batch_stream(s->b[i]);
   }
   S_TRY(hipSetDevice(device));
+  S_TRY(hipStreamCreateWithFlags(&s->st_up, hipStreamNonBlocking));
+  for (int i = 0; i < 2; i++) S_TRY(hipEventCreateWithFlags(&s->ev_in_free[i], hipEventDisableTiming));
   for (int i = 0; i < NIN; i++) {
     S_TRY(hipHostMalloc((void **)&s->h_in[i], s->fbytes * chunk, hipHostMallocDefault));
     S_TRY(hipEventCreateWithFlags(&s->ev_up[i], hipEventDisableTiming));
@@ -260,6 +273,24 @@ static int stream_run(mij_stream *s, int n, const FillFn &fill, const DrainFn &d
   for (double &v : s->stats) v = 0.0;
   const double t_start = now_s();
   const int nchunks = (n + s->chunk - 1) / s->chunk;
+  // diagnostics (MIJ_STREAM_TRACE=1): per chunk, host times of its read,
+  // enqueue and drain steps and device times of its uploads and encode, to
+  // stderr after the run
+  static const bool trace = getenv("MIJ_STREAM_TRACE") && atoi(getenv("MIJ_STREAM_TRACE"));
+  struct Tr {
+    double r0 = 0, r1 = 0, enq = 0, len = 0, out = 0, wr = 0;
+    hipEvent_t up = nullptr, enc = nullptr;
+  };
+  std::vector<Tr> tr(trace ? nchunks : 0);
+  hipEvent_t tr0 = nullptr;
+  if (trace) {
+    S_TRY(hipEventCreate(&tr0));
+    S_TRY(hipEventRecord(tr0, s->st[0]));
+    for (Tr &x : tr) {
+      S_TRY(hipEventCreate(&x.up));
+      S_TRY(hipEventCreate(&x.enc));
+    }
+  }
   auto count = [&](int k) { return std::min(s->chunk, n - k * s->chunk); };
   // reader and writer pools share the host threads (writes are small)
   const int wthreads = std::max(1, s->threads / 4), rthreads = std::max(1, s->threads - wthreads);
@@ -272,27 +303,32 @@ static int stream_run(mij_stream *s, int n, const FillFn &fill, const DrainFn &d
     int rc = MIJ_OK, bad = -1;
     double secs = 0.0;
   } rd[NIN];
-  auto start_read = [&](int k) {
+  auto start_read = [&](int k) -> int {
     Read &r = rd[k % NIN];
     r.rc = MIJ_OK;
     r.bad = -1;
+    // batch k & 1's input is free once chunk k - 2's encode has run (its
+    // uploads wait for that on the upload stream; the reads do not)
+    if (k >= 2) S_TRY(hipStreamWaitEvent(s->st_up, s->ev_in_free[k & 1], 0));
     r.th = std::thread([&, k]() {
       const int first = k * s->chunk, cnt = count(k);
       uint8_t *dst = s->h_in[k % NIN];
       const double t0 = now_s();
-      // each frame's upload enqueued as soon as it is read (the copies run
-      // while the chunk's other files are read: no chunk-long read before the
-      // first byte crosses PCIe); batch k & 1's stream orders them after chunk
-      // k - 2's encode, which was enqueued before this thread started
+      if (trace) tr[k].r0 = t0 - t_start;
+      // each frame's upload enqueued on the upload stream as soon as it is
+      // read (the copies run while the chunk's other files are read: no
+      // chunk-long read before the first byte crosses PCIe)
       mij_batch *bk = s->b[k & 1];
       r.rc = parallel_for(cnt, rthreads, [&](int i) {
         uint8_t *fd = dst + (size_t)i * s->fbytes;
         const int rc = fill(first + i, fd);
-        return rc ? rc : mij_batch_upload_slot_async(bk, fd, i);
+        return rc ? rc : mij_batch_upload_slot_async(bk, fd, i, s->st_up);
       }, &r.bad);
       if (r.rc && r.bad >= 0) r.bad += first;
       r.secs = now_s() - t0;
+      if (trace) tr[k].r1 = now_s() - t_start;
     });
+    return MIJ_OK;
   };
   auto join_read = [&](int k) -> int {
     Read &r = rd[k % NIN];
@@ -305,12 +341,20 @@ static int stream_run(mij_stream *s, int n, const FillFn &fill, const DrainFn &d
   auto enqueue = [&](int k) -> int {
     const int sl = k & 1, cnt = count(k);
     int rc;
-    // (the frames' uploads were enqueued by the reader threads: buffer k % NIN
-    // is free once the copies enqueued before this event are done)
-    S_TRY(hipEventRecord(s->ev_up[k % NIN], s->st[sl]));
+    // (the frames' uploads were enqueued on the upload stream by the reader
+    // threads, all before this: buffer k % NIN is free and the batch's input
+    // is in once the copies before this event are done)
+    S_TRY(hipEventRecord(s->ev_up[k % NIN], s->st_up));
+    if (trace) {
+      tr[k].enq = now_s() - t_start;
+      S_TRY(hipEventRecord(tr[k].up, s->st_up));
+    }
+    S_TRY(hipStreamWaitEvent(s->st[sl], s->ev_up[k % NIN], 0));
     S_TRY(hipEventRecord(s->ev_t0[sl], s->st[sl]));
     if ((rc = mij_batch_encode(s->b[sl], cnt))) return rc;
     S_TRY(hipEventRecord(s->ev_t1[sl], s->st[sl]));
+    S_TRY(hipEventRecord(s->ev_in_free[sl], s->st[sl]));
+    if (trace) S_TRY(hipEventRecord(tr[k].enc, s->st[sl]));
     if ((rc = mij_batch_lengths_async(s->b[sl], s->h_len[sl], s->h_err[sl], cnt))) return rc;
     S_TRY(hipEventRecord(s->ev_len[sl], s->st[sl]));
     s->stats[5] += (double)cnt * s->fbytes;
@@ -320,6 +364,7 @@ static int stream_run(mij_stream *s, int n, const FillFn &fill, const DrainFn &d
   auto finish = [&](int k) -> int {
     const int sl = k & 1, first = k * s->chunk, cnt = count(k);
     S_TRY(hipEventSynchronize(s->ev_len[sl]));
+    if (trace) tr[k].len = now_s() - t_start;
     std::vector<size_t> &off = s->off[sl];
     off[0] = 0;
     for (int i = 0; i < cnt; i++) {
@@ -340,6 +385,7 @@ static int stream_run(mij_stream *s, int n, const FillFn &fill, const DrainFn &d
     }
     S_TRY(hipEventRecord(s->ev_out[sl], s->st[sl]));
     S_TRY(hipEventSynchronize(s->ev_out[sl]));
+    if (trace) tr[k].out = now_s() - t_start;
     float ms = 0.f;
     S_TRY(hipEventElapsedTime(&ms, s->ev_t0[sl], s->ev_t1[sl]));
     s->stats[3] += ms * 1e-3;
@@ -348,6 +394,7 @@ static int stream_run(mij_stream *s, int n, const FillFn &fill, const DrainFn &d
     const int rc = parallel_for(cnt, wthreads,
                                 [&](int i) { return drain(first + i, s->h_out[sl] + off[i], off[i + 1] - off[i]); }, &bad);
     s->stats[2] += now_s() - t0;
+    if (trace) tr[k].wr = now_s() - t_start;
     s->stats[4] += cnt;
     s->stats[6] += (double)off[cnt];
     if (rc && failed) *failed = first + bad;
@@ -359,12 +406,12 @@ static int stream_run(mij_stream *s, int n, const FillFn &fill, const DrainFn &d
   // k + 1 is enqueued).  Buffer k % NIN is refilled with chunk k + NIN only
   // after its upload event.
   int rc = MIJ_OK;
-  if (nchunks) start_read(0);
+  if (nchunks) rc = start_read(0);
   for (int k = 0; k < nchunks && !rc; k++) {
     rc = join_read(k);
     if (!rc && k + 1 < nchunks) {
       if (k + 1 >= NIN) S_TRY(hipEventSynchronize(s->ev_up[(k + 1) % NIN]));
-      start_read(k + 1);
+      rc = start_read(k + 1);
     }
     if (!rc) rc = enqueue(k);
     if (!rc && k >= 1) rc = finish(k - 1);  // chunk k - 1 drains while k uploads and k + 1 is read
@@ -373,10 +420,26 @@ static int stream_run(mij_stream *s, int n, const FillFn &fill, const DrainFn &d
   for (auto &r : rd)
     if (r.th.joinable()) r.th.join();  // (an error left a read running)
   if (rc) {  // drain what is still queued before returning
+    hipStreamSynchronize(s->st_up);
     hipStreamSynchronize(s->st[0]);
     hipStreamSynchronize(s->st[1]);
   }
   s->stats[0] = now_s() - t_start;
+  if (trace) {
+    hipDeviceSynchronize();
+    for (int k = 0; k < nchunks; k++) {
+      float up = 0.f, enc = 0.f;
+      hipEventElapsedTime(&up, tr0, tr[k].up);
+      hipEventElapsedTime(&enc, tr0, tr[k].enc);
+      fprintf(stderr, "stream chunk %d: read %.2f-%.2f ms, enqueued %.2f, uploads done %.2f (device), "
+              "encoded %.2f (device), lengths %.2f, bytes back %.2f, files written %.2f\n", k, 1e3 * tr[k].r0,
+              1e3 * tr[k].r1, 1e3 * tr[k].enq, up, enc, 1e3 * tr[k].len, 1e3 * tr[k].out, 1e3 * tr[k].wr);
+      hipEventDestroy(tr[k].up);
+      hipEventDestroy(tr[k].enc);
+    }
+    fprintf(stderr, "stream run %.2f ms\n", 1e3 * s->stats[0]);
+    hipEventDestroy(tr0);
+  }
   if (!rc) mij_clear_error();
   return rc;
 }
