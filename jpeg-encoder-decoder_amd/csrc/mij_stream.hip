@@ -391,7 +391,8 @@ static int stream_run(mij_stream *s, int n, const FillFn &fill, const DrainFn &d
     s->stats[3] += ms * 1e-3;
     const double t0 = now_s();
     int bad = -1;
-    const int rc = parallel_for(cnt, wthreads,
+    // (the last chunk's files on every host thread: nothing is read by then)
+    const int rc = parallel_for(cnt, k == nchunks - 1 ? s->threads : wthreads,
                                 [&](int i) { return drain(first + i, s->h_out[sl] + off[i], off[i + 1] - off[i]); }, &bad);
     s->stats[2] += now_s() - t0;
     if (trace) tr[k].wr = now_s() - t_start;
