@@ -9,7 +9,10 @@ rank encodes its own 256 frames; frames are independent, so there is no
 data-path collective -- DESIGN.md §Multi-GPU).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F]
+      (N > 1: the script starts N rank processes itself, one per GPU)
   torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+--gpus must equal WORLD_SIZE when a launcher sets it; otherwise bench.py exits
+non-zero instead of reporting a one-GPU number as an N-GPU one.
 
 Rank 0 prints one JSON line (metric, value, roofline, cpu_baseline, ...).
 """
@@ -63,7 +66,8 @@ def parse():
     ap.add_argument("--coef-launches", type=int, default=5,
                     help="extra launches of the coefficient-output K1 variant after the timed "
                          "region, for its own 6 B/px roofline line (0 disables)")
-    ap.add_argument("--workload", choices=["config3", "config4", "regions", "detect", "decode", "stream"],
+    ap.add_argument("--workload", choices=["config3", "config4", "regions", "detect", "decode", "stream",
+                                               "ranks"],
                     default="config3",
                     help="config4: a stream of 7680x4320 frames, each split into MCU-row bands "
                          "over the ranks with the RCCL exchange steps (strong scaling)")
@@ -89,10 +93,72 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` with no WORLD_SIZE in the environment: start N
+    child processes of this same script, one rank per GPU (RANK = LOCAL_RANK
+    = r, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1 and a free port), wait for all
+    of them and return the worst exit code.  The parent touches no GPU: it
+    never initialises HIP (torch.cuda.device_count() does not on this image)
+    and starts the ranks as children instead of exec'ing itself.  Rank 0
+    prints the one JSON line.  A rank that fails ends the others."""
+    import signal
+    import subprocess
+    backend = os.environ.get("MIJ_DIST_BACKEND", "nccl")
+    if backend == "nccl" and args.workload != "ranks":
+        import torch
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        # same process group as this parent: a `timeout` around the launch
+        # reaches every rank
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+
+    def _forward(sig, _frame):
+        for q in procs:
+            if q.poll() is None:
+                q.send_signal(sig)
+        raise SystemExit(128 + sig)
+    signal.signal(signal.SIGTERM, _forward)
+    signal.signal(signal.SIGINT, _forward)
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0:
+                rc = rc or (code if code > 0 else 128 - code)
+                for q in live:      # the exact children this parent started
+                    q.terminate()
+        if live:
+            time.sleep(0.05)
+    return rc
+
+
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        # a mis-launched scaling run must not print a valid-looking line
+        raise SystemExit(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world} "
+                         f"(launch with --gpus N alone, or torchrun --nproc-per-node N ... --gpus N)")
     # MIJ_DIST_FORCE=1: a process group even for one rank (runs the device
     # branch of the nccl exchanges on a single GPU)
     if world > 1 or os.environ.get("MIJ_DIST_FORCE"):
@@ -869,9 +935,38 @@ def cpu_baseline_parallel(h, w, seconds, workers):
                       f"per process, aggregate over the slowest process ({wall:.1f} s wall incl. start-up)"}
 
 
+def run_ranks(args, world, rank, local, dist):
+    """--workload ranks: the launcher's own check, no encode.  Every rank
+    joins the process group, meets the others at a barrier and reports its
+    rank; rank 0 prints who came.  (tests/test_bench_launch.py runs it over
+    gloo on the CPU.)"""
+    el = 0.0
+    t0 = time.perf_counter()
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    ranks = sharding.gather_ints([rank, os.getpid()], dist, dist_device(dist, local))
+    el, _ = sharding.reduce_timing(el, 0, dist, dist_device(dist, local))
+    if rank == 0:
+        print(json.dumps({"workload": "ranks", "n_gpus": world,
+                          "backend": dist.get_backend() if dist is not None else "none",
+                          "ranks": [r[0] for r in ranks], "pids": [r[1] for r in ranks],
+                          "barrier_s": round(el, 6)}), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    if not 1 <= args.quality <= 100:
+        raise SystemExit(f"bench.py: --quality {args.quality} outside 1..100")
     world, rank, local, dist, torch = dist_setup(args)
+    if args.workload == "ranks":
+        return run_ranks(args, world, rank, local, dist)
     if args.workload == "config4":
         return run_config4(args, world, rank, local, dist)
     if args.workload == "regions":
@@ -961,6 +1056,8 @@ def main():
     if args.verify and args.mode == "encode" and not os.environ.get("MIJ_K1_FLAGS"):
         verified, pinned = verify_batch(batch, frames, F, args, rank)
 
+    # per-rank verification counts (every rank checks its own batch)
+    ver_ranks = sharding.gather_ints([verified, pinned], dist, dist_device(dist, local))
     px_step = W * H * F
     value = px_all / el / 1e6
     geo = batch.geometry()
@@ -1017,6 +1114,9 @@ def main():
         "stages_ms": stage_avg,
         "verified_frames": verified,
         "verified_contents_pinned_to_reference_sha": pinned,
+        "verified_frames_per_rank": [v[0] for v in ver_ranks],
+        # ranks in the RCCL (nccl backend) process group; 0 for one process or gloo
+        "rccl_world": world if dist is not None and dist.get_backend() == "nccl" else 0,
         # blocks re-encoded in FP64 by k_fix_blocks (split pipeline) or coefficients
         # replayed in place (fused pipeline), per frame
         "fp64_fixups_per_frame": round(replays / (F * (args.warmup + 2 * args.steps)), 2),  # timed + events pass

@@ -153,13 +153,8 @@ int mij_batch_set_overlap(mij_batch *b, int nsub);
  *                         > 0: JFIF-assembly workgroups per frame
  *   MIJ_OPT_OVERLAP_PRIO  1 (default): the overlap stream (set_overlap) at
  *                         the highest priority; 0: the lowest
- *   MIJ_OPT_FAULT_TICKET  0 (default).  Fault injection for tests: v > 0
- *                         makes the next encode's packing start frame 0's
- *                         luma pack ticket at v, as a stale ticket word would
- *                         (pack group 0 never runs, the groups after it wait
- *                         on its look-back word); the frame must fail with
- *                         MIJ_EHANG within the wait bound instead of hanging
- *                         the launch.  Consumed by that encode.
+ *   (7 is reserved: an internal fault-injection hook of the test suite,
+ *   not settable through this call)
  *   MIJ_OPT_PACK_SEGS     -1 (default: chosen from the quality); otherwise
  *                         ly + 4 * lc (0..15): the packing's groups take
  *                         32 << ly luma and 32 << lc chroma segments */
@@ -171,7 +166,7 @@ enum {
   MIJ_OPT_PACK_WIDE = 4,
   MIJ_OPT_EMIT_SLOTS = 5,
   MIJ_OPT_OVERLAP_PRIO = 6,
-  MIJ_OPT_FAULT_TICKET = 7,
+  /* 7: reserved */
   MIJ_OPT_PACK_SEGS = 8,
   MIJ_OPT_COUNT = 9
 };

@@ -14,6 +14,7 @@
 #include "mij_host.h"
 #include "mij_internal.h"
 #include "mijpeg.h"
+#include "mij_testing.h"
 
 namespace mij {
 // launch wrappers (mij_kernels.hip)
@@ -918,10 +919,10 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
     HIP_TRY(hipMalloc(&a.dbg, sizeof(unsigned long long) * 6 * nwords));
     HIP_TRY(hipMemsetAsync(a.dbg, 0, sizeof(unsigned long long) * 6 * nwords, st));
   }
-  if (b->opt[MIJ_OPT_FAULT_TICKET] && f0 == 0) {
+  if (b->opt[OPT_TEST_FAULT_TICKET] && f0 == 0) {
     // fault injection (tests): frame 0's luma ticket starts past group 0
-    const int v = b->opt[MIJ_OPT_FAULT_TICKET];
-    b->opt[MIJ_OPT_FAULT_TICKET] = 0;
+    const int v = b->opt[OPT_TEST_FAULT_TICKET];
+    b->opt[OPT_TEST_FAULT_TICKET] = 0;
     if (!a.zero_pack) {
       HIP_TRY(hipMemsetAsync(a.pack_state, 0, sizeof(unsigned long long) * nwords, st));
       HIP_TRY(hipMemsetAsync(a.pack_ticket, 0, sizeof(unsigned) * 3 * nframes, st));
@@ -1135,6 +1136,10 @@ extern "C" int mij_batch_upload_regions(mij_batch *b, const uint8_t *bgr, int st
 
 // ---- asynchronous host transfers for the streaming engine (mij_stream.hip):
 // queued on the batch stream, no synchronisation
+// (runs on the stream's reader threads: the checks of pipe_check -- no
+// assembler -- are inline, and a region batch is refused outright, so no slot
+// needs canvas_frames' size reset; the caller re-raises a failure's message
+// on its own thread, mij_stream.hip join_read)
 int mij_batch_upload_slot_async(mij_batch *b, const uint8_t *host, int slot, void *stream) {
   if (!b || b->assembler || !host || slot < 0 || slot >= b->cap || !b->own_in || b->use_fdims)
     return fail(MIJ_EINVAL, "upload_slot_async: bad args");
@@ -1184,11 +1189,10 @@ extern "C" int mij_batch_set_overlap(mij_batch *b, int nsub) {
 extern "C" int mij_batch_set_option(mij_batch *b, int opt, int value) {
   if (pipe_check(b, "set_option")) return g_err;
   if (opt < 0 || opt >= MIJ_OPT_COUNT) return fail(MIJ_EINVAL, "set_option: unknown option %d", opt);
-  const bool binary = opt != MIJ_OPT_PACK_WIDE && opt != MIJ_OPT_EMIT_SLOTS && opt != MIJ_OPT_FAULT_TICKET &&
-                      opt != MIJ_OPT_PACK_SEGS;
+  if (opt == OPT_TEST_FAULT_TICKET) return fail(MIJ_EINVAL, "set_option: unknown option %d", opt);
+  const bool binary = opt != MIJ_OPT_PACK_WIDE && opt != MIJ_OPT_EMIT_SLOTS && opt != MIJ_OPT_PACK_SEGS;
   if ((binary && value != 0 && value != 1) || (opt == MIJ_OPT_PACK_WIDE && (value < -1 || value > 1)) ||
       (opt == MIJ_OPT_EMIT_SLOTS && (value < 0 || value > 4096)) ||
-      (opt == MIJ_OPT_FAULT_TICKET && (value < 0 || value > 1 << 20)) ||
       (opt == MIJ_OPT_PACK_SEGS && (value < -1 || value > 15)))
     return fail(MIJ_EINVAL, "set_option: value %d out of range for option %d", value, opt);
   if (opt == MIJ_OPT_OVERLAP_PRIO && b->stream2)
@@ -1198,8 +1202,18 @@ extern "C" int mij_batch_set_option(mij_batch *b, int opt, int value) {
 }
 
 extern "C" int mij_batch_get_option(mij_batch *b, int opt) {
-  if (!b || opt < 0 || opt >= MIJ_OPT_COUNT) return fail(MIJ_EINVAL, "get_option: bad args"), -2;
+  if (!b || opt < 0 || opt >= MIJ_OPT_COUNT || opt == OPT_TEST_FAULT_TICKET)
+    return fail(MIJ_EINVAL, "get_option: bad args"), -2;
   return b->opt[opt];
+}
+
+// test-only (csrc/mij_testing.h, not the public header): arm the stale-ticket
+// fault for the next encode; returns the value that was armed before
+extern "C" int mij_test_stale_ticket(mij_batch *b, int v) {
+  if (!b || v < 0 || v > 1 << 20) return fail(MIJ_EINVAL, "test_stale_ticket: bad args"), -2;
+  const int old = b->opt[OPT_TEST_FAULT_TICKET];
+  b->opt[OPT_TEST_FAULT_TICKET] = v;
+  return old;
 }
 
 extern "C" int mij_batch_dct(mij_batch *b, int nframes) {

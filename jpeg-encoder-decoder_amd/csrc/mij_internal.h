@@ -24,10 +24,16 @@ constexpr int DCTIE_WORDS = 33;      // DC tie bits for K = 0..1055 (|S| <= 8192
 constexpr int FERR_TABLE = 1;     // Huffman construction outside the reference's defined behaviour
 constexpr int FERR_OVERFLOW = 2;  // bits past a scan buffer (tokens no K1 wrote): nothing written
 constexpr int FERR_ASSEMBLY = 3;  // band assembly: a piece outside its buffer
+// option slot 7 (reserved in include/mijpeg.h): the test suite's stale-ticket
+// fault, armed only through mij_test_stale_ticket (csrc/mij_testing.h)
+constexpr int OPT_TEST_FAULT_TICKET = 7;
 constexpr int FERR_SPIN = 4;      // a device-side wait outlasted SPIN_TICKS, or a stale pack ticket
-// bound of every device-side wait (s_memrealtime ticks, 100 MHz: 100 ms); the
-// waits are microseconds long when the state they wait on is intact
-constexpr unsigned long long SPIN_TICKS = 10000000ull;
+// bound of every device-side wait without progress (s_memrealtime ticks,
+// 100 MHz: 2 s); the waits are microseconds long when the state they wait on
+// is intact, and the bound is long enough for a queue switched out under
+// multi-process time-slicing (the pack look-back restarts it whenever a
+// predecessor's state word changes)
+constexpr unsigned long long SPIN_TICKS = 200000000ull;
 
 // ---- entropy stage: segments ---------------------------------------------
 // A segment is the run of blocks one K1 N-tile covers in a component's scan

@@ -1027,7 +1027,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
       };
       // N-tile nt: the error bound of its N (lanes of a block: its L1) and
       // the three digits
-      auto dct_ntile = [&](const int nt, v4i (&acc)[4], float &lc) {
+      auto dct_ntile = [&](const int nt, v4i (&acc)[4], uint32_t &lc) {
         const v4i Bp = *(const v4i *)(L + (nt * 16 + bcol) * LDS_BLK + 16 * g);
         // L1 = sum |pixel - 128| of the block bounds the integer DCT's
         // rounding error: |N - 2^19 sum K X| <= sum |W - 2^19 K| |X| <= L1 / 2
@@ -1040,13 +1040,15 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
         const uint32_t L1 = r32[0] + r32[1];
         if (nt < 2) {
           // luma, integer rule: E = floor(L1 / 2) + 1 >= L1 / 2 + the
-          // reference's own FP64 rounding (< 1e-3 in N' units), kept as bits
-          lc = __uint_as_float((L1 >> 1) + 1u);
+          // reference's own FP64 rounding (< 1e-3 in N' units), an integer
+          lc = (L1 >> 1) + 1u;
         } else {
           // chroma, fp32 rule: 1.25 * (L1/2 + 64) for the integer DCT and
           // float(N'), + 0.095 L1 for the fp32 roundings of t -+ tau (<= 1.8e-7
           // |N'| with |N'| <= 2^19 L1)
-          lc = fmaf((float)L1, 0.72f, 80.0f);
+          // (the float's bits: lc is a uint32_t, so no float value ever
+          // holds the luma bound's integer bits)
+          lc = __float_as_uint(fmaf((float)L1, 0.72f, 80.0f));
         }
         const v4i Bf = Bp ^ (int)0x80808080;  // pixel - 128 as int8
 #pragma unroll
@@ -1189,7 +1191,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
         // coefficient variant spills at 168 VGPRs with it, 3.12 -> 3.18)
         constexpr bool PIPE = TOK;
         v4i accs[PIPE ? 2 : 1][4];
-        float lcs[PIPE ? 2 : 1];  // per block: error bound of N in N units
+        uint32_t lcs[PIPE ? 2 : 1];  // per block: error bound of N (luma: integer E; chroma: fp32 bits)
         if (PIPE) dct_ntile(0, accs[0], lcs[0]);
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
@@ -1201,7 +1203,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
             dct_ntile(nt + 1, accs[PIPE ? (cur ^ 1) : 0], lcs[PIPE ? (cur ^ 1) : 0]);
           }
           v4i(&acc)[4] = accs[cur];
-          const float lc = lcs[cur];
+          const uint32_t lcb = lcs[cur];
           int o[16];
           // Chroma N-tile: when |N| < L_z (Tables::czl) for every AC
           // coefficient of every lane, all of them quantise to 0 (the
@@ -1277,7 +1279,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
             for (int k = 0; k < 16; k++) o[k] = acc[k >> 2][k & 3];
             hz = 0;
           } else if (nt < 2) {
-            const uint32_t E = __float_as_uint(lc);
+            const uint32_t E = lcb;
             const uint32_t E1 = E + 1u, EE = 2u * E + 1u;  // hi - EE = a - E
             // one OR per M-tile (4 coefficients): the rare path recomputes only
             // the M-tiles some lane flags
@@ -1289,6 +1291,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
 #pragma unroll
             for (int m = 0; m < 4; m++) {
               const float4 fac = *(const float4 *)&s_fac[comp][16 * g + 4 * m];
+              const float lc = __uint_as_float(lcb);
               const f2v lc2 = {lc, lc};
 #pragma unroll
               for (int h = 0; h < 2; h++) {
@@ -1328,14 +1331,14 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
               for (int r = 0; r < 4; r++) {
                 const int k = 4 * m + r;
                 if (nt < 2) {
-                  const uint32_t E = __float_as_uint(lc);
+                  const uint32_t E = lcb;
                   uint32_t x = 0;
                   (void)lquant(acc[m][r], E + 1u, 2u * E + 1u, kq, x);
                   mm |= (uint32_t)((x >> kq) != 0) << k;
                 } else {
                   const float nf = (float)acc[m][r];
                   const float fa = s_fac[comp][16 * g + k];
-                  const float tv = fmaf(fa, lc, 1.0e-6f);
+                  const float tv = fmaf(fa, __uint_as_float(lcb), 1.0e-6f);
                   mm |= (uint32_t)((int)fmaf(nf, fa, -tv) != (int)fmaf(nf, fa, tv)) << k;
                 }
               }
@@ -3164,7 +3167,11 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
     if (q > 0) {
       prefix = 0;
       long long j = gid - 1;
-      const unsigned long long t_wait = __builtin_amdgcn_s_memrealtime();
+      // the bound counts from the last progress seen (a predecessor's
+      // state word changing, or the window moving back), so a long but
+      // live wait -- a predecessor slowed by time-slicing -- never trips it
+      unsigned long long t_wait = __builtin_amdgcn_s_memrealtime();
+      unsigned long long seen = ~0ull;
       while (true) {
         const long long jj = j - lane;
         unsigned long long sv = jj >= gscan0 ? __hip_atomic_load(&stt[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
@@ -3173,15 +3180,21 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
         const unsigned long long upto = m2 ? (m2 & (~m2 + 1)) : 0ull;  // lowest inclusive lane
         if (m0 & (upto ? upto - 1 : ~0ull)) {  // a group before it has not published yet
           // (groups publish in claim order, so this wait is short; one that
-          // outlasts SPIN_TICKS means a lost publication: the frame fails
-          // instead of the launch hanging)
-          if (__builtin_amdgcn_s_memrealtime() - t_wait > SPIN_TICKS) {
+          // outlasts SPIN_TICKS without progress means a lost publication:
+          // the frame fails instead of the launch hanging)
+          const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+          if (m0 != seen) {
+            seen = m0;
+            t_wait = now;
+          } else if (now - t_wait > SPIN_TICKS) {
             hung = true;
             break;
           }
           __builtin_amdgcn_s_sleep(1);
           continue;
         }
+        seen = ~0ull;
+        t_wait = __builtin_amdgcn_s_memrealtime();
         const int kk = upto ? __ffsll((long long)m2) - 1 : 63;
         unsigned long long add = lane <= kk ? (sv & LB_VAL) : 0ull;
         for (int off = 32; off; off >>= 1) add += __shfl_xor(add, off);

@@ -22,6 +22,7 @@
 #include <atomic>
 #include <chrono>
 #include <functional>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -243,12 +244,15 @@ static double now_s() {
 }
 
 // runs job(i) for i in [0, n) on up to `threads` host threads; returns the
-// first nonzero result (by index) or 0
+// first nonzero result (by index) or 0.  A failing job's error (thread-local
+// to the worker that ran it) is raised again on the calling thread.
 static int parallel_for(int n, int threads, const std::function<int(int)> &job, int *failed) {
   std::vector<int> rc(n, 0);
+  std::vector<std::string> msg(n);
   std::atomic<int> next{0};
   auto worker = [&]() {
-    for (int i; (i = next.fetch_add(1)) < n;) rc[i] = job(i);
+    for (int i; (i = next.fetch_add(1)) < n;)
+      if ((rc[i] = job(i))) msg[i] = mij_last_message();
   };
   const int nt = std::min(n, threads);
   std::vector<std::thread> pool;
@@ -258,7 +262,7 @@ static int parallel_for(int n, int threads, const std::function<int(int)> &job, 
   for (int i = 0; i < n; i++)
     if (rc[i]) {
       if (failed) *failed = i;
-      return rc[i];
+      return mij_fail(rc[i], "%s", msg[i].c_str());
     }
   return 0;
 }
@@ -302,11 +306,13 @@ static int stream_run(mij_stream *s, int n, const FillFn &fill, const DrainFn &d
     std::thread th;
     int rc = MIJ_OK, bad = -1;
     double secs = 0.0;
+    std::string msg;  // the reader thread's error, raised again by join_read
   } rd[NIN];
   auto start_read = [&](int k) -> int {
     Read &r = rd[k % NIN];
     r.rc = MIJ_OK;
     r.bad = -1;
+    r.msg.clear();
     // batch k & 1's input is free once chunk k - 2's encode has run (its
     // uploads wait for that on the upload stream; the reads do not)
     if (k >= 2) S_TRY(hipStreamWaitEvent(s->st_up, s->ev_in_free[k & 1], 0));
@@ -325,6 +331,18 @@ static int stream_run(mij_stream *s, int n, const FillFn &fill, const DrainFn &d
         return rc ? rc : mij_batch_upload_slot_async(bk, fd, i, s->st_up);
       }, &r.bad);
       if (r.rc && r.bad >= 0) r.bad += first;
+      if (r.rc) {
+        r.msg = mij_last_message();
+      } else {
+        // every upload of chunk k is on the upload stream now, and nothing
+        // of chunk k + 1 yet (start_read(k + 1) runs after join_read(k)):
+        // the event covers exactly this chunk's copies
+        if (hipEventRecord(s->ev_up[k % NIN], s->st_up) != hipSuccess ||
+            (trace && hipEventRecord(tr[k].up, s->st_up) != hipSuccess)) {
+          r.rc = MIJ_EHIP;
+          r.msg = "stream: recording a chunk's upload event failed";
+        }
+      }
       r.secs = now_s() - t0;
       if (trace) tr[k].r1 = now_s() - t_start;
     });
@@ -335,20 +353,20 @@ static int stream_run(mij_stream *s, int n, const FillFn &fill, const DrainFn &d
     if (r.th.joinable()) r.th.join();
     s->stats[1] += r.secs;
     if (r.rc && failed) *failed = r.bad;
+    // (the reader thread's error is thread-local to it: raised again here,
+    // on the caller's thread, naming the frame)
+    if (r.rc) return r.bad >= 0 ? mij_fail(r.rc, "stream: frame %d: %s", r.bad, r.msg.c_str())
+                                : mij_fail(r.rc, "%s", r.msg.c_str());
     return r.rc;
   };
 
   auto enqueue = [&](int k) -> int {
     const int sl = k & 1, cnt = count(k);
     int rc;
-    // (the frames' uploads were enqueued on the upload stream by the reader
-    // threads, all before this: buffer k % NIN is free and the batch's input
-    // is in once the copies before this event are done)
-    S_TRY(hipEventRecord(s->ev_up[k % NIN], s->st_up));
-    if (trace) {
-      tr[k].enq = now_s() - t_start;
-      S_TRY(hipEventRecord(tr[k].up, s->st_up));
-    }
+    // (the reader thread recorded ev_up[k % NIN] after chunk k's last
+    // upload: buffer k % NIN is free and the batch's input is in once it
+    // completes)
+    if (trace) tr[k].enq = now_s() - t_start;
     S_TRY(hipStreamWaitEvent(s->st[sl], s->ev_up[k % NIN], 0));
     S_TRY(hipEventRecord(s->ev_t0[sl], s->st[sl]));
     if ((rc = mij_batch_encode(s->b[sl], cnt))) return rc;

@@ -71,7 +71,7 @@ class MijError(RuntimeError):
 
 # mij_batch_set_option (include/mijpeg.h: MIJ_OPT_*)
 OPTIONS = {"seam": 0, "ff_pack": 1, "actab": 2, "segdc_fused": 3, "pack_wide": 4, "emit_slots": 5,
-           "overlap_prio": 6, "fault_ticket": 7, "pack_segs": 8}
+           "overlap_prio": 6, "pack_segs": 8}
 
 
 _lib = None

@@ -42,6 +42,20 @@ def reduce_timing(elapsed_s: float, units: int, dist=None, device=None):
     return float(t.item()), int(u.item())
 
 
+def gather_ints(values, dist=None, device=None):
+    """Every rank's list of ints (same length on every rank), in rank order:
+    [[rank 0's values], [rank 1's], ...].  One all-gather; a single process
+    returns [values]."""
+    vals = [int(v) for v in values]
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return [vals]
+    import torch
+    t = torch.tensor(vals, dtype=torch.int64, device=device)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [[int(x) for x in o.cpu().tolist()] for o in out]
+
+
 # ---------------------------------------------------------------------------
 # one large frame over several ranks (SURVEY.md §8(e), config 4)
 # ---------------------------------------------------------------------------

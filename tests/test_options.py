@@ -154,7 +154,8 @@ def test_option_validation():
 
 def test_stale_pack_ticket_fails_the_frame_instead_of_hanging():
     """Every device-side wait is bounded (mij_internal.h SPIN_TICKS).  A
-    stale pack ticket (MIJ_OPT_FAULT_TICKET: frame 0's luma ticket starts at
+    stale pack ticket (mij_test_stale_ticket, csrc/mij_testing.h -- a
+    test-only entry point, not the public option enum: frame 0's luma ticket starts at
     1, so pack group 0 never runs and group 1's look-back waits for a
     publication that never comes) fails frame 0 with MIJ_EHANG within the
     bound, the other frames stay byte-exact, and the next encode of the same
@@ -164,20 +165,34 @@ def test_stale_pack_ticket_fails_the_frame_instead_of_hanging():
     want = [O.cref_encode(f) for f in frames]
     b = mijpeg.Batch(W, H, 3)
     b.upload(frames)
-    b.set_option("fault_ticket", 1)
+    import ctypes as C
+    arm = b.lib.mij_test_stale_ticket
+    arm.argtypes, arm.restype = [C.c_void_p, C.c_int], C.c_int
+    assert arm(b.h_, 1) == 0
     t0 = time.time()
     b.encode(3)
     b.sync()
-    assert time.time() - t0 < 10.0, "the bounded wait should end in ~0.1 s"
+    assert time.time() - t0 < 10.0, "the bounded wait (2 s without progress) should end the wait"
     with pytest.raises(mijpeg.MijError, match="outlasted its bound"):
         b.output(0)
     assert b.lib.mij_last_error() == 9  # MIJ_EHANG
     for i in (1, 2):
         assert b.output(i) == want[i]
-    assert b.get_option("fault_ticket") == 0  # consumed
+    assert arm(b.h_, 0) == 0  # consumed by that encode
     b.encode(3)
     _check(b, frames, 3, 50, want)
     b.close()
+
+
+def test_reserved_option_slot_is_not_settable():
+    """Option slot 7 is the test suite's fault hook: the public option calls
+    refuse it (include/mijpeg.h marks it reserved)."""
+    b = mijpeg.Batch(W, H, 1)
+    try:
+        assert b.lib.mij_batch_set_option(b.h_, 7, 1) != 0
+        assert b.lib.mij_batch_get_option(b.h_, 7) == -2
+    finally:
+        b.close()
 
 
 def test_get_option_error_raises():
