@@ -337,13 +337,14 @@ constexpr uint32_t MAGIC_BITS = 0x4B400000u;
 // bits lie in [1, 1023]).  tests/colour_check.c checks both over all 2^24
 // colours.  This replaced a +0.0005 bias, a truncating conversion and a
 // fract per pixel (two slow-class VALU ops) by one fast shift and one AND.
-// Outputs: yb = Y in magic form, cbm/crm = chroma in magic form, cc/cy = the
-// run holds a possible Cb/Cr resp. Y exception.
+// Outputs: yb = Y in magic form, cbm/crm = chroma in magic form, pd = 0 when
+// the run holds a possible Cb/Cr exception, cy = it holds a possible Y one.
 constexpr float YMAGIC = 12288.0f;  // 1.5 * 2^13
 struct Run4 {
   uint32_t yb[4];
   uint32_t cbm[4], crm[4];
-  bool cc, cy;
+  float pd;  // product of the run's R-G and B-G differences (0: a possible Cb/Cr exception)
+  bool cy;
 };
 
 template <bool RGB>
@@ -380,9 +381,11 @@ __device__ __forceinline__ void convert4(uint32_t w0, uint32_t w1, uint32_t w2, 
     }
   }
   // some pixel has R == G or B == G: the product of the 8 (exact, integer)
-  // differences is 0 (|product| <= 255^8, no underflow or overflow)
+  // differences is 0; colour_stage multiplies the two rows' products (16
+  // nonzero integer factors: |product| <= 255^16 < 2^128, no overflow, and
+  // >= 1, no underflow) and tests once per run pair
   const f2v pd = (dr[0] * db[0]) * (dr[1] * db[1]);
-  o.cc = pd[0] * pd[1] == 0.0f;
+  o.pd = pd[0] * pd[1];
   // some pixel has an exact-integer Y: the low 10 bits of its magic form are 0
   const uint32_t m01 = min(o.yb[0] & 0x3FFu, o.yb[1] & 0x3FFu), m23 = min(o.yb[2] & 0x3FFu, o.yb[3] & 0x3FFu);
   o.cy = min(m01, m23) == 0u;
@@ -550,7 +553,7 @@ __device__ __forceinline__ void colour_stage(const uint8_t *raw, uint8_t *L, int
                                                      c4 | (pr << 5));
         if (corr) *Yd[dy] = py[dy] - corr;  // no borrows: a corrected Y is >= 1
       }
-    if (__ballot(r[0].cc | r[1].cc)) {
+    if (__ballot(r[0].pd * r[1].pd == 0.0f)) {
       uint32_t cbc[2][4], crc[2][4];
 #pragma unroll
       for (int dy = 0; dy < 2; dy++)
