@@ -2,7 +2,7 @@
  * public C ABI (include/mijpeg.h); the test suite binds them by name. */
 #ifndef MIJ_TESTING_H
 #define MIJ_TESTING_H
-#include "../../include/mijpeg.h"
+#include "mijpeg.h"
 #ifdef __cplusplus
 extern "C" {
 #endif

@@ -127,3 +127,13 @@ def test_division_magic(tmp_path):
     out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     assert out.stdout.startswith("ok")
+
+
+def test_fault_hook_is_not_public_abi():
+    """The stale-ticket fault injection is a test-only entry point
+    (csrc/mij_testing.h): exported for the GPU tests, absent from the public
+    header and from the option enum."""
+    src = open(HEADER).read()
+    assert "FAULT" not in src and "mij_test_" not in src
+    assert "fault_ticket" not in mijpeg.OPTIONS
+    assert hasattr(mijpeg.load(), "mij_test_stale_ticket")
