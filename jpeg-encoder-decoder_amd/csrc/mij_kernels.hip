@@ -2930,6 +2930,13 @@ constexpr int EMIT_CW = EMIT_CH / 4;  // stream words per emit chunk
 // ===========================================================================
 constexpr int PF_THREADS = 256, PF_WAVES = PF_THREADS / 64;
 constexpr int PF_K = 2, PF_OCC = 8, PF_OCC_WIDE = 6;
+// PF_PAIR (round 6): a thread's two chunks of a round are consecutive in the
+// stream, so one segment search and one wave scan serve both (0: the chunks
+// 256 apart, two searches and two scans per round)
+#ifndef PF_PAIR
+#define PF_PAIR 1
+#endif
+static_assert(!PF_PAIR || PF_K == 2, "k_pack_flat: the pair mapping takes two chunks per thread");
 template <int PW>
 constexpr int pf_occ() { return PW > PACK_WORDS ? PF_OCC_WIDE : PF_OCC; }
 static_assert(PACK_SEGS_MAX == PF_THREADS, "k_pack_flat: a thread per segment of the widest group");
@@ -3033,17 +3040,37 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   for (uint32_t i = 4u * tid; i < wz; i += 4u * PF_THREADS) *(u4v *)&buf[i] = u4v{0u, 0u, 0u, 0u};
   const uint32_t *tokg = a.tok + fs0 * SEG_TOK;
   // chunk c's 4 tokens (c < C): its segment s is the last with s_cp[s] <= c
-  auto chunk_load = [&](uint32_t c, u4v &t) {
-    t = u4v{0u, 0u, 0u, 0u};
-    if (c >= C) return;
+  auto chunk_seg = [&](uint32_t c) -> int {
     int s = 0;
 #pragma unroll
     for (int step = PACK_SEGS_MAX / 2; step; step >>= 1)  // (entries past the group read ~0)
       if (s_cp[s + step] <= c) s += step;
+    return s;
+  };
+  auto chunk_at = [&](uint32_t c, int s, u4v &t) {
     const uint32_t o = 4u * (c - s_cp[s]);
     t = *(const u4v *)(tokg + (long long)s * SEG_TOK + o);
     if (o == 0) t[0] = a.tok0[fs0 + s];  // token 0 of a segment (dense array)
   };
+  auto chunk_load = [&](uint32_t c, u4v &t) {
+    t = u4v{0u, 0u, 0u, 0u};
+    if (c >= C) return;
+    chunk_at(c, chunk_seg(c), t);
+  };
+#if PF_PAIR
+  // a thread's two chunks of a round are consecutive (c, c + 1): one search
+  // for the first, and the second's segment is the first's or a later one
+  // (later than the next only past empty segments: region batches)
+  auto pair_load = [&](uint32_t c, u4v (&t)[2]) {
+    t[0] = t[1] = u4v{0u, 0u, 0u, 0u};
+    if (c >= C) return;
+    int s = chunk_seg(c);
+    chunk_at(c, s, t[0]);
+    if (c + 1 >= C) return;
+    while (s_cp[s + 1] <= c + 1) s++;
+    chunk_at(c + 1, s, t[1]);
+  };
+#endif
   // a chunk's bits: per token the code (magnitude bits included) and its
   // ZRLs (encoder.c:490-494); merged into one left-growing string when they
   // fit 64 bits
@@ -3065,6 +3092,12 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   // tid), all loaded at once, and needs one barrier; with `publish` the
   // group's aggregate goes out as soon as the last round's scan has it,
   // before that round is placed.
+  // chunk k of this thread in a round, relative to the round's first chunk:
+  // PF_PAIR, the thread's PF_K chunks back to back (2 tid, 2 tid + 1);
+  // otherwise interleaved (k * 256 + tid)
+  auto chunk_of = [&](int k) -> uint32_t {
+    return PF_PAIR ? (uint32_t)(PF_K * tid + k) : (uint32_t)(k * PF_THREADS + tid);
+  };
   auto sweep = [&](bool whole, uint32_t boff, uint32_t lo_bit, uint32_t hi_bit, bool publish) -> uint32_t {
     const uint32_t lim = (wz - 1) * 32;  // the zeroed words, one spare for the shifted store
     uint32_t r0 = 0;
@@ -3077,16 +3110,24 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
     uint32_t run = boff + s_run[r0];
     bool over = false;
     u4v tn[PF_K];  // the next round's chunks, loaded while a round is placed
+#if PF_PAIR
+    pair_load(r0 * PF_K * PF_THREADS + chunk_of(0), tn);
+#else
 #pragma unroll
-    for (int k = 0; k < PF_K; k++) chunk_load(r0 * PF_K * PF_THREADS + k * PF_THREADS + tid, tn[k]);
+    for (int k = 0; k < PF_K; k++) chunk_load(r0 * PF_K * PF_THREADS + chunk_of(k), tn[k]);
+#endif
     for (uint32_t c0 = r0 * PF_K * PF_THREADS, r = r0; c0 < C && (whole || run < hi_bit);
          c0 += PF_K * PF_THREADS, r++) {
       u4v t[PF_K];
 #pragma unroll
       for (int k = 0; k < PF_K; k++) t[k] = tn[k];
       if (c0 + PF_K * PF_THREADS < C) {
+#if PF_PAIR
+        pair_load(c0 + PF_K * PF_THREADS + chunk_of(0), tn);
+#else
 #pragma unroll
-        for (int k = 0; k < PF_K; k++) chunk_load(c0 + (PF_K + k) * PF_THREADS + tid, tn[k]);
+        for (int k = 0; k < PF_K; k++) chunk_load(c0 + PF_K * PF_THREADS + chunk_of(k), tn[k]);
+#endif
       }
       uint32_t nb[PF_K], x[PF_K];
       unsigned long long acc[PF_K];
@@ -3094,18 +3135,39 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
       for (int k = 0; k < PF_K; k++) {
         uint32_t L[4], code[4], nzr[4];
         nb[k] = decode(t[k], L, code, nzr);  // (a chunk past the group: zero tokens, no bits)
-        if (c0 + k * PF_THREADS + tid >= C) nb[k] = 0;
+        if (c0 + chunk_of(k) >= C) nb[k] = 0;
         acc[k] = 0;
 #pragma unroll
         for (int e = 0; e < 4; e++) {
           for (uint32_t z = nzr[e]; z; z--) acc[k] = (acc[k] << Lz) | zcode;
           acc[k] = (acc[k] << L[e]) | code[e];
         }
+#if !PF_PAIR
         x[k] = wave_scan64(nb[k]);
         if (lane == 63) s_ws[r & 1][k][wave] = x[k];
+#endif
       }
+#if PF_PAIR
+      // one scan of the pair's bits: the two chunks are consecutive in the stream
+      x[0] = wave_scan64(nb[0] + nb[1]);
+      if (lane == 63) s_ws[r & 1][0][wave] = x[0];
+#endif
       __syncthreads();
       uint32_t pos[PF_K];
+#if PF_PAIR
+      {
+        uint32_t before = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < PF_WAVES; w++) {
+          const uint32_t v = s_ws[r & 1][0][w];
+          tot += v;
+          before += w < wave ? v : 0u;
+        }
+        pos[0] = run + before + x[0] - nb[0] - nb[1];
+        pos[1] = pos[0] + nb[0];
+        run += tot;
+      }
+#else
 #pragma unroll
       for (int k = 0; k < PF_K; k++) {
         uint32_t before = 0, tot = 0;
@@ -3118,6 +3180,7 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
         pos[k] = run + before + x[k] - nb[k];
         run += tot;
       }
+#endif
       if (publish && c0 + PF_K * PF_THREADS >= C && tid == 0 && q > 0)
         __hip_atomic_store(&a.pack_state[gid], LB_AGG | (run - boff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (whole && tid == 0) s_run[r + 1] = run;  // (read after the look-back's barrier)
@@ -3133,7 +3196,7 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
           else put_bits64_win(buf, p0, acc[k] << (64 - n), n, lo_bit, hi_bit);
         } else {  // more than 64 bits (rare): the chunk again, token by token
           u4v tt;
-          chunk_load(c0 + k * PF_THREADS + tid, tt);
+          chunk_load(c0 + chunk_of(k), tt);
           uint32_t L[4], code[4], nzr[4];
           decode(tt, L, code, nzr);
           uint32_t p = p0;
