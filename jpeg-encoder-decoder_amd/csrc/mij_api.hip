@@ -651,16 +651,17 @@ static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0, bool band = false
   a.fdims = b->use_fdims ? b->d_fdims : nullptr;
   // JFIF-assembly workgroups per frame (its chunks dealt round-robin over
   // the three scans; A/B per scan in round 2, profiles/r02/emit_slots_ab.txt):
-  // 16 on large low-Q batches (emit 0.247 -> 0.232 ms at config 3, Q=50),
-  // 64 otherwise (Q=90: 0.62 at 64 against 0.68 at 16; a single frame needs
+  // 48 on large batches at any quality (round 6 sweep on config 3,
+  // scripts/emit_sweep.sh, profiles/r06/probe/emit_slots.txt: emit 0.146 ms
+  // at 48 against 0.154-0.189 at 16-384 for Q=50, 0.383 against 0.401 at the
+  // former 192 for Q=90), 1536 on frames of 8 Mpixels and more (config 4: few
+  // scans of hundreds of chunks each), 192 otherwise (a single frame needs
   // the width)
-  // 512 on frames of 8 Mpixels and more (config 4: few scans of hundreds of
-  // chunks each)
   const int slots_opt = b->opt[MIJ_OPT_EMIT_SLOTS];
-  a.emit_slots = slots_opt > 0                           ? slots_opt
-                 : (nframes >= 43 && b->quality <= 60)   ? 48
-                 : ((long long)b->g.w * b->g.h >= (8 << 20)) ? 1536
-                                                           : 192;
+  a.emit_slots = slots_opt > 0                                 ? slots_opt
+                 : nframes >= 43                               ? 48
+                 : ((long long)b->g.w * b->g.h >= (8 << 20))    ? 1536
+                                                                : 192;
   a.pack_wide = ent_args_pack_wide(b);
   ent_args_pack_ls(b, nframes, a.pack_ls);
   if (f0) {  // sub-batch: frames f0.. of the batch (every per-frame array shifted)
