@@ -2902,7 +2902,7 @@ constexpr int EMIT_CW = EMIT_CH / 4;  // stream words per emit chunk
 // bitstream is its segments' token strings back to back, and K1 pads every
 // segment to a multiple of 4 tokens (LB_NOTOK, no bits), so the group is a
 // list of 4-token chunks, each inside one segment slot and 16-byte aligned.
-// Every thread takes PF_K chunks per round (the segment of a chunk by binary
+// Every thread takes K consecutive chunks per round (the first's segment by binary
 // search of the chunk counts' prefix), merges each chunk's 4 tokens into one
 // bit string, and a workgroup scan of the string lengths places them in the
 // LDS window relative to the group's first bit -- every token is read and
@@ -2930,13 +2930,18 @@ constexpr int EMIT_CW = EMIT_CH / 4;  // stream words per emit chunk
 // ===========================================================================
 constexpr int PF_THREADS = 256, PF_WAVES = PF_THREADS / 64;
 constexpr int PF_K = 2, PF_OCC = 8, PF_OCC_WIDE = 6;
-// PF_PAIR (round 6): a thread's two chunks of a round are consecutive in the
-// stream, so one segment search and one wave scan serve both (0: the chunks
-// 256 apart, two searches and two scans per round)
-#ifndef PF_PAIR
-#define PF_PAIR 1
+// Round 6: a thread's chunks of a round are consecutive in the stream (chunks
+// K tid .. K tid + K - 1 of the round), so one segment search and one wave
+// scan serve all K of them (round 5: chunks tid + 256 k, a search and a scan
+// each).  PF_K_WIDE: chunks per thread for the wide window (high quality),
+// whose LDS holds it at 6 workgroups per CU; measured at Q=90 (one box,
+// three rounds): 2 chunks 1.238-1.244 ms, 3 chunks 1.265-1.267 (no spills,
+// fewer rounds per group, but longer rounds), 4 chunks spill 13 VGPRs.
+#ifndef PF_K_WIDE
+#define PF_K_WIDE 2
 #endif
-static_assert(!PF_PAIR || PF_K == 2, "k_pack_flat: the pair mapping takes two chunks per thread");
+template <int PW>
+constexpr int pf_k() { return PW > PACK_WORDS ? PF_K_WIDE : PF_K; }
 template <int PW>
 constexpr int pf_occ() { return PW > PACK_WORDS ? PF_OCC_WIDE : PF_OCC; }
 static_assert(PACK_SEGS_MAX == PF_THREADS, "k_pack_flat: a thread per segment of the widest group");
@@ -2949,10 +2954,11 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   // the first pass's bit offset at every round start (the windowed path
   // starts a window's sweep at the round it begins in), and the first bit it
   // could not place
-  constexpr int PF_ROUNDS = (PACK_SEGS_MAX * (SEG_TOK / 4) + PF_K * PF_THREADS - 1) / (PF_K * PF_THREADS);
+  constexpr int K = pf_k<PW>();  // chunks per thread and round
+  constexpr int PF_ROUNDS = (PACK_SEGS_MAX * (SEG_TOK / 4) + K * PF_THREADS - 1) / (K * PF_THREADS);
   __shared__ uint32_t s_run[PF_ROUNDS + 1];
   __shared__ uint32_t s_p1;
-  __shared__ uint32_t s_ws[2][PF_K][PF_WAVES];  // a round's bits per chunk set and wave (two rounds in turn)
+  __shared__ uint32_t s_ws[2][PF_WAVES];  // a round's bits per wave (two rounds in turn)
   __shared__ unsigned long long s_prefix;
   __shared__ int s_ticket;
   __shared__ uint32_t s_over;
@@ -3057,20 +3063,22 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
     if (c >= C) return;
     chunk_at(c, chunk_seg(c), t);
   };
-#if PF_PAIR
-  // a thread's two chunks of a round are consecutive (c, c + 1): one search
-  // for the first, and the second's segment is the first's or a later one
-  // (later than the next only past empty segments: region batches)
-  auto pair_load = [&](uint32_t c, u4v (&t)[2]) {
-    t[0] = t[1] = u4v{0u, 0u, 0u, 0u};
+  // a thread's K chunks of a round are consecutive (c .. c + K - 1): one
+  // search for the first, and each next chunk's segment is the one before or
+  // a later one (later than the next only past empty segments: region batches)
+  auto run_load = [&](uint32_t c, u4v (&t)[K]) {
+#pragma unroll
+    for (int k = 0; k < K; k++) t[k] = u4v{0u, 0u, 0u, 0u};
     if (c >= C) return;
     int s = chunk_seg(c);
     chunk_at(c, s, t[0]);
-    if (c + 1 >= C) return;
-    while (s_cp[s + 1] <= c + 1) s++;
-    chunk_at(c + 1, s, t[1]);
+#pragma unroll
+    for (int k = 1; k < K; k++) {
+      if (c + k >= C) break;
+      while (s_cp[s + 1] <= c + k) s++;
+      chunk_at(c + k, s, t[k]);
+    }
   };
-#endif
   // a chunk's bits: per token the code (magnitude bits included) and its
   // ZRLs (encoder.c:490-494); merged into one left-growing string when they
   // fit 64 bits
@@ -3088,51 +3096,35 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   // first bit (+ boff); whole: every bit into the window (a chunk past it
   // sets the overflow flag and is left out), else only the bits inside
   // [lo_bit, hi_bit), from the round that window starts in to the round that
-  // passes its end.  A round takes PF_K chunks per thread (chunk c0 + 256 k +
-  // tid), all loaded at once, and needs one barrier; with `publish` the
+  // passes its end.  A round takes K chunks per thread (chunks c0 + K tid +
+  // k), all loaded at once, and needs one barrier; with `publish` the
   // group's aggregate goes out as soon as the last round's scan has it,
   // before that round is placed.
-  // chunk k of this thread in a round, relative to the round's first chunk:
-  // PF_PAIR, the thread's PF_K chunks back to back (2 tid, 2 tid + 1);
-  // otherwise interleaved (k * 256 + tid)
-  auto chunk_of = [&](int k) -> uint32_t {
-    return PF_PAIR ? (uint32_t)(PF_K * tid + k) : (uint32_t)(k * PF_THREADS + tid);
-  };
+  // chunk k of this thread in a round, relative to the round's first chunk
+  auto chunk_of = [&](int k) -> uint32_t { return (uint32_t)(K * tid + k); };
   auto sweep = [&](bool whole, uint32_t boff, uint32_t lo_bit, uint32_t hi_bit, bool publish) -> uint32_t {
     const uint32_t lim = (wz - 1) * 32;  // the zeroed words, one spare for the shifted store
     uint32_t r0 = 0;
     if (!whole) {  // the last round starting at or before lo_bit (s_run from the whole pass)
-      const uint32_t nr = (C + PF_K * PF_THREADS - 1) / (PF_K * PF_THREADS);
+      const uint32_t nr = (C + K * PF_THREADS - 1) / (K * PF_THREADS);
 #pragma unroll
       for (uint32_t step = 128; step; step >>= 1)
         if (r0 + step < nr && boff + s_run[r0 + step] <= lo_bit) r0 += step;
     }
     uint32_t run = boff + s_run[r0];
     bool over = false;
-    u4v tn[PF_K];  // the next round's chunks, loaded while a round is placed
-#if PF_PAIR
-    pair_load(r0 * PF_K * PF_THREADS + chunk_of(0), tn);
-#else
+    u4v tn[K];  // the next round's chunks, loaded while a round is placed
+    run_load(r0 * K * PF_THREADS + chunk_of(0), tn);
+    for (uint32_t c0 = r0 * K * PF_THREADS, r = r0; c0 < C && (whole || run < hi_bit);
+         c0 += K * PF_THREADS, r++) {
+      u4v t[K];
 #pragma unroll
-    for (int k = 0; k < PF_K; k++) chunk_load(r0 * PF_K * PF_THREADS + chunk_of(k), tn[k]);
-#endif
-    for (uint32_t c0 = r0 * PF_K * PF_THREADS, r = r0; c0 < C && (whole || run < hi_bit);
-         c0 += PF_K * PF_THREADS, r++) {
-      u4v t[PF_K];
+      for (int k = 0; k < K; k++) t[k] = tn[k];
+      if (c0 + K * PF_THREADS < C) run_load(c0 + K * PF_THREADS + chunk_of(0), tn);
+      uint32_t nb[K], tot_t = 0;
+      unsigned long long acc[K];
 #pragma unroll
-      for (int k = 0; k < PF_K; k++) t[k] = tn[k];
-      if (c0 + PF_K * PF_THREADS < C) {
-#if PF_PAIR
-        pair_load(c0 + PF_K * PF_THREADS + chunk_of(0), tn);
-#else
-#pragma unroll
-        for (int k = 0; k < PF_K; k++) chunk_load(c0 + PF_K * PF_THREADS + chunk_of(k), tn[k]);
-#endif
-      }
-      uint32_t nb[PF_K], x[PF_K];
-      unsigned long long acc[PF_K];
-#pragma unroll
-      for (int k = 0; k < PF_K; k++) {
+      for (int k = 0; k < K; k++) {
         uint32_t L[4], code[4], nzr[4];
         nb[k] = decode(t[k], L, code, nzr);  // (a chunk past the group: zero tokens, no bits)
         if (c0 + chunk_of(k) >= C) nb[k] = 0;
@@ -3142,50 +3134,31 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
           for (uint32_t z = nzr[e]; z; z--) acc[k] = (acc[k] << Lz) | zcode;
           acc[k] = (acc[k] << L[e]) | code[e];
         }
-#if !PF_PAIR
-        x[k] = wave_scan64(nb[k]);
-        if (lane == 63) s_ws[r & 1][k][wave] = x[k];
-#endif
+        tot_t += nb[k];
       }
-#if PF_PAIR
-      // one scan of the pair's bits: the two chunks are consecutive in the stream
-      x[0] = wave_scan64(nb[0] + nb[1]);
-      if (lane == 63) s_ws[r & 1][0][wave] = x[0];
-#endif
+      // one scan of the thread's bits: its K chunks are consecutive in the stream
+      const uint32_t x = wave_scan64(tot_t);
+      if (lane == 63) s_ws[r & 1][wave] = x;
       __syncthreads();
-      uint32_t pos[PF_K];
-#if PF_PAIR
+      uint32_t pos[K];
       {
         uint32_t before = 0, tot = 0;
 #pragma unroll
         for (int w = 0; w < PF_WAVES; w++) {
-          const uint32_t v = s_ws[r & 1][0][w];
+          const uint32_t v = s_ws[r & 1][w];
           tot += v;
           before += w < wave ? v : 0u;
         }
-        pos[0] = run + before + x[0] - nb[0] - nb[1];
-        pos[1] = pos[0] + nb[0];
+        pos[0] = run + before + x - tot_t;
+#pragma unroll
+        for (int k = 1; k < K; k++) pos[k] = pos[k - 1] + nb[k - 1];
         run += tot;
       }
-#else
-#pragma unroll
-      for (int k = 0; k < PF_K; k++) {
-        uint32_t before = 0, tot = 0;
-#pragma unroll
-        for (int w = 0; w < PF_WAVES; w++) {
-          const uint32_t v = s_ws[r & 1][k][w];
-          tot += v;
-          before += w < wave ? v : 0u;
-        }
-        pos[k] = run + before + x[k] - nb[k];
-        run += tot;
-      }
-#endif
-      if (publish && c0 + PF_K * PF_THREADS >= C && tid == 0 && q > 0)
+      if (publish && c0 + K * PF_THREADS >= C && tid == 0 && q > 0)
         __hip_atomic_store(&a.pack_state[gid], LB_AGG | (run - boff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (whole && tid == 0) s_run[r + 1] = run;  // (read after the look-back's barrier)
 #pragma unroll
-      for (int k = 0; k < PF_K; k++) {
+      for (int k = 0; k < K; k++) {
         const uint32_t n = nb[k], p0 = pos[k];
         if (!n) continue;
         if (whole && p0 + n > lim) {
