@@ -195,7 +195,10 @@ constexpr int K1F_NO_LUT = 1, K1F_NO_REPLAY = 2, K1F_NO_COLOUR = 4, K1F_NO_DCT =
               K1F_LINEAR_STORE = 128, K1F_PLAIN_STORE = 256,
               K1F_NO_HIST = 512, K1F_NO_TOKSTORE = 1024,
               K1F_EXTRA_LDS = 2048, K1F_NO_EMIT = 4096, K1F_NO_ACLOOP = 8192,
-              K1F_NO_DMAWAIT = 16384;
+              K1F_NO_DMAWAIT = 16384,
+              K1F_REPLAY_NO_FP64 = 32768,  // replay pass without its FP64 rounds
+              K1F_COUNT_PASSES = 65536,    // the replay counter counts passes
+              K1F_COUNT_LUMA = 131072;     // ... and replays of luma N-tiles only
 
 struct EntArgs {
   Geom g;

@@ -1391,8 +1391,9 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
           if (!DEFER && __ballot(hz != 0) && !(kflags & K1F_NO_REPLAY)) {
             // rare path: find the straddling coefficients (same arithmetic) and
             // recompute them in FP64 exactly as encoder.c:87-109
-            uint32_t mm = straddle_mask(need_mtiles());
-            nrep += (uint32_t)__popc(mm);
+            const uint32_t mm = straddle_mask(need_mtiles());
+            if (!(kflags & K1F_COUNT_LUMA) || nt < 2)
+              nrep += (kflags & K1F_COUNT_PASSES) ? (uint32_t)(lane == 0) : (uint32_t)__popc(mm);
             if constexpr (TOK) {
               // The wave's straddles listed (lane << 4 | k, in the wave's
               // token staging, free until this N-tile's tokens) and replayed
@@ -1419,7 +1420,7 @@ __global__ __launch_bounds__(64 * k1_waves<MODE>(), k1_wide<MODE>() ? 1 : 2) voi
                 }
                 wave_lds_sync();
                 const int nch = min(T - c0, 64);
-                for (int r = 0; r < nch; r += 8) {
+                for (int r = 0; r < nch && !(kflags & K1F_REPLAY_NO_FP64); r += 8) {
                   const int j = r + (lane >> 3), x = lane & 7;
                   const int e = lst[j < nch ? j : 0];
                   const int ol = e >> 4, k = e & 15;
