@@ -2995,16 +2995,27 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   const int gscan0 = f * P.stride + (comp == 0 ? 0 : gy + (comp == 2 ? gc : 0));
   const int pseg = PACK_SEGS << a.pack_ls[comp != 0];  // the group's segments (32 to 256)
   const int nq = comp == 0 ? gy : gc;
-  if (tid == 0) s_ticket = (int)atomicAdd(&a.pack_ticket[f * 3 + comp], 1u);
+  // Every load of the prologue goes out before the ticket's atomic, so one
+  // memory latency covers them all (in program order each waited for the
+  // one before): the code table, the ZRL code, and the group's segment
+  // counts for the group this workgroup's dispatch place names -- the scan's
+  // groups are dispatched in order, so the ticket usually equals it, and
+  // otherwise the counts are loaded again after it.
   const int chroma = comp != 0;
-  for (int i = tid; i < 512; i += PF_THREADS)
-    tab[i] = lb_tab_entry(a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + i], (uint32_t)i & 255u);
-  uint32_t Lz, zcode;
-  {  // the ZRL code (AC symbol 0xF0: cls 0, so the entry is code / length)
-    const uint32_t zac = a.ehuf[(long long)f * 1024 + (chroma ? 512 : 0) + 256 + 0xF0];
-    Lz = zac >> 16;
-    zcode = zac & 0xFFFFu;
-  }
+  const uint32_t *eh = a.ehuf + (long long)f * 1024 + (chroma ? 512 : 0);
+  static_assert(2 * PF_THREADS == 512, "k_pack_flat: two code-table entries per thread");
+  const uint32_t e0 = eh[tid], e1 = eh[256 + tid], zac = eh[256 + 0xF0];
+  const int qg = bq - (comp == 0 ? 0 : (comp == 1 ? gy : gy + gc));
+  auto seg_count = [&](int qq) -> uint32_t {
+    const int s0q = qq * pseg, nsq = min(ns, s0q + pseg) - s0q;
+    return tid < nsq ? a.seg_ntok[(long long)f * G.nseg + sbase + s0q + tid] : 0u;
+  };
+  const uint32_t nt_guess = seg_count(qg);
+  if (tid == 0) s_ticket = (int)atomicAdd(&a.pack_ticket[f * 3 + comp], 1u);
+  tab[tid] = lb_tab_entry(e0, (uint32_t)tid);
+  tab[256 + tid] = lb_tab_entry(e1, (uint32_t)tid);
+  // the ZRL code (AC symbol 0xF0: cls 0, so the entry is code / length)
+  const uint32_t Lz = zac >> 16, zcode = zac & 0xFFFFu;
   __syncthreads();
   PF_STAMP(5);
   const int q = s_ticket;
@@ -3019,7 +3030,7 @@ __global__ __launch_bounds__(PF_THREADS, pf_occ<PW>()) void k_pack_flat(EntArgs 
   const int s0 = q * pseg, nsg = min(ns, s0 + pseg) - s0;
   const long long fs0 = (long long)f * G.nseg + sbase + s0;  // the group's first segment
   {  // chunks per segment (K1 padded each to a multiple of 4 tokens), a thread per segment
-    const uint32_t nt = tid < nsg ? min(a.seg_ntok[fs0 + tid], (uint32_t)SEG_TOK) : 0u;
+    const uint32_t nt = min(q == qg ? nt_guess : seg_count(q), (uint32_t)SEG_TOK);
     const uint32_t ch = (nt + 3u) >> 2;
     const uint32_t incl = wave_scan64(ch);
     if (lane == 63) s_wt[wave] = incl;
