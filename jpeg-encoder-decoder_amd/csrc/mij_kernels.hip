@@ -3491,29 +3491,42 @@ __device__ __forceinline__ int emit_headers(const EntArgs &a, int f, uint8_t *ou
   {
     const FGeom fg = frame_geom(a.g, a.fdims, f);
     const int W = fg.w, H = fg.h;
-    for (int i = tid; i < hlen; i += 256) {
-      uint8_t v;
+    auto hbyte = [&](int i) -> uint8_t {
       if (i < 20) {
         const uint8_t app0[20] = {0xFF, 0xD8, 0xFF, 0xE0, 0x00, 0x10, 0x4A, 0x46, 0x49, 0x46,
                                   0x00, 0x01, 0x01, 0x00, 0x00, 0x48, 0x00, 0x48, 0x00, 0x00};
-        v = app0[i];
-      } else if (i < doff[0]) {  // DQT (encoder.c:559-571)
+        return app0[i];
+      }
+      if (i < doff[0]) {  // DQT (encoder.c:559-571)
         const int t = (i - 20) / 69, k = (i - 20) - 69 * t;
         const uint8_t m[5] = {0xFF, 0xDB, 0x00, 0x43, (uint8_t)t};
-        v = k < 5 ? m[k] : (uint8_t)a.tab->dqt[t][k - 5];
-      } else if (i < doff[4]) {  // DHT (encoder.c:504-532)
+        return k < 5 ? m[k] : (uint8_t)a.tab->dqt[t][k - 5];
+      }
+      if (i < doff[4]) {  // DHT (encoder.c:504-532)
         const int t = i >= doff[3] ? 3 : i >= doff[2] ? 2 : i >= doff[1] ? 1 : 0;
         const int k = i - doff[t], len = 19 + s_n[t];
         const uint8_t m[5] = {0xFF, 0xC4, (uint8_t)(len >> 8), (uint8_t)len, (uint8_t)((t & 1) << 4 | (t >> 1))};
-        v = k < 5 ? m[k] : k < 21 ? (uint8_t)hc[t].code_len_freq[k - 4] : (uint8_t)hc[t].sym_sorted[k - 21];
-      } else {  // SOF0 (encoder.c:573-600)
-        const uint8_t sof[19] = {0xFF, 0xC0, 0x00, 0x11, 0x08, (uint8_t)(H >> 8), (uint8_t)H,
-                                 (uint8_t)(W >> 8), (uint8_t)W, 0x03, 0x01, 0x22, 0x00,
-                                 0x02, 0x11, 0x01, 0x03, 0x11, 0x01};
-        v = sof[i - doff[4]];
+        return k < 5 ? m[k] : k < 21 ? (uint8_t)hc[t].code_len_freq[k - 4] : (uint8_t)hc[t].sym_sorted[k - 21];
       }
-      out[i] = v;
-    }
+      // SOF0 (encoder.c:573-600)
+      const uint8_t sof[19] = {0xFF, 0xC0, 0x00, 0x11, 0x08, (uint8_t)(H >> 8), (uint8_t)H,
+                               (uint8_t)(W >> 8), (uint8_t)W, 0x03, 0x01, 0x22, 0x00,
+                               0x02, 0x11, 0x01, 0x03, 0x11, 0x01};
+      return sof[i - doff[4]];
+    };
+    // a thread's first HB bytes all computed before any is stored: their
+    // loads then go out together instead of each waiting behind the store
+    // before it (hlen = 261 + the four tables' symbols: <= 768 whenever the
+    // tables hold <= 507 symbols in all -- 2 x 162 AC + 2 x 12 DC at most in
+    // practice; the loop after covers the rest)
+    constexpr int HB = 3;
+    uint8_t hv[HB];
+#pragma unroll
+    for (int hb = 0; hb < HB; hb++) hv[hb] = tid + 256 * hb < hlen ? hbyte(tid + 256 * hb) : (uint8_t)0;
+#pragma unroll
+    for (int hb = 0; hb < HB; hb++)
+      if (tid + 256 * hb < hlen) out[tid + 256 * hb] = hv[hb];
+    for (int i = tid + 256 * HB; i < hlen; i += 256) out[i] = hbyte(i);
   }
   return hlen;
 }
@@ -3522,7 +3535,7 @@ __device__ __forceinline__ int emit_headers(const EntArgs &a, int f, uint8_t *ou
 // SOS of each scan, the output offset of every chunk (exclusive scan of the
 // 0xFF counts), the pad bytes (:425-432), EOI and the frame's length.
 __global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
-  __shared__ int red[4];
+  __shared__ int red[3][4];
   const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (!emit_frame_ok(a, f)) {
     if (tid == 0) a.out_len[f] = 0;
@@ -3530,6 +3543,15 @@ __global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
   }
   uint8_t *out = a.out + (long long)f * a.g.out_cap;
   const long long nchmax = emit_chunks(a.g);
+  // the scans' bit counts, once (the byte stores below may alias them for
+  // the compiler, which would load them again after each)
+  unsigned long long nbits[3];
+  long long nch[3];
+#pragma unroll
+  for (int comp = 0; comp < 3; comp++) {
+    nbits[comp] = a.scan_bits[f * 3 + comp];
+    nch[comp] = (long long)(((nbits[comp] >> 3) + EMIT_CH - 1) / EMIT_CH);
+  }
   // seam mode with the packing's 0xFF counts: the frame's seam words first
   // (their OR-s and count adds land in L2; the counts and the pad words below
   // are read past this CU's L1, which may hold lines of a neighbouring frame)
@@ -3539,9 +3561,38 @@ __global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
     for (int bq = tid; bq < P.gpf; bq += 256) seam_fix_group(a, P, f, bq);
     __threadfence();
   }
+  auto count_at = [&](int comp, long long c) -> int {
+    const uint32_t *cnt = a.ffc + (long long)(f * 3 + comp) * nchmax;
+    return c < nch[comp] ? (int)(seams ? __hip_atomic_load(cnt + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : cnt[c])
+                         : 0;
+  };
+  // the loads the offsets and pads need, all issued before the headers'
+  // (one memory latency for all of them): the first 256 chunk counts of each
+  // scan and the words holding the pad bytes' bits
+  int v0[3];
+  uint32_t padw[3] = {0u, 0u, 0u};
+#pragma unroll
+  for (int comp = 0; comp < 3; comp++) {
+    v0[comp] = count_at(comp, tid);
+    const unsigned long long nbytes = nbits[comp] >> 3;
+    if (tid == 0 && (nbits[comp] & 7)) {
+      const uint32_t *raw = scan_raw(a, f, comp);
+      padw[comp] = seams ? __hip_atomic_load(raw + (nbytes >> 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                         : raw[nbytes >> 2];
+    }
+  }
   __shared__ int s_n[4];
   const int hlen = emit_headers(a, f, out, s_n);
+  // the three scans' first rounds of offsets in one pass (one barrier)
+  int incl0[3];
+#pragma unroll
+  for (int comp = 0; comp < 3; comp++) {
+    incl0[comp] = (int)wave_scan64((uint32_t)v0[comp]);
+    if (lane == 63) red[comp][wave] = incl0[comp];
+  }
+  __syncthreads();
   unsigned long long pos = (unsigned long long)hlen;
+#pragma unroll
   for (int comp = 0; comp < 3; comp++) {
     if (tid == 0) {  // SOS (encoder.c:601-620)
       const uint8_t sos[10] = {0xFF, 0xDA, 0x00, 0x08, 0x01, (uint8_t)(comp + 1),
@@ -3549,36 +3600,39 @@ __global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
       for (int i = 0; i < 10; i++) out[pos + i] = sos[i];
     }
     pos += 10;
-    const unsigned long long nbits = a.scan_bits[f * 3 + comp], nbytes = nbits >> 3;
-    const long long nch = (long long)((nbytes + EMIT_CH - 1) / EMIT_CH);
-    const uint32_t *cnt = a.ffc + (long long)(f * 3 + comp) * nchmax;
+    const unsigned long long nbytes = nbits[comp] >> 3;
     uint32_t *off = a.choff + (long long)(f * 3 + comp) * nchmax;
     unsigned long long carry = 0;  // 0xFF bytes of the earlier chunks
-    for (long long c0 = 0; c0 < nch; c0 += 256) {
+    {
+      int wb = 0, tot = 0;
+      for (int q = 0; q < 4; q++) {
+        if (q < wave) wb += red[comp][q];
+        tot += red[comp][q];
+      }
+      if (tid < nch[comp]) off[tid] = (uint32_t)(pos + (unsigned long long)tid * EMIT_CH + wb + incl0[comp] - v0[comp]);
+      carry = tot;
+    }
+    for (long long c0 = 256; c0 < nch[comp]; c0 += 256) {  // (scans of more than 256 chunks: 2 MB)
       const long long c = c0 + tid;
-      const int v = c < nch ? (int)(seams ? __hip_atomic_load(cnt + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                          : cnt[c]) : 0;
+      const int v = count_at(comp, c);
       const int incl = (int)wave_scan64((uint32_t)v);
-      if (lane == 63) red[wave] = incl;
+      __syncthreads();  // (red: the pass before has read it)
+      if (lane == 63) red[comp][wave] = incl;
       __syncthreads();
       int wb = 0, tot = 0;
       for (int q = 0; q < 4; q++) {
-        if (q < wave) wb += red[q];
-        tot += red[q];
+        if (q < wave) wb += red[comp][q];
+        tot += red[comp][q];
       }
-      __syncthreads();
-      if (c < nch) off[c] = (uint32_t)(pos + (unsigned long long)c * EMIT_CH + carry + wb + incl - v);
+      if (c < nch[comp]) off[c] = (uint32_t)(pos + (unsigned long long)c * EMIT_CH + carry + wb + incl - v);
       carry += tot;
     }
     pos += nbytes + carry;
     if (tid == 0) {  // the pad byte of fill_last_byte, never stuffed
-      const uint32_t *raw = scan_raw(a, f, comp);
-      const int r = (int)(nbits & 7);
+      const int r = (int)(nbits[comp] & 7);
       uint8_t pad = 0xFF;
       if (r) {
-        const uint32_t w = seams ? __hip_atomic_load(raw + (nbytes >> 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                 : raw[nbytes >> 2];
-        const uint8_t part = (uint8_t)(w >> (24 - 8 * (nbytes & 3)));
+        const uint8_t part = (uint8_t)(padw[comp] >> (24 - 8 * (nbytes & 3)));
         pad = (uint8_t)(part | ((1u << (8 - r)) - 1u));
       }
       out[pos] = pad;
@@ -3594,13 +3648,15 @@ __global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
 
 // The stuffed bytes (encoder.c:403-408: 0x00 after every 0xFF) of chunk
 // [cb, cb + EMIT_CH) of a byte stream nbytes long whose big-endian word w is
-// word(w), written at out + o0; tot = the chunk's 0xFF bytes.  after_load(w)
-// runs once per loaded word, after the load (k_emit_write zeroes the scan
-// word there).  Called by a whole 256-thread workgroup; s_out: 2 * EMIT_CH
-// bytes, red: 4 ints of LDS.
-template <class WordFn, class AfterFn>
-__device__ __forceinline__ void stuff_chunk(const WordFn &word, const AfterFn &after_load, unsigned long long nbytes,
-                                            unsigned long long cb, unsigned long long o0, int tot, uint8_t *out,
+// word(w), written at out + o0; tot = the chunk's 0xFF bytes, both from
+// meta(o0, tot), called after the words' loads are issued (its own loads then
+// share their wait instead of preceding them).  after_load(w) runs once per
+// loaded word, after the load (k_emit_write zeroes the scan word there).
+// Called by a whole 256-thread workgroup; s_out: 2 * EMIT_CH bytes, red: 4
+// ints of LDS.
+template <class WordFn, class AfterFn, class MetaFn>
+__device__ __forceinline__ void stuff_chunk(const WordFn &word, const AfterFn &after_load, const MetaFn &meta,
+                                            unsigned long long nbytes, unsigned long long cb, uint8_t *out,
                                             uint8_t *s_out, int *red) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int WPW = EMIT_CH / 16;  // stream words per wave
@@ -3619,6 +3675,9 @@ __device__ __forceinline__ void stuff_chunk(const WordFn &word, const AfterFn &a
     lims[k] = mb < nbytes ? (int)min(nbytes - mb, 4ull) : 0;
     wds[k] = lims[k] ? word(mb >> 2) : 0u;
   }
+  unsigned long long o0;
+  int tot;
+  meta(o0, tot);
 #pragma unroll
   for (int k = 0; k < WPW / 64; k++) {  // (kept: the layout pass below needs them again)
     cfs[k] = lims[k] ? ff_bytes(wds[k], lims[k]) : 0;
@@ -3695,9 +3754,11 @@ __global__ __launch_bounds__(256) void k_emit_write(EntArgs a) {
   uint8_t *out = a.out + (long long)f * a.g.out_cap;
   const long long nchmax = emit_chunks(a.g);
   long long nch[3];
+  unsigned long long nbs[3];  // (kept: the stores below may alias scan_bits for the compiler)
 #pragma unroll
   for (int comp = 0; comp < 3; comp++) {
     const unsigned long long nbits = a.scan_bits[f * 3 + comp], nbytes = nbits >> 3;
+    nbs[comp] = nbytes;
     nch[comp] = (long long)((nbytes + EMIT_CH - 1) / EMIT_CH);
     if (zero && slot == 0 && tid < 2) {  // words past the last whole byte (the pad byte's bits)
       const unsigned long long w = ((nbytes + 3) >> 2) + tid;
@@ -3708,16 +3769,18 @@ __global__ __launch_bounds__(256) void k_emit_write(EntArgs a) {
   for (long long i = slot; i < nch[0] + nch[1] + nch[2]; i += a.emit_slots) {
     const int comp = i < nch[0] ? 0 : (i < nch[0] + nch[1] ? 1 : 2);
     const long long c = i - (comp == 0 ? 0 : (comp == 1 ? nch[0] : nch[0] + nch[1]));
-    const unsigned long long nbytes = a.scan_bits[f * 3 + comp] >> 3;
+    const unsigned long long nbytes = comp == 0 ? nbs[0] : (comp == 1 ? nbs[1] : nbs[2]);
     uint32_t *raw = (uint32_t *)scan_raw(a, f, comp);
     const long long ci = (long long)(f * 3 + comp) * nchmax + c;
-    const int tot = (int)a.ffc[ci];
-    const unsigned long long o0 = a.choff[ci];
     stuff_chunk([&](unsigned long long w) { return raw[w]; },
                 [&](unsigned long long w) {
                   if (zero) raw[w] = 0u;
                 },
-                nbytes, (unsigned long long)c * EMIT_CH, o0, tot, out, s_out, red);
+                [&](unsigned long long &o0, int &tot) {
+                  tot = (int)a.ffc[ci];
+                  o0 = a.choff[ci];
+                },
+                nbytes, (unsigned long long)c * EMIT_CH, out, s_out, red);
     if (tid == 0) a.ffc[ci] = 0;  // read: left zeroed (ff_pack adds)
   }
 }
@@ -3871,8 +3934,12 @@ __global__ __launch_bounds__(256) void k_band_write(EntArgs a, uint8_t *dst, uns
     const unsigned long long o0 = a.scan_base[f * 3 + comp] + a.choff[ci];
     const unsigned long long clen = min((unsigned long long)EMIT_CH, nbytes - (unsigned long long)c * EMIT_CH) + tot;
     if (o0 + clen <= cap)  // (workgroup-uniform)
-      stuff_chunk([&](unsigned long long w) { return shifted_word(raw, w, h); }, [](unsigned long long) {}, nbytes,
-                  (unsigned long long)c * EMIT_CH, o0, tot, dst, s_out, red);
+      stuff_chunk([&](unsigned long long w) { return shifted_word(raw, w, h); }, [](unsigned long long) {},
+                  [&](unsigned long long &o, int &t) {
+                    o = o0;
+                    t = tot;
+                  },
+                  nbytes, (unsigned long long)c * EMIT_CH, dst, s_out, red);
     if (threadIdx.x == 0) a.ffc[ci] = 0;  // left zeroed for the next count
   }
 }
