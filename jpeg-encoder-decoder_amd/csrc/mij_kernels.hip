@@ -4335,6 +4335,11 @@ int k1_grid(int device, long long ntiles, int mode) {
 #endif
   long long want = (ntiles + nw - 1) / nw;
   long long cap = (long long)cus * per_cu * (mult > 0 ? mult : 1);
+  // too few tiles to give every wave of a full grid one (a single 1920x1280
+  // frame: 1,200 tiles): spread them over every CU's workgroup slot instead
+  // of filling a few CUs' waves -- a tile's time is then its own wave's
+  // issue, not three waves' sharing one SIMD
+  if (want < cap) want = ntiles < cap ? ntiles : cap;
   return (int)(want < cap ? want : cap);
 }
 
