@@ -330,6 +330,7 @@ struct mij_batch {
   uint32_t *d_seam = nullptr;     // k_pack_flat -> k_seam_fix: shared first word per pack group
   unsigned long long *d_pack_state = nullptr;  // k_pack_flat look-back words, per pack group
   unsigned *d_pack_ticket = nullptr;
+  uint32_t *d_dcx = nullptr;      // k_segdc_actab (dc_last): per frame 64 words, left zeroed
   uint16_t *d_fixmask = nullptr;  // K1 fix masks: per N-tile (tile * 3 + nt), zero between launches
   uint16_t *d_audit = nullptr;    // mij_batch_audit: per frame, block, lane group 16 straddle bits
   size_t audit_cap = 0;
@@ -396,7 +397,7 @@ static void batch_free(mij_batch *b) {
                   b->d_scan_bits, b->d_out_len, b->d_hc, b->d_out, b->d_err, b->d_replays,
                   b->d_dcpred, b->d_bitbase, b->d_stage, b->d_fixmask, b->d_audit, b->d_ffc, b->d_choff, b->d_scan_base,
                   b->d_seam, b->d_pack_state, b->d_pack_ticket, b->d_fdims, b->d_frame, b->d_regions, b->d_pieces,
-                  b->d_bound_acc};
+                  b->d_bound_acc, b->d_dcx};
   for (void *p : ptrs)
     if (p) hipFree(p);
   for (auto &row : b->evh)
@@ -459,6 +460,8 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
     HIP_TRY(hipMemsetAsync(b->d_fixmask, 0, sizeof(uint16_t) * F * g.tiles_per_frame * 3, b->stream));
     HIP_TRY(dalloc(&b->d_pack_state, F * pack_stride(g)));
     HIP_TRY(dalloc(&b->d_pack_ticket, F * 3));  // one per scan
+    HIP_TRY(dalloc(&b->d_dcx, F * 64));
+    HIP_TRY(hipMemsetAsync(b->d_dcx, 0, sizeof(uint32_t) * F * 64, b->stream));
     HIP_TRY(dalloc(&b->d_seam, F * pack_stride(g)));
     HIP_TRY(dalloc(&b->d_regions, F));
   }
@@ -648,6 +651,7 @@ static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0, bool band = false
   a.scan_base = b->d_scan_base;
   a.pack_state = b->d_pack_state;
   a.pack_ticket = b->d_pack_ticket;
+  a.dcx = b->d_dcx;
   a.fdims = b->use_fdims ? b->d_fdims : nullptr;
   // JFIF-assembly workgroups per frame (its chunks dealt round-robin over
   // the three scans; A/B per scan in round 2, profiles/r02/emit_slots_ab.txt):
@@ -689,6 +693,7 @@ static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0, bool band = false
     a.scan_base += F * 3;
     a.pack_state += F * gpf;
     a.pack_ticket += F * 3;
+    if (a.dcx) a.dcx += F * 64;
     if (a.fdims) a.fdims += F;
   }
   return a;
@@ -815,9 +820,20 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   // segment DCs + tables 0.077 -> 0.062 ms at config 3 Q=50, 0.102 -> 0.075
   // at Q=90).  Not on small batches: one frame's four tables take as long
   // as its AC tables, and the DC tables after them add 10 us.
-  const bool actab = dc_fix && !a.seg_dc && !tables_given && !ttime && b->opt[MIJ_OPT_ACTAB] && nframes >= 16;
+  // dc_last: the DC tables in the same launch, built by each frame's last
+  // segment-DC workgroup while the AC tables' waves still merge (no
+  // k_tables_1w launch) -- on batches of up to 64 frames (profiles/r06/dc_last:
+  // one 1920x1280 frame 0.062 -> 0.059 ms, 16 frames 0.173 -> 0.162, 64
+  // frames 0.354 -> 0.348; at 256 frames of 3840x2160 the tables after the
+  // launch are faster: 3.63 against 3.70 ms)
+  static const int dc_last_max = diag_env("MIJ_DC_LAST_MAX", 64);
+  const bool dc_last = dc_fix && !a.seg_dc && !tables_given && !ttime && b->opt[MIJ_OPT_ACTAB] &&
+                       nframes <= dc_last_max && b->d_dcx;
+  const bool actab =
+      dc_last || (dc_fix && !a.seg_dc && !tables_given && !ttime && b->opt[MIJ_OPT_ACTAB] && nframes >= 16);
   if (actab) {
     a.zero_pack = 1;  // (the AC workgroups zero the counts they read)
+    a.dc_last = dc_last;
     HIP_TRY(launch_segdc_actab(a, st));
   } else if (dc_fix && !a.seg_dc) {
     HIP_TRY(launch_seg_dc(a, st));
@@ -888,7 +904,7 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
       fprintf(stderr, "k_tables frame span %.0f clocks; DC waves: segment DCs %.0f, wait %.0f; wave entry spread %.0f\n",
               span / nframes, sw / (2.0 * nframes), ww / (2.0 * nframes), ent / nframes);
     }
-  } else if (!tables_given) {
+  } else if (!tables_given && !dc_last) {
     a.zero_pack = !a.seg_dc;  // one wave per table: it zeroes the pack state too
     a.tab_dc_only = actab;
     HIP_TRY(launch_tables(a, st));

@@ -239,6 +239,10 @@ struct EntArgs {
   int zero_pack;                   // k_tables_1w also zeroes k_pack_flat's look-back words and tickets
   int seg_dc;                      // k_tables: compute the segment-first DC tokens first (k_seg_dc)
   int tab_dc_only;                 // k_tables_1w: the DC tables only (k_segdc_actab built the AC ones)
+  int dc_last;                     // k_segdc_actab: a frame's last segment-DC workgroup builds its two
+                                   // DC tables (and zeroes the pack state): no k_tables_1w launch
+  uint32_t *dcx;                   // dc_last: per frame 64 words -- the segment-first DCs' class
+                                   // counts [luma, chroma][16] and the arrivals [32]; left zeroed
   int ff_pack;                     // seam mode: k_pack_flat / k_seam_fix count the 0xFF bytes of every
                                    // EMIT_CH chunk into ffc as they store (k_emit_count not run;
                                    // k_emit_write leaves the counts zeroed)

@@ -1723,8 +1723,17 @@ __device__ __forceinline__ void seg_dc_block(const EntArgs &a, int b, uint32_t *
   if (threadIdx.x < 32) {
     uint32_t v = 0;
     for (int c = 0; c < 32; c++) v += hs[threadIdx.x * 32 + ((c + threadIdx.x) & 31)];
-    if (v)
-      atomicAdd(&a.hist[((long long)f * 4 + (threadIdx.x >= 16 ? 2 : 0)) * 257 + (threadIdx.x & 15)], v);
+    if (v) {
+      if (a.dc_last) {
+        // (returning: the wave waits until the add is performed -- device-wide
+        // atomics meet at one coherence point -- before the block's arrival
+        // is counted; no cache-writeback fence)
+        const uint32_t old = atomicAdd(&a.dcx[(long long)f * 64 + threadIdx.x], v);
+        asm volatile("" ::"v"(old));
+      } else {
+        atomicAdd(&a.hist[((long long)f * 4 + (threadIdx.x >= 16 ? 2 : 0)) * 257 + (threadIdx.x & 15)], v);
+      }
+    }
   }
 }
 
@@ -2684,18 +2693,60 @@ __global__ __launch_bounds__(64) void k_tables_1w(EntArgs a) {
 // luma AC table's merge (the long pole of the table stage) runs beside the
 // segment DCs, and k_tables_1w builds only the DC tables after
 // (EntArgs::tab_dc_only).  One wave of an AC workgroup works.
+// DC_LAST (EntArgs::dc_last, small batches): the segment-DC workgroups
+// count their classes into dcx and the last of a frame's to arrive builds
+// the frame's two DC tables, two waves at once, while the AC tables' waves
+// are still merging; its other two waves zero the frame's pack state -- so
+// the table stage is one launch whose length is the luma AC table's.  (Not
+// on large batches: a frame's DC tables then wait for its own segment DCs,
+// dispatched frame after frame, where k_tables_1w builds all of them at once
+// after the launch; config 3: 0.052 -> 0.10 ms.)
+template <bool DC_LAST>
 __global__ __launch_bounds__(SEGDC_WG) void k_segdc_actab(EntArgs a) {
-  __shared__ TabScratch2 S;
+  __shared__ TabScratch2 S[DC_LAST ? 2 : 1];
   __shared__ uint32_t hs[32 * 32];
+  __shared__ uint32_t s_x[32];
+  __shared__ int s_last;
   const int nac = 2 * a.nframes;
   if ((int)blockIdx.x >= nac) {
-    seg_dc_block(a, (int)blockIdx.x - nac, hs);
+    const int b = (int)blockIdx.x - nac;
+    seg_dc_block(a, b, hs);
+    if (!DC_LAST) return;
+    const int per = (a.g.nseg + SEGDC_WG - 1) / SEGDC_WG, f = b / per;
+    uint32_t *dcx = a.dcx + (long long)f * 64;
+    // Arrival after the block's counts are performed (seg_dc_block waited for
+    // its returning adds); the last arrival's own atomics then find every
+    // count (a device-scope fence here -- an L2 writeback per block -- cost
+    // 1.6 ms per config-3 launch)
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(&dcx[32], 1u) == (unsigned)(per - 1);
+    __syncthreads();
+    if (!s_last) return;
+    // the counts read and reset by one atomic each (left zeroed for the next launch)
+    if (threadIdx.x < 33) {
+      const uint32_t v = atomicExch(&dcx[threadIdx.x], 0u);
+      if (threadIdx.x < 32) s_x[threadIdx.x] = v;
+    }
+    __syncthreads();
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (w < 2) {
+      const int t = 2 * w;  // luma DC, chroma DC
+      build_table_wave2(a.hist + ((long long)f * 4 + t) * 257, &s_x[16 * w], (HuffCode *)a.hc + (long long)f * 4 + t,
+                        (uint32_t *)a.ehuf + ((long long)f * 4 + t) * 256, &S[DC_LAST ? w : 0], lane, a.err + f,
+                        nullptr);
+      if (a.zero_pack)  // the counts are read: left zeroed for the next K1
+        for (int i = lane; i < 257; i += 64) a.hist[((long long)f * 4 + t) * 257 + i] = 0;
+    } else if (a.zero_pack) {  // k_pack_flat runs next: its look-back words and tickets zeroed
+      const long long st = pack_stride(a.g);
+      for (long long i = threadIdx.x - 128; i < st; i += 128) a.pack_state[f * st + i] = 0;
+      if (threadIdx.x - 128 < 3) a.pack_ticket[f * 3 + threadIdx.x - 128] = 0;
+    }
     return;
   }
   if (threadIdx.x >= 64) return;
   const int f = blockIdx.x >> 1, t = 1 + 2 * (blockIdx.x & 1), lane = threadIdx.x;
   build_table_wave2(a.hist + ((long long)f * 4 + t) * 257, nullptr, (HuffCode *)a.hc + (long long)f * 4 + t,
-                    (uint32_t *)a.ehuf + ((long long)f * 4 + t) * 256, &S, lane, a.err + f, nullptr);
+                    (uint32_t *)a.ehuf + ((long long)f * 4 + t) * 256, &S[0], lane, a.err + f, nullptr);
   if (a.zero_pack)  // the counts are read: left zeroed for the next K1
     for (int i = lane; i < 257; i += 64) a.hist[((long long)f * 4 + t) * 257 + i] = 0;
 }
@@ -3384,7 +3435,10 @@ __device__ __forceinline__ void seam_fix_group(const EntArgs &a, const PackGrid 
   if (a.ff_pack) {  // the 0xFF bytes the OR adds (an OR never removes one, so the adds telescope)
     const uint32_t W = (uint32_t)(start >> 5), nb = (uint32_t)(a.scan_bits[f * 3 + comp] >> 3);
     const int d = ff_word(old | sv, W, nb) - ff_word(old, W, nb);
-    if (d) atomicAdd(&a.ffc[(long long)(f * 3 + comp) * emit_chunks(G) + W / EMIT_CW], (uint32_t)d);
+    if (d) {  // (returning, as the OR: the caller's threads read both after a barrier)
+      const uint32_t o2 = atomicAdd(&a.ffc[(long long)(f * 3 + comp) * emit_chunks(G) + W / EMIT_CW], (uint32_t)d);
+      asm volatile("" ::"v"(o2));
+    }
   }
 }
 
@@ -3555,6 +3609,10 @@ __global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
   // seam mode with the packing's 0xFF counts: the frame's seam words first
   // (their OR-s and count adds land in L2; the counts and the pad words below
   // are read past this CU's L1, which may hold lines of a neighbouring frame)
+  // (one device fence per frame here: at most 15 frames take this path; the
+  // counts and pad words are then read past this CU's L1.  Reading them back
+  // by atomics instead, without the fence, measured 0.9 us slower on four
+  // frames, equal on one)
   const bool seams = a.seam && a.ff_pack && a.seam_in_scan;
   if (seams) {
     const PackGrid P = pack_grid(a);
@@ -4233,12 +4291,14 @@ __global__ __launch_bounds__(256) void k_band_bound(const uint32_t *hist, const 
   if (lane == 0) s_w[w] = words;
   __syncthreads();
   if (threadIdx.x == 0) {
-    atomicAdd(&acc[0], s_w[0] + s_w[1] + s_w[2] + s_w[3]);
-    __threadfence();
+    // (the sum's add returns before the arrival is counted, and the last
+    // arrival reads it by an atomic: both at the point where device-wide
+    // atomics meet, so no cache-writeback fence is needed)
+    const unsigned long long old = atomicAdd(&acc[0], s_w[0] + s_w[1] + s_w[2] + s_w[3]);
+    asm volatile("" ::"v"(old));
     if (atomicAdd(&acc[1], 1ull) == gridDim.x - 1) {
-      __threadfence();
       bound[0] = atomicExch(&acc[0], 0ull);
-      acc[1] = 0;
+      atomicExch(&acc[1], 0ull);
     }
   }
 }
@@ -4405,8 +4465,9 @@ hipError_t launch_dc_diff(int16_t *coef, const int16_t *dc, const Geom &g, int n
   return hipGetLastError();
 }
 hipError_t launch_segdc_actab(const EntArgs &a, hipStream_t s) {
-  hipLaunchKernelGGL(k_segdc_actab, dim3(a.nframes * (2 + (a.g.nseg + SEGDC_WG - 1) / SEGDC_WG)),
-                     dim3(SEGDC_WG), 0, s, a);
+  const dim3 grid(a.nframes * (2 + (a.g.nseg + SEGDC_WG - 1) / SEGDC_WG));
+  if (a.dc_last) hipLaunchKernelGGL(k_segdc_actab<true>, grid, dim3(SEGDC_WG), 0, s, a);
+  else hipLaunchKernelGGL(k_segdc_actab<false>, grid, dim3(SEGDC_WG), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_tables(const EntArgs &a, hipStream_t s) {

@@ -1,7 +1,9 @@
 #!/bin/bash
 # scripts/small_batch_ab.sh -- small batches of 1920x1280 frames (config 2's
-# shape): with LIBS, the library builds alternating (MIJ_LIB); otherwise the
-# in-tree library with and without option $OPT (default segdc_fused=1).
+# shape): with ENVS, the in-tree library under each environment setting in
+# turn (e.g. ENVS="MIJ_X=0 MIJ_X=1"); with LIBS, the library builds
+# alternating (MIJ_LIB); otherwise the in-tree library with and without
+# option $OPT (default segdc_fused=1).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 OPT=${OPT:-segdc_fused=1}
@@ -11,7 +13,9 @@ run() {  # <label> <env-or-empty> <extra args>
 }
 for n in ${NS:-1 4 16}; do
   for r in $(seq ${ROUNDS:-2}); do
-    if [ -n "${LIBS:-}" ]; then
+    if [ -n "${ENVS:-}" ]; then
+      for e in $ENVS; do run "$e" "$e" "" || exit 1; done
+    elif [ -n "${LIBS:-}" ]; then
       for lib in $LIBS; do run "$lib" "MIJ_LIB=$PWD/$lib" "" || exit 1; done
     else
       run "default" "" "" || exit 1
