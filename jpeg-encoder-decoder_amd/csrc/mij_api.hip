@@ -832,7 +832,8 @@ static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given
   const bool actab =
       dc_last || (dc_fix && !a.seg_dc && !tables_given && !ttime && b->opt[MIJ_OPT_ACTAB] && nframes >= 16);
   if (actab) {
-    a.zero_pack = 1;  // (the AC workgroups zero the counts they read)
+    static const int dc_last_nozero = diag_env("MIJ_DC_LAST_NOZERO", 0);  // (diag: the packing zeroes its state)
+    a.zero_pack = dc_last && dc_last_nozero ? 0 : 1;  // (the AC workgroups zero the counts they read)
     a.dc_last = dc_last;
     HIP_TRY(launch_segdc_actab(a, st));
   } else if (dc_fix && !a.seg_dc) {

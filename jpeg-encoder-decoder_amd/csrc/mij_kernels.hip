@@ -3435,10 +3435,7 @@ __device__ __forceinline__ void seam_fix_group(const EntArgs &a, const PackGrid 
   if (a.ff_pack) {  // the 0xFF bytes the OR adds (an OR never removes one, so the adds telescope)
     const uint32_t W = (uint32_t)(start >> 5), nb = (uint32_t)(a.scan_bits[f * 3 + comp] >> 3);
     const int d = ff_word(old | sv, W, nb) - ff_word(old, W, nb);
-    if (d) {  // (returning, as the OR: the caller's threads read both after a barrier)
-      const uint32_t o2 = atomicAdd(&a.ffc[(long long)(f * 3 + comp) * emit_chunks(G) + W / EMIT_CW], (uint32_t)d);
-      asm volatile("" ::"v"(o2));
-    }
+    if (d) atomicAdd(&a.ffc[(long long)(f * 3 + comp) * emit_chunks(G) + W / EMIT_CW], (uint32_t)d);
   }
 }
 
@@ -3618,6 +3615,9 @@ __global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
     const PackGrid P = pack_grid(a);
     for (int bq = tid; bq < P.gpf; bq += 256) seam_fix_group(a, P, f, bq);
     __threadfence();
+    // every thread's fixes in before any thread reads a count or pad word
+    // (the loads below come before the headers' barrier)
+    __syncthreads();
   }
   auto count_at = [&](int comp, long long c) -> int {
     const uint32_t *cnt = a.ffc + (long long)(f * 3 + comp) * nchmax;

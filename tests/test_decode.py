@@ -99,6 +99,36 @@ def test_decode_quality_sweep_and_long_codes(quality):
 
 
 @pytest.mark.gpu
+def test_repeated_encodes_same_bytes_small_batch():
+    """The same two-frame batch (config-3 frame + uniform noise, the
+    small-batch paths: seam fixes inside k_emit_scan, DC tables inside the
+    segment-DC launch) encoded 12 times: identical JFIF bytes every time, and
+    each decodes to the encoder's own coefficients.  (Round 6: a missing
+    barrier between the seam fixes and the chunk-count reads made the noise
+    frame's bytes differ in about a third of the repetitions.)"""
+    frames = np.stack([recipes.config3_frame(0), recipes.config3_uniform(1)])
+    b = mijpeg.Batch(3840, 2160, 2, 50, keep_coefs=True)
+    d = mijpeg.Decoder(3840, 2160, 2)
+    try:
+        b.upload(frames)
+        first = None
+        for _ in range(12):
+            b.encode(2)
+            streams = [b.output(i) for i in range(2)]
+            shas = [hashlib.sha256(x).hexdigest() for x in streams]
+            if first is None:
+                first = shas
+                d.decode(streams)
+                for i in range(2):
+                    for g, w in zip(d.coefs(i), b.coefs(i, diffed=True)):
+                        assert (g == w).all()
+            assert shas == first
+    finally:
+        b.close()
+        d.close()
+
+
+@pytest.mark.gpu
 def test_round_trip_config3_full_size():
     """decode(GPU encode) == the GPU encoder's own coefficients, 3840x2160."""
     frames = np.stack([recipes.config3_frame(0), recipes.config3_uniform(1)])
