@@ -367,6 +367,13 @@ int mij_band_words_async(mij_batch *b, int n, uint32_t *d_dst, size_t cap_words)
 int mij_assemble_tables_async(mij_batch *b, int n, const uint32_t *d_ghist);
 int mij_assemble_async(mij_batch *b, int n, const uint64_t *d_allbits, int world, const uint32_t *d_src,
                        size_t stride_words);
+/* A device-to-host copy of `bytes` on the batch's stream (the word bounds
+ * and stuffed totals of the device protocol, read by the host to size the
+ * word exchange): ordered after the collectives and launches enqueued on
+ * that stream before it, so the caller waits for just those (an event on the
+ * batch's stream) and not for a copy queued behind the packing on another
+ * stream.  h_dst must be pinned host memory. */
+int mij_copy_to_host_async(mij_batch *b, void *h_dst, const void *d_src, size_t bytes);
 /* Distributed JFIF emission (the config-4 bands, sharding.encode_banded_dev
  * with emit="bands"): after mij_band_pack_async and the all-gather of every
  * band's d_bits into d_allbits [world][3n + 1], band `rank` stuffs the bytes

@@ -1820,6 +1820,13 @@ extern "C" int mij_assemble_tables_async(mij_batch *b, int n, const uint32_t *d_
   return MIJ_OK;
 }
 
+extern "C" int mij_copy_to_host_async(mij_batch *b, void *h_dst, const void *d_src, size_t bytes) {
+  if (!b || !h_dst || !d_src) return fail(MIJ_EINVAL, "copy_to_host_async: null argument");
+  HIP_TRY(hipSetDevice(b->dev));
+  HIP_TRY(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, b->stream));
+  return MIJ_OK;
+}
+
 extern "C" int mij_assemble_async(mij_batch *b, int n, const uint64_t *d_allbits, int world, const uint32_t *d_src,
                                   size_t stride_words) {
   if (band_check(b, n, "assemble_async", true)) return g_err;

@@ -30,7 +30,7 @@ EXPORTS = [
     "mij_band_words_all", "mij_assemble_pieces", "mij_assembler_create",
     "mij_band_analyze_async", "mij_band_histograms_async", "mij_band_tables_async", "mij_band_pack_async",
     "mij_band_words_async", "mij_assemble_tables_async", "mij_assemble_async",
-    "mij_band_stuff_async", "mij_assemble_stuffed_async",
+    "mij_band_stuff_async", "mij_assemble_stuffed_async", "mij_copy_to_host_async",
     "mij_probe_mfma", "mij_colour_lut", "mij_build_target",
     # change detector (reference include/brain.h:7-10 drop-in + extensions)
     "subsample", "store", "compare", "enlargeAdjust", "mij_set_frame_height",
@@ -126,6 +126,7 @@ def load() -> C.CDLL:
     lib.mij_assemble_async.argtypes = [p, i, p, i, p, sz]
     lib.mij_band_stuff_async.argtypes = [p, i, p, i, i, p, p, p, sz]
     lib.mij_assemble_stuffed_async.argtypes = [p, i, p, i, p, sz]
+    lib.mij_copy_to_host_async.argtypes = [p, p, p, sz]
     lib.mij_batch_build_tables.argtypes = [p, i, p]
     lib.mij_batch_sync.argtypes = [p]
     lib.mij_batch_output.argtypes = [p, i, p, sz, C.POINTER(sz)]
@@ -577,6 +578,10 @@ class Batch:
         stuffed, into d_dst; records [n, 3, 4] u64 and the total to d_rec / d_total"""
         _check(self.lib.mij_band_stuff_async(self.h_, n, d_allbits, world, rank, d_rec, d_total, d_dst, cap),
                "band_stuff_async")
+
+    def copy_to_host_async(self, h_dst: int, d_src: int, nbytes: int) -> None:
+        """device -> pinned host bytes on the batch's stream"""
+        _check(self.lib.mij_copy_to_host_async(self.h_, h_dst, d_src, nbytes), "copy_to_host_async")
 
     def assemble_stuffed_async(self, n: int, d_allrec: int, world: int, d_src: int, stride: int) -> None:
         _check(self.lib.mij_assemble_stuffed_async(self.h_, n, d_allrec, world, d_src, stride),

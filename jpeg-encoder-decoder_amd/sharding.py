@@ -12,6 +12,8 @@ default) needs no partition at all.
 """
 from __future__ import annotations
 
+import os
+
 
 def frame_range(n_frames: int, world: int, rank: int) -> range:
     """Contiguous, balanced block of frame indices owned by `rank`.
@@ -313,6 +315,36 @@ class StagedExchange(DeviceExchange):
         return None
 
 
+# MIJ_HOST_READ=default: the host reads' copies on torch's default stream
+# (rounds 4-6, kept for A/B) instead of the band batch's stream
+_HOST_READ_DEFAULT = os.environ.get("MIJ_HOST_READ", "batch") == "default"
+
+
+def _to_host(band, s, h, d_src, dev):
+    """d_src (int64, on the band stream) -> the pinned host tensor h; returns
+    the event to wait on.  The copy is the library's, on the band stream right
+    after the collective that produced d_src, so it runs before the packing
+    launched next (a copy on another stream waits for a free slot behind the
+    packing's workgroups: 40 us on config 4), and torch's pinned allocator
+    records no event of the library's stream."""
+    import torch
+    if _HOST_READ_DEFAULT:
+        # (on torch's own stream: the host allocator keeps an event of the
+        # copy's stream, and the library's stream may be gone before that
+        # event is released)
+        d = torch.cuda.default_stream(dev)
+        d.wait_stream(s)
+        with torch.cuda.stream(d):
+            h.copy_(d_src, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(d)
+        return ev
+    band.copy_to_host_async(h.data_ptr(), d_src.data_ptr(), 8 * d_src.numel())
+    ev = torch.cuda.Event()
+    ev.record(s)
+    return ev
+
+
 def encode_banded_dev(band, n: int, xch, frame_batch=None, events=None, emit: str = "root"):
     """encode_banded with the device-resident protocol: the last DCs (int16
     [n, 4], gathered as int32 pairs), the histograms (summed in place), the
@@ -373,16 +405,8 @@ def encode_banded_dev(band, n: int, xch, frame_batch=None, events=None, emit: st
         bound = torch.empty(1, dtype=torch.int64, device=dev)
         band.band_tables_async(n, hist.data_ptr(), bound.data_ptr())
         bounds = xch.all_gather(bound)                            # [world, 1]
-        # (the copy into pinned memory runs on torch's own stream: the host
-        # allocator keeps an event of the copy's stream, and the library's
-        # stream may be gone before that event is released)
         h_bounds = xch.host_buffer(world)
-        d = torch.cuda.default_stream(dev)
-        d.wait_stream(s)
-        with torch.cuda.stream(d):
-            h_bounds.copy_(bounds.view(-1), non_blocking=True)
-            ready = torch.cuda.Event()
-            ready.record(d)
+        ready = _to_host(band, s, h_bounds, bounds.view(-1), dev)
         bits = torch.empty(3 * n + 1, dtype=torch.int64, device=dev)
         band.band_pack_async(n, bits.data_ptr())
         allbits = xch.all_gather(bits).contiguous()               # [world, 3n + 1]
@@ -398,13 +422,8 @@ def encode_banded_dev(band, n: int, xch, frame_batch=None, events=None, emit: st
                                   sbuf.data_ptr(), cap)
             allrec = xch.all_gather(rec).contiguous()             # [world, n*3*4]
             tots = xch.all_gather(tot)                           # [world, 1]
-            h_tot = xch.host_buffer(world)
-            d.wait_stream(s)
-            with torch.cuda.stream(d):
-                h_tot.copy_(tots.view(-1), non_blocking=True)
-                ready2 = torch.cuda.Event()
-                ready2.record(d)
-            ready2.synchronize()
+            h_tot = xch.host_buffer(2 * world)[world:]
+            _to_host(band, s, h_tot, tots.view(-1), dev).synchronize()
             if int(h_tot.max()) > cap:  # (every rank sees the same totals: all raise)
                 raise RuntimeError(f"band stuffing: {int(h_tot.max())} stuffed bytes exceed the "
                                    f"{cap}-byte buffer the word bound gave")
