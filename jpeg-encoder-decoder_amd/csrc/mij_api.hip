@@ -349,6 +349,7 @@ struct mij_batch {
   int band_async_n = 0;                        // frames of the last mij_band_pack_async
   int asm_tables_n = 0;                        // frames of the last mij_assemble_tables_async
   int hist_zero_n = 0;  // frames 0..n-1 of d_hist left zeroed by the last encode's k_tables_1w
+  int band_hist_zero = 0;  // frames 0..n-1 of d_hist left zeroed by mij_band_tables_async's k_band_bound
   int hist_zero_after = 0;  // set by run_entropy: the frames its k_tables_1w zeroed
   unsigned long long *d_bound_acc = nullptr;   // k_band_bound: {sum, arrivals}, left zeroed by its last workgroup
   // region batches (mij_batch_set_frame_dims / _gather_regions): per-frame
@@ -705,7 +706,7 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int se
                   bool stage_events = true) {
   // a token-emitting K1 (modes 2, 3, 6: the band calls too) adds onto d_hist:
   // the next encode must zero it again
-  if (mode & 2) b->hist_zero_n = 0;
+  if (mode & 2) b->hist_zero_n = b->band_hist_zero = 0;
   K1Args k;
   memset(&k, 0, sizeof(k));
   k.in = b->d_in;
@@ -803,6 +804,7 @@ static int run_k1(mij_batch *b, int nframes, int mode, int dc_diffed = 0, int se
 // structs are already in d_hc and d_ehuf (drop-in write_jpg).
 static int run_entropy(mij_batch *b, int nframes, bool dc_fix, bool tables_given, int f0 = 0,
                        hipStream_t st = nullptr) {
+  b->band_hist_zero = 0;  // (its segment DCs add onto d_hist)
   EntArgs a = ent_args(b, nframes, f0);
   const bool t = b->timing && !st;  // (sub-batches: no stage events)
   if (!st) st = b->stream;
@@ -1696,6 +1698,7 @@ extern "C" int mij_band_analyze(mij_batch *b, int n, int16_t *last_dc) {
 
 extern "C" int mij_band_histograms(mij_batch *b, int n, const int16_t *prev_dc, uint32_t *hist) {
   if (band_check(b, n, "band_histograms")) return g_err;
+  b->band_hist_zero = 0;
   if (!prev_dc || !hist) return fail(MIJ_EINVAL, "band_histograms: null argument");
   std::vector<int16_t> pred((size_t)n * 4, 0);
   for (int f = 0; f < n; f++)
@@ -1711,6 +1714,7 @@ extern "C" int mij_band_histograms(mij_batch *b, int n, const int16_t *prev_dc, 
 }
 
 static int upload_hist_tables(mij_batch *b, int n, const uint32_t *hist) {
+  b->band_hist_zero = 0;
   HIP_TRY(hipMemcpyAsync(b->d_hist, hist, sizeof(uint32_t) * n * 4 * 257, hipMemcpyHostToDevice,
                          b->stream));
   HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * n, b->stream));
@@ -1743,8 +1747,10 @@ static int ensure_pieces(mij_batch *b, size_t n) {
 extern "C" int mij_band_analyze_async(mij_batch *b, int n, int16_t *d_last) {
   if (band_check(b, n, "band_analyze_async")) return g_err;
   if (!d_last) return fail(MIJ_EINVAL, "band_analyze_async: null d_last");
-  HIP_TRY(hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * n * 4 * 257, b->stream));
-  HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int) * n, b->stream));
+  // (the last step's k_band_bound zeroed the histograms it read, and K1
+  // zeroes the error words: no fills on the band stream's critical path)
+  if (n > b->band_hist_zero) HIP_TRY(hipMemsetAsync(b->d_hist, 0, sizeof(uint32_t) * n * 4 * 257, b->stream));
+  b->k1_err_zero = n;
   if (run_k1(b, n, 2)) return g_err;
   HIP_TRY(launch_band_last(b->d_dc, b->g, n, d_last, b->stream));
   return MIJ_OK;
@@ -1752,6 +1758,7 @@ extern "C" int mij_band_analyze_async(mij_batch *b, int n, int16_t *d_last) {
 
 extern "C" int mij_band_histograms_async(mij_batch *b, int n, const int16_t *d_prev, uint32_t *d_hist) {
   if (band_check(b, n, "band_histograms_async")) return g_err;
+  b->band_hist_zero = 0;
   if (!d_hist) return fail(MIJ_EINVAL, "band_histograms_async: null d_hist");
   // the previous band's last DCs are read in place (null: band 0, zeros)
   EntArgs a = ent_args(b, n);
@@ -1776,6 +1783,7 @@ extern "C" int mij_band_tables_async(mij_batch *b, int n, const uint32_t *d_ghis
     HIP_TRY(hipMemsetAsync(b->d_bound_acc, 0, 2 * sizeof(unsigned long long), b->stream));
   }
   HIP_TRY(launch_band_bound(ent_args(b, n), b->d_bound_acc, (unsigned long long *)d_bound, b->stream));
+  b->band_hist_zero = n;  // (k_band_bound zeroes the band's histograms it reads)
   b->band_async_n = -n;  // tables built, not packed yet
   return MIJ_OK;
 }

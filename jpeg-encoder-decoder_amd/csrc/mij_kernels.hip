@@ -4261,8 +4261,10 @@ __global__ void k_band_assembly(const unsigned long long *allbits, int world, in
 // (hist[f][t][sym]) weighted by the tables' code lengths (ehuf, len << 16 |
 // code); the three scans' words round up at most 3 words more.  A wave per
 // frame; the workgroups' sums meet in acc = {sum, arrivals}, which the last
-// workgroup to arrive reads, writes to bound[0] and leaves zeroed.
-__global__ __launch_bounds__(256) void k_band_bound(const uint32_t *hist, const uint32_t *ehuf, int n,
+// workgroup to arrive reads, writes to bound[0] and leaves zeroed.  The
+// histograms are left zeroed (each count by the lane that read it) for the
+// band's next K1, which adds onto them.
+__global__ __launch_bounds__(256) void k_band_bound(uint32_t *hist, const uint32_t *ehuf, int n,
                                                     unsigned long long *acc, unsigned long long *bound,
                                                     unsigned long long *pack_state, long long nstate,
                                                     unsigned *pack_ticket) {
@@ -4277,13 +4279,15 @@ __global__ __launch_bounds__(256) void k_band_bound(const uint32_t *hist, const 
   if (f < n) {
     unsigned long long b = 0;
     for (int t = 0; t < 4; t++) {
-      const uint32_t *h = hist + ((long long)f * 4 + t) * 257;
+      uint32_t *h = hist + ((long long)f * 4 + t) * 257;
       const uint32_t *e = ehuf + ((long long)f * 4 + t) * 256;
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const int s = 64 * k + lane;
         b += (unsigned long long)h[s] * ((e[s] >> 16) + (s & 15));
+        h[s] = 0u;
       }
+      if (lane == 0) h[256] = 0u;
     }
     for (int off = 32; off; off >>= 1) b += __shfl_xor(b, off);
     words = (b + 31) / 32 + 3;
