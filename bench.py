@@ -204,6 +204,10 @@ def run_config4(args, world, rank, local, dist):
     # the root assembles on an assembler batch: tables, scan buffers and
     # outputs only (no whole-frame input, coefficient or token buffers)
     full = mijpeg.Batch(W, H, n, args.quality, device=gpu, assembler=True) if rank == 0 else None
+    for k, v in (o.split("=", 1) for o in args.opt):  # (A/B variants; the assembler's emission slots)
+        band.set_option(k, int(v))
+        if full is not None and k == "emit_slots":
+            full.set_option(k, int(v))
     if not on_dev:
         xch = sharding.TorchExchange(dist, dist_device(dist, local))
     elif backend == "gloo":

@@ -659,13 +659,15 @@ static EntArgs ent_args(mij_batch *b, int nframes, int f0 = 0, bool band = false
   // 48 on large batches at any quality (round 6 sweep on config 3,
   // scripts/emit_sweep.sh, profiles/r06/probe/emit_slots.txt: emit 0.146 ms
   // at 48 against 0.154-0.189 at 16-384 for Q=50, 0.383 against 0.401 at the
-  // former 192 for Q=90), 1536 on frames of 8 Mpixels and more (config 4: few
-  // scans of hundreds of chunks each), 192 otherwise (a single frame needs
-  // the width)
+  // former 192 for Q=90), about 4096 per launch on frames of 8 Mpixels and
+  // more (config 4: few scans of hundreds of chunks each; 1536 per frame for
+  // one or two frames, 512 for config 4's eight: its assembly 0.094-0.097 ms
+  // at 1536, 0.089 at 512, profiles/r06/probe/c4_emit_slots.txt), 192
+  // otherwise (a single frame needs the width)
   const int slots_opt = b->opt[MIJ_OPT_EMIT_SLOTS];
   a.emit_slots = slots_opt > 0                                 ? slots_opt
                  : nframes >= 43                               ? 48
-                 : ((long long)b->g.w * b->g.h >= (8 << 20))    ? 1536
+                 : ((long long)b->g.w * b->g.h >= (8 << 20))    ? std::max(192, std::min(1536, 4096 / nframes))
                                                                 : 192;
   a.pack_wide = ent_args_pack_wide(b);
   ent_args_pack_ls(b, nframes, a.pack_ls);
@@ -1207,7 +1209,8 @@ extern "C" int mij_batch_set_overlap(mij_batch *b, int nsub) {
 }
 
 extern "C" int mij_batch_set_option(mij_batch *b, int opt, int value) {
-  if (pipe_check(b, "set_option")) return g_err;
+  // (an assembler emits the frames: its emission slots are its one option)
+  if (!(b && b->assembler && opt == MIJ_OPT_EMIT_SLOTS) && pipe_check(b, "set_option")) return g_err;
   if (opt < 0 || opt >= MIJ_OPT_COUNT) return fail(MIJ_EINVAL, "set_option: unknown option %d", opt);
   if (opt == OPT_TEST_FAULT_TICKET) return fail(MIJ_EINVAL, "set_option: unknown option %d", opt);
   const bool binary = opt != MIJ_OPT_PACK_WIDE && opt != MIJ_OPT_EMIT_SLOTS && opt != MIJ_OPT_PACK_SEGS;
