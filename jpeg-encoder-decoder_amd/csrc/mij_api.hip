@@ -308,7 +308,9 @@ static void fill_tables(int quality, Tables *t) {
 // ---------------------------------------------------------------------------
 struct mij_batch {
   int dev = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // where the batch enqueues: its own, or the caller's (mij_batch_set_stream)
+  hipStream_t own_stream = nullptr;
+  hipEvent_t ev_switch = nullptr;  // orders a stream switch after the work before it
   Geom g;
   int cap = 0, quality = 50;
   Tables *d_tab = nullptr;
@@ -392,7 +394,8 @@ static hipError_t dalloc(T **p, size_t count) {
 static void batch_free(mij_batch *b) {
   if (!b) return;
   hipSetDevice(b->dev);
-  if (b->stream) hipStreamSynchronize(b->stream);
+  if (b->stream && b->stream != b->own_stream) hipStreamSynchronize(b->stream);
+  if (b->own_stream) hipStreamSynchronize(b->own_stream);
   void *ptrs[] = {b->d_tab, b->own_in ? b->d_in : nullptr, b->d_coef, b->d_dc, b->d_hist,
                   b->d_ehuf, b->d_raw, b->d_tok, b->d_tok0, b->d_seg_ntok, b->d_seg_bits, b->d_seg_off,
                   b->d_scan_bits, b->d_out_len, b->d_hc, b->d_out, b->d_err, b->d_replays,
@@ -411,7 +414,8 @@ static void batch_free(mij_batch *b) {
     hipStreamSynchronize(b->stream2);
     hipStreamDestroy(b->stream2);
   }
-  if (b->stream) hipStreamDestroy(b->stream);
+  if (b->ev_switch) hipEventDestroy(b->ev_switch);
+  if (b->own_stream) hipStreamDestroy(b->own_stream);
   delete b;
 }
 
@@ -429,6 +433,7 @@ static int batch_init(mij_batch *b, int device, int w, int h, int frames, int qu
   b->assembler = assembler;
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+  b->own_stream = b->stream;
   b->g = make_geom(w, h);
   b->cap = frames;
   b->quality = quality;
@@ -536,6 +541,19 @@ static int pipe_check(const mij_batch *b, const char *what) {
 extern "C" void mij_batch_destroy(mij_batch *b) { batch_free(b); }
 
 extern "C" void *mij_batch_stream(mij_batch *b) { return b ? (void *)b->stream : nullptr; }
+
+extern "C" int mij_batch_set_stream(mij_batch *b, void *stream) {
+  if (!b) return fail(MIJ_EINVAL, "set_stream: null batch");
+  HIP_TRY(hipSetDevice(b->dev));
+  const hipStream_t s = stream ? (hipStream_t)stream : b->own_stream;
+  if (s == b->stream) return MIJ_OK;
+  // the new stream runs after everything enqueued so far on the old one
+  if (!b->ev_switch) HIP_TRY(hipEventCreateWithFlags(&b->ev_switch, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(b->ev_switch, b->stream));
+  HIP_TRY(hipStreamWaitEvent(s, b->ev_switch, 0));
+  b->stream = s;
+  return MIJ_OK;
+}
 
 // slots first..first+n-1 hold canvas-sized frames again; a region batch
 // whose slots are then all canvas-sized is a plain batch

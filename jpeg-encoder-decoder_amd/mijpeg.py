@@ -24,7 +24,7 @@ EXPORTS = [
     "mij_batch_create", "mij_batch_destroy", "mij_batch_upload", "mij_batch_set_input",
     "mij_batch_encode", "mij_batch_keep_coefs", "mij_batch_set_split", "mij_batch_set_overlap", "mij_batch_set_option", "mij_batch_get_option", "mij_batch_dct", "mij_batch_pattern_floor", "mij_batch_sync", "mij_batch_output",
     "mij_batch_lengths", "mij_batch_coefs", "mij_batch_tables", "mij_batch_set_timing",
-    "mij_batch_stage_ms", "mij_batch_stage_history", "mij_batch_token_count", "mij_batch_geometry", "mij_batch_replays", "mij_batch_stream", "mij_batch_audit", "mij_batch_build_tables",
+    "mij_batch_stage_ms", "mij_batch_stage_history", "mij_batch_token_count", "mij_batch_geometry", "mij_batch_replays", "mij_batch_stream", "mij_batch_set_stream", "mij_batch_audit", "mij_batch_build_tables",
     "mij_band_analyze", "mij_band_histograms", "mij_band_tables", "mij_band_pack", "mij_band_words",
     "mij_assemble_begin", "mij_assemble_words", "mij_assemble_end",
     "mij_band_words_all", "mij_assemble_pieces", "mij_assembler_create",
@@ -143,6 +143,7 @@ def load() -> C.CDLL:
     lib.mij_batch_replays.argtypes = [p]
     lib.mij_batch_stream.restype = p
     lib.mij_batch_stream.argtypes = [p]
+    lib.mij_batch_set_stream.argtypes = [p, p]
     u64 = C.c_ulonglong
     lib.mij_band_analyze.argtypes = [p, i, p]
     lib.mij_band_histograms.argtypes = [p, i, p, p]
@@ -546,6 +547,11 @@ class Batch:
     def stream_ptr(self) -> int:
         """the batch's HIP stream (hipStream_t), for torch.cuda.ExternalStream"""
         return int(self.lib.mij_batch_stream(self.h_) or 0)
+
+    def set_stream(self, stream_ptr: int) -> None:
+        """enqueue on another HIP stream from now on (0: the batch's own);
+        ordered after the work enqueued before (mij_batch_set_stream)"""
+        _check(self.lib.mij_batch_set_stream(self.h_, stream_ptr or None), "set_stream")
 
     def band_analyze_async(self, n: int, d_last: int) -> None:
         _check(self.lib.mij_band_analyze_async(self.h_, n, d_last), "band_analyze_async")

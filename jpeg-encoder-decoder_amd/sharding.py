@@ -318,6 +318,9 @@ class StagedExchange(DeviceExchange):
 # MIJ_HOST_READ=default: the host reads' copies on torch's default stream
 # (rounds 4-6, kept for A/B) instead of the band batch's stream
 _HOST_READ_DEFAULT = os.environ.get("MIJ_HOST_READ", "batch") == "default"
+# MIJ_ASSEMBLE_STREAM=own: the root's assembly on the assembler's own stream
+# behind cross-queue waits (rounds 4-6, kept for A/B)
+_ASSEMBLE_OWN_STREAM = os.environ.get("MIJ_ASSEMBLE_STREAM", "band") == "own"
 
 
 def _to_host(band, s, h, d_src, dev):
@@ -441,13 +444,28 @@ def encode_banded_dev(band, n: int, xch, frame_batch=None, events=None, emit: st
             mark("words")
             if a is None:
                 return
-    a.wait_stream(s)
-    with torch.cuda.stream(a):
-        if emit == "bands":
-            frame_batch.assemble_stuffed_async(n, allrec.data_ptr(), world, gathered.data_ptr(), stride)
-        else:
-            frame_batch.assemble_async(n, allbits.data_ptr(), world, gathered.data_ptr(), stride)
-    # the tensors read by the assembly are freed on the band stream: keep that
-    # stream behind the assembly
-    s.wait_stream(a)
+    # the assembly runs on the band stream itself (after the root's tables on
+    # its own stream: mij_batch_set_stream orders the switch), so the word
+    # move, the assembly and the next step's K1 follow each other in one
+    # queue -- a cross-queue wait costs ~13 us each way on config 4
+    # (profiles/r06/probe/c4_trace/); the tensors it reads are freed on that
+    # stream too
+    if _ASSEMBLE_OWN_STREAM:
+        a.wait_stream(s)
+        with torch.cuda.stream(a):
+            _assemble(frame_batch, emit, n, allbits, allrec if emit == "bands" else None, world, gathered, stride)
+        s.wait_stream(a)
+    else:
+        frame_batch.set_stream(band.stream_ptr())
+        try:
+            _assemble(frame_batch, emit, n, allbits, allrec if emit == "bands" else None, world, gathered, stride)
+        finally:
+            frame_batch.set_stream(0)
     mark("assemble")
+
+
+def _assemble(frame_batch, emit, n, allbits, allrec, world, gathered, stride):
+    if emit == "bands":
+        frame_batch.assemble_stuffed_async(n, allrec.data_ptr(), world, gathered.data_ptr(), stride)
+    else:
+        frame_batch.assemble_async(n, allbits.data_ptr(), world, gathered.data_ptr(), stride)
