@@ -3711,8 +3711,10 @@ __global__ __launch_bounds__(256) void k_emit_scan(EntArgs a) {
 // share their wait instead of preceding them).  after_load(w) runs once per
 // loaded word, after the load (k_emit_write zeroes the scan word there).
 // Called by a whole 256-thread workgroup; s_out: 2 * EMIT_CH bytes, red: 4
-// ints of LDS.
-template <class WordFn, class AfterFn, class MetaFn>
+// ints of LDS.  DIRECT: every word's bytes go straight to out (a word without
+// 0xFF bytes by one unaligned dword store, the rest byte by byte); s_out is
+// not used.
+template <bool DIRECT = false, class WordFn, class AfterFn, class MetaFn>
 __device__ __forceinline__ void stuff_chunk(const WordFn &word, const AfterFn &after_load, const MetaFn &meta,
                                             unsigned long long nbytes, unsigned long long cb, uint8_t *out,
                                             uint8_t *s_out, int *red) {
@@ -3757,7 +3759,18 @@ __device__ __forceinline__ void stuff_chunk(const WordFn &word, const AfterFn &a
     const int incl = (int)wave_scan64((uint32_t)(lim + cf));
     int op = carry + incl - (lim + cf);
     carry += __shfl(incl, 63);
-    if (cf == 0) {
+    if (DIRECT) {
+      uint8_t *d = out + o0;
+      if (cf == 0 && lim == 4) {
+        *(uint32_t *)(d + op) = __builtin_bswap32(wd);  // (unaligned: the hardware's unaligned mode)
+      } else {
+        for (int j = 0; j < lim; j++) {
+          const uint8_t byte = (uint8_t)(wd >> (24 - 8 * j));
+          d[op++] = byte;
+          if (byte == 0xFF) d[op++] = 0x00;
+        }
+      }
+    } else if (cf == 0) {
 #pragma unroll
       for (int j = 0; j < 4; j++)
         if (j < lim) s_out[op + j] = (uint8_t)(wd >> (24 - 8 * j));
@@ -3769,7 +3782,8 @@ __device__ __forceinline__ void stuff_chunk(const WordFn &word, const AfterFn &a
       }
     }
   }
-  __syncthreads();
+  __syncthreads();  // (DIRECT: before the next chunk's wave totals overwrite red)
+  if (DIRECT) return;
   // copy out: head bytes up to a 4-byte boundary, whole words (re-aligned
   // from LDS words with v_alignbyte), tail bytes; every byte of
   // [o0, o0 + clen) belongs to this chunk alone
@@ -3792,7 +3806,10 @@ __device__ __forceinline__ void stuff_chunk(const WordFn &word, const AfterFn &a
 
 // k_emit_write: the stuffed bytes of every chunk at the offset k_emit_scan gave.
 __global__ __launch_bounds__(256) void k_emit_write(EntArgs a) {
-  __shared__ uint8_t s_out[2 * EMIT_CH];
+  // (no LDS staging: each word's bytes go straight to the output, round 6:
+  // emit 0.142 -> 0.111 ms at Q=50, 0.390 -> 0.315 at Q=90)
+  constexpr bool DIRECT = true;
+  uint8_t *s_out = nullptr;
   __shared__ int red[4];
   const int slot = blockIdx.x % a.emit_slots, f = blockIdx.x / a.emit_slots;
   const int tid = threadIdx.x;
@@ -3830,7 +3847,7 @@ __global__ __launch_bounds__(256) void k_emit_write(EntArgs a) {
     const unsigned long long nbytes = comp == 0 ? nbs[0] : (comp == 1 ? nbs[1] : nbs[2]);
     uint32_t *raw = (uint32_t *)scan_raw(a, f, comp);
     const long long ci = (long long)(f * 3 + comp) * nchmax + c;
-    stuff_chunk([&](unsigned long long w) { return raw[w]; },
+    stuff_chunk<DIRECT>([&](unsigned long long w) { return raw[w]; },
                 [&](unsigned long long w) {
                   if (zero) raw[w] = 0u;
                 },
