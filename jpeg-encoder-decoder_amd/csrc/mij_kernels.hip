@@ -3991,7 +3991,7 @@ __global__ __launch_bounds__(256) void k_band_count_ff(EntArgs a) {
 // band's buffer, cap bytes: a chunk that would end past it is not written,
 // and the counts say so to the caller via the total)
 __global__ __launch_bounds__(256) void k_band_write(EntArgs a, uint8_t *dst, unsigned long long cap) {
-  __shared__ uint8_t s_out[2 * EMIT_CH];
+  uint8_t *s_out = nullptr;  // (stuff_chunk<true>: straight to dst, as k_emit_write)
   __shared__ int red[4];
   const int slot = blockIdx.x % a.emit_slots, f = blockIdx.x / a.emit_slots;
   const long long nchmax = emit_chunks(a.g);
@@ -4009,7 +4009,7 @@ __global__ __launch_bounds__(256) void k_band_write(EntArgs a, uint8_t *dst, uns
     const unsigned long long o0 = a.scan_base[f * 3 + comp] + a.choff[ci];
     const unsigned long long clen = min((unsigned long long)EMIT_CH, nbytes - (unsigned long long)c * EMIT_CH) + tot;
     if (o0 + clen <= cap)  // (workgroup-uniform)
-      stuff_chunk([&](unsigned long long w) { return shifted_word(raw, w, h); }, [](unsigned long long) {},
+      stuff_chunk<true>([&](unsigned long long w) { return shifted_word(raw, w, h); }, [](unsigned long long) {},
                   [&](unsigned long long &o, int &t) {
                     o = o0;
                     t = tot;
